@@ -1,0 +1,827 @@
+// hakai_capi.cpp -- C ABI of libhakai_hip.so (declared in include/hakai_hip.h).
+//
+// Owns the persistent device context: model, Gauss-point state in SoA, ping-pong displacement
+// buffers, the node->element incidence CSR used for the deterministic force gather, BC tables,
+// deletion log and per-kernel HIP-event timers. One HIP stream per context.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hakai_hip.h"
+#include "hakai_internal.hpp"
+#include "hakai_kernels.hpp"
+
+using hk::DevMat;
+
+namespace {
+thread_local std::string g_err;
+}
+
+namespace hkc {
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(HAKAI_ERR_DEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+}  // namespace hkc
+
+using hkc::fail;
+using hkc::hip_fail;
+
+#define HIPCHK(x)                                           \
+    do {                                                    \
+        hipError_t _e = (x);                                \
+        if (_e != hipSuccess) return hip_fail(_e, #x);      \
+    } while (0)
+
+template <class T>
+static hipError_t dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc((void**)p, n * sizeof(T));
+}
+
+template <class T>
+static void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+namespace hkc {
+
+static void free_model(hakai_ctx* c) {
+    dfree(c->d_coord);
+    dfree(c->d_u[0]);
+    dfree(c->d_u[1]);
+    dfree(c->d_mass);
+    dfree(c->d_conn);
+    dfree(c->d_flag);
+    dfree(c->d_mat);
+    dfree(c->d_mats);
+    dfree(c->d_stress);
+    dfree(c->d_strain);
+    dfree(c->d_eqps);
+    dfree(c->d_yield);
+    dfree(c->d_triax);
+    dfree(c->d_fe);
+    dfree(c->d_inc_ptr);
+    dfree(c->d_inc);
+    dfree(c->d_qbuf);
+    dfree(c->d_fext);
+    c->model_ok = false;
+    c->state_ok = false;
+}
+
+static void free_bc(hakai_ctx* c) {
+    dfree(c->d_bc_dof);
+    dfree(c->d_bc_grp);
+    dfree(c->d_bc_val);
+    dfree(c->d_amp_n);
+    dfree(c->d_amp_off);
+    dfree(c->d_amp_t);
+    dfree(c->d_amp_v);
+    c->nbc = 0;
+}
+
+// Material constants exactly as hakai() derives them (v2/HAKAI_j.jl:143-160) and readInpFile
+// builds Hd (v2/readInpFile_j.jl:763-768).
+int build_devmat(const hakai_material_t& in, DevMat& o) {
+    std::memset(&o, 0, sizeof o);
+    const double young = in.young, poisson = in.poisson;
+    const double d1 = (1.0 - poisson), d2 = poisson, d3 = (1.0 - 2.0 * poisson) / 2.0;
+    const double cc = young / (1.0 + poisson) / (1.0 - 2.0 * poisson);
+    o.Dn = cc * d1;
+    o.Do = cc * d2;
+    o.Ds = cc * d3;
+    o.G = young / 2. / (1.0 + poisson);
+    o.density = in.density;
+    if (in.n_plastic < 0 || in.n_plastic > hk::kMaxPlastic)
+        return fail(HAKAI_ERR_ARG, "material: %d plastic rows (max %d)", in.n_plastic, hk::kMaxPlastic);
+    if (in.n_ductile < 0 || in.n_ductile > hk::kMaxDuctile)
+        return fail(HAKAI_ERR_ARG, "material: %d ductile rows (max %d)", in.n_ductile, hk::kMaxDuctile);
+    if (in.n_plastic == 1)
+        return fail(HAKAI_ERR_MODEL,
+                    "material: a single *Plastic row gives an empty Hd; the reference raises BoundsError "
+                    "(v2/HAKAI_j.jl:1267)");
+    o.npp = in.n_plastic;
+    o.nd = in.n_ductile;
+    o.yield0 = in.n_plastic > 0 ? in.plastic[0] : 0.0;
+    for (int r = 0; r < in.n_plastic; ++r) o.pl_eps[r] = in.plastic[2 * r + 1];
+    for (int r = 0; r + 1 < in.n_plastic; ++r)
+        o.Hd[r] = (in.plastic[2 * (r + 1)] - in.plastic[2 * r]) / (in.plastic[2 * (r + 1) + 1] - in.plastic[2 * r + 1]);
+    for (int r = 0; r < in.n_ductile; ++r) {
+        o.du_eps[r] = in.ductile[3 * r + 0];
+        o.du_tri[r] = in.ductile[3 * r + 1];
+    }
+    return 0;
+}
+
+hipStream_t ctx_stream(hakai_ctx* c) { return c->stream; }
+int ctx_device(hakai_ctx* c) { return c->device; }
+
+}  // namespace hkc
+
+// ---------------------------------------------------------------------------------------------
+// profiling
+// ---------------------------------------------------------------------------------------------
+static void prof_harvest(hakai_ctx* c) {
+    if (c->ev_pending.empty()) return;
+    (void)hipEventSynchronize(c->ev_pending.back().b);
+    for (auto& p : c->ev_pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->k_ms[p.kernel] += ms;
+            c->k_n[p.kernel] += 1;
+        }
+        c->ev_pool.push_back(p.a);
+        c->ev_pool.push_back(p.b);
+    }
+    c->ev_pending.clear();
+}
+
+static hipEvent_t prof_event(hakai_ctx* c) {
+    if (c->ev_pool.empty()) {
+        if (c->ev_pending.size() >= 2048) prof_harvest(c);
+        if (c->ev_pool.empty()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            return e;
+        }
+    }
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+}
+
+namespace hkc {
+void prof_begin(hakai_ctx* c, int kernel, EventPair* p) {
+    if (!c->prof) return;
+    p->kernel = kernel;
+    p->a = prof_event(c);
+    p->b = prof_event(c);
+    (void)hipEventRecord(p->a, c->stream);
+}
+void prof_end(hakai_ctx* c, EventPair* p) {
+    if (!c->prof) return;
+    (void)hipEventRecord(p->b, c->stream);
+    c->ev_pending.push_back(*p);
+}
+}  // namespace hkc
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int hakai_abi_version(void) { return HAKAI_ABI_VERSION; }
+const char* hakai_last_error(void) { return g_err.c_str(); }
+
+int hakai_device_count(int* n) {
+    if (!n) return fail(HAKAI_ERR_ARG, "null");
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess) cnt = 0;
+    *n = cnt;
+    return 0;
+}
+
+int hakai_create(hakai_ctx** out, int device) {
+    if (!out) return fail(HAKAI_ERR_ARG, "null ctx pointer");
+    *out = nullptr;
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
+        return fail(HAKAI_ERR_DEVICE, "no HIP device visible: the HAKAI MI355X path has no CPU fallback");
+    if (device < 0 || device >= cnt) return fail(HAKAI_ERR_ARG, "device %d out of range (%d visible)", device, cnt);
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(HAKAI_ERR_DEVICE, "device %d is %s; libhakai_hip is built for gfx950 only", device,
+                    prop.gcnArchName);
+    hakai_ctx* c = new hakai_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    if (dalloc(&c->d_del_count, 1) != hipSuccess || dalloc(&c->d_del_log, 2 * (size_t)c->del_cap) != hipSuccess ||
+        dalloc(&c->d_negjac, 1) != hipSuccess) {
+        delete c;
+        return fail(HAKAI_ERR_DEVICE, "hipMalloc for context bookkeeping failed");
+    }
+    (void)hipMemsetAsync(c->d_del_count, 0, sizeof(int), c->stream);
+    (void)hipMemsetAsync(c->d_negjac, 0, sizeof(unsigned long long), c->stream);
+    *out = c;
+    return 0;
+}
+
+int hakai_destroy(hakai_ctx* c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    prof_harvest(c);
+    hkc::comm_destroy(c);
+    hkc::free_model(c);
+    hkc::free_bc(c);
+    dfree(c->d_del_count);
+    dfree(c->d_del_log);
+    dfree(c->d_negjac);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int64_t nElement,
+                       const int64_t* elementmat, const int64_t* element_material, int32_t nMat,
+                       const hakai_material_t* mats, const double* diag_M) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null ctx");
+    if (nNode <= 0 || nElement < 0 || !coordmat || (nElement > 0 && (!elementmat || !element_material)) || nMat <= 0 ||
+        !mats || !diag_M)
+        return fail(HAKAI_ERR_ARG, "upload_model: bad arguments");
+    if (8 * nElement >= (int64_t)INT32_MAX || nNode >= (int64_t)INT32_MAX)
+        return fail(HAKAI_ERR_ARG, "upload_model: mesh too large for int32 indexing on one rank");
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipStreamSynchronize(c->stream);
+    hkc::free_model(c);
+    const long long nN = nNode, nE = nElement;
+    // host-side conversions
+    std::vector<int> conn((size_t)(8 * nE)), mat((size_t)nE);
+    for (long long e = 0; e < nE; ++e) {
+        for (int i = 0; i < 8; ++i) {
+            const int64_t n = elementmat[8 * e + i];
+            if (n < 1 || n > nN) return fail(HAKAI_ERR_ARG, "elementmat[%d,%lld] = %lld out of 1..%lld", i + 1, e + 1, (long long)n, nN);
+            conn[8 * e + i] = (int)(n - 1);
+        }
+        const int64_t m = element_material[e];
+        if (m < 1 || m > nMat) return fail(HAKAI_ERR_ARG, "element_material[%lld] = %lld out of 1..%d", e + 1, (long long)m, nMat);
+        mat[e] = (int)(m - 1);
+    }
+    std::vector<double> mass((size_t)nN);
+    for (long long n = 0; n < nN; ++n) {
+        const double m0 = diag_M[3 * n], m1 = diag_M[3 * n + 1], m2 = diag_M[3 * n + 2];
+        if (!(m0 == m1 && m1 == m2))
+            return fail(HAKAI_ERR_ARG, "diag_M: node %lld has different masses per dof", n + 1);
+        mass[n] = m0;
+    }
+    c->h_mats.assign((size_t)nMat, DevMat());
+    c->has_ductile = false;
+    for (int i = 0; i < nMat; ++i) {
+        int r = hkc::build_devmat(mats[i], c->h_mats[i]);
+        if (r) return r;
+    }
+    for (long long e = 0; e < nE; ++e)
+        if (c->h_mats[mat[e]].nd > 0) c->has_ductile = true;
+    // node -> (8e+i) incidence CSR in ascending element order (counting sort keeps the order)
+    std::vector<int> ptr((size_t)nN + 1, 0), inc((size_t)(8 * nE));
+    for (long long j = 0; j < 8 * nE; ++j) ptr[conn[j] + 1]++;
+    for (long long n = 0; n < nN; ++n) ptr[n + 1] += ptr[n];
+    {
+        std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+        for (long long j = 0; j < 8 * nE; ++j) inc[fill[conn[j]]++] = (int)j;
+    }
+    c->nN = nN;
+    c->nE = nE;
+    c->ld = ((8 * nE + 63) / 64) * 64;
+    const size_t ld = (size_t)c->ld;
+    HIPCHK(dalloc(&c->d_coord, 3 * (size_t)nN));
+    HIPCHK(dalloc(&c->d_u[0], 3 * (size_t)nN));
+    HIPCHK(dalloc(&c->d_u[1], 3 * (size_t)nN));
+    HIPCHK(dalloc(&c->d_mass, (size_t)nN));
+    HIPCHK(dalloc(&c->d_conn, 8 * (size_t)nE));
+    HIPCHK(dalloc(&c->d_flag, (size_t)nE));
+    HIPCHK(dalloc(&c->d_mat, (size_t)nE));
+    HIPCHK(dalloc(&c->d_mats, (size_t)nMat));
+    HIPCHK(dalloc(&c->d_stress, 6 * ld));
+    HIPCHK(dalloc(&c->d_strain, 6 * ld));
+    HIPCHK(dalloc(&c->d_eqps, ld));
+    HIPCHK(dalloc(&c->d_yield, ld));
+    HIPCHK(dalloc(&c->d_triax, ld));
+    HIPCHK(dalloc(&c->d_fe, 24 * (size_t)nE));
+    HIPCHK(dalloc(&c->d_inc_ptr, (size_t)nN + 1));
+    HIPCHK(dalloc(&c->d_inc, 8 * (size_t)nE));
+    HIPCHK(dalloc(&c->d_qbuf, 3 * (size_t)nN));
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemcpyAsync(c->d_coord, coordmat, 3 * nN * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_mass, mass.data(), nN * sizeof(double), hipMemcpyHostToDevice, s));
+    if (nE) {
+        HIPCHK(hipMemcpyAsync(c->d_conn, conn.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_mat, mat.data(), nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_inc, inc.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(c->d_mats, c->h_mats.data(), nMat * sizeof(DevMat), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_inc_ptr, ptr.data(), (nN + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // host vectors go out of scope
+    c->model_ok = true;
+    c->state_ok = false;
+    return hakai_reset_state(c, 0, nullptr, nullptr, 1.0);
+}
+
+int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
+    if (!c || !bc) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_bc before upload_model");
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipStreamSynchronize(c->stream);
+    hkc::free_bc(c);
+    const int G = bc->n_groups;
+    if (G <= 0) return 0;
+    // Resolve in-order overwrites: final writer of each dof (v2/HAKAI_j.jl:585-617).
+    std::map<long long, std::pair<int, double>> last;
+    for (int g = 0; g < G; ++g) {
+        if (bc->amp_n[g] == 1)
+            return fail(HAKAI_ERR_MODEL, "BC group %d: one-point amplitude, the reference raises BoundsError (:598)", g + 1);
+        for (int64_t en = bc->entry_off[g]; en < bc->entry_off[g + 1]; ++en)
+            for (int64_t d = bc->dof_off[en]; d < bc->dof_off[en + 1]; ++d) {
+                const int64_t dof = bc->dofs[d];
+                if (dof < 1 || dof > 3 * c->nN) return fail(HAKAI_ERR_ARG, "BC dof %lld out of range", (long long)dof);
+                last[dof - 1] = std::make_pair(g, bc->entry_value[en]);
+            }
+    }
+    std::vector<int> dof, grp;
+    std::vector<double> val;
+    for (auto& kv : last) {
+        dof.push_back((int)kv.first);
+        grp.push_back(kv.second.first);
+        val.push_back(kv.second.second);
+    }
+    std::vector<int> amp_n(G), amp_off(G);
+    long long n_amp = 0;
+    for (int g = 0; g < G; ++g) {
+        amp_n[g] = bc->amp_n[g];
+        amp_off[g] = (int)bc->amp_off[g];
+        n_amp = std::max<long long>(n_amp, bc->amp_off[g] + bc->amp_n[g]);
+    }
+    c->nbc = (int)dof.size();
+    HIPCHK(dalloc(&c->d_bc_dof, dof.size()));
+    HIPCHK(dalloc(&c->d_bc_grp, grp.size()));
+    HIPCHK(dalloc(&c->d_bc_val, val.size()));
+    HIPCHK(dalloc(&c->d_amp_n, (size_t)G));
+    HIPCHK(dalloc(&c->d_amp_off, (size_t)G));
+    HIPCHK(dalloc(&c->d_amp_t, (size_t)n_amp));
+    HIPCHK(dalloc(&c->d_amp_v, (size_t)n_amp));
+    hipStream_t s = c->stream;
+    if (!dof.empty()) {
+        HIPCHK(hipMemcpyAsync(c->d_bc_dof, dof.data(), dof.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_bc_grp, grp.data(), grp.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_bc_val, val.data(), val.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(c->d_amp_n, amp_n.data(), G * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_amp_off, amp_off.data(), G * sizeof(int), hipMemcpyHostToDevice, s));
+    if (n_amp) {
+        HIPCHK(hipMemcpyAsync(c->d_amp_t, bc->amp_time, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_amp_v, bc->amp_value, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const double* ic_values, double d_time) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "reset_state before upload_model");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t fn = 3 * (size_t)c->nN;
+    c->cur = 0;
+    HIPCHK(hipMemsetAsync(c->d_u[0], 0, fn * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(c->d_u[1], 0, fn * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(c->d_fe, 0, 24 * (size_t)c->nE * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(c->d_del_count, 0, sizeof(int), s));
+    HIPCHK(hipMemsetAsync(c->d_negjac, 0, sizeof(unsigned long long), s));
+    HIPCHK(hk::launch_reset_gp(c->d_stress, c->d_strain, c->d_eqps, c->d_yield, c->d_triax, c->d_flag, c->d_mat,
+                               c->d_mats, c->nE, c->ld, s));
+    c->h_velo0.assign(fn, 0.0);
+    c->q_from_buf = false;
+    c->steps_done = 0;
+    hkc::comm_reset(c);
+    if (n_ic > 0) {
+        if (!ic_dofs || !ic_values) return fail(HAKAI_ERR_ARG, "reset_state: null IC arrays");
+        std::vector<double> dpre(fn, 0.0);
+        for (int64_t j = 0; j < n_ic; ++j) {  // v2/HAKAI_j.jl:233-239
+            const int64_t d = ic_dofs[j];
+            if (d < 1 || d > (int64_t)fn) return fail(HAKAI_ERR_ARG, "IC dof %lld out of range", (long long)d);
+            dpre[d - 1] = -ic_values[j] * d_time;
+            c->h_velo0[d - 1] = ic_values[j];
+        }
+        HIPCHK(hipMemcpyAsync(c->d_u[1 - c->cur], dpre.data(), fn * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    c->state_ok = true;
+    return 0;
+}
+
+int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
+    if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "upload_state before upload_model");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t fn = 3 * (size_t)c->nN, nGP = 8 * (size_t)c->nE;
+    if (st->disp) HIPCHK(hipMemcpyAsync(c->d_u[c->cur], st->disp, fn * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->disp_pre)
+        HIPCHK(hipMemcpyAsync(c->d_u[1 - c->cur], st->disp_pre, fn * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->velo) c->h_velo0.assign(st->velo, st->velo + fn);
+    if (st->Q) {
+        HIPCHK(hipMemcpyAsync(c->d_qbuf, st->Q, fn * sizeof(double), hipMemcpyHostToDevice, s));
+        c->q_from_buf = true;
+    }
+    if (st->integ_stress || st->integ_strain) {
+        double* tmp = nullptr;
+        HIPCHK(dalloc(&tmp, 6 * nGP));
+        if (st->integ_stress) {
+            HIPCHK(hipMemcpyAsync(tmp, st->integ_stress, 6 * nGP * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hk::launch_aos_to_soa6(tmp, c->d_stress, (long long)nGP, c->ld, s));
+        }
+        if (st->integ_strain) {
+            HIPCHK(hipMemcpyAsync(tmp, st->integ_strain, 6 * nGP * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hk::launch_aos_to_soa6(tmp, c->d_strain, (long long)nGP, c->ld, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        dfree(tmp);
+    }
+    if (st->integ_yield_stress)
+        HIPCHK(hipMemcpyAsync(c->d_yield, st->integ_yield_stress, nGP * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->integ_eq_plastic_strain)
+        HIPCHK(hipMemcpyAsync(c->d_eqps, st->integ_eq_plastic_strain, nGP * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->integ_triax_stress)
+        HIPCHK(hipMemcpyAsync(c->d_triax, st->integ_triax_stress, nGP * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->element_flag) {
+        std::vector<int> f((size_t)c->nE);
+        for (long long e = 0; e < c->nE; ++e) f[e] = st->element_flag[e] != 0 ? 1 : 0;
+        HIPCHK(hipMemcpyAsync(c->d_flag, f.data(), c->nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        // fe of elements uploaded as deleted must not contribute
+        std::vector<double> z;
+        for (long long e = 0; e < c->nE; ++e)
+            if (!f[e]) {
+                if (z.empty()) z.assign(24, 0.0);
+                HIPCHK(hipMemcpyAsync(c->d_fe + 24 * e, z.data(), 24 * sizeof(double), hipMemcpyHostToDevice, s));
+            }
+    }
+    if (st->Qe) HIPCHK(hipMemcpyAsync(c->d_fe, st->Qe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->steps_done = 0;
+    hkc::comm_reset(c);
+    c->state_ok = true;
+    return 0;
+}
+
+int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
+    if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->state_ok) return fail(HAKAI_ERR_STATE, "download_state without state");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t fn = 3 * (size_t)c->nN, nGP = 8 * (size_t)c->nE;
+    HIPCHK(hipStreamSynchronize(s));
+    if (st->disp) HIPCHK(hipMemcpyAsync(st->disp, c->d_u[c->cur], fn * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->disp_pre)
+        HIPCHK(hipMemcpyAsync(st->disp_pre, c->d_u[1 - c->cur], fn * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->velo) {
+        if (c->steps_done == 0) {
+            std::memcpy(st->velo, c->h_velo0.data(), fn * sizeof(double));
+        } else {  // velo = d_disp / d_time with d_disp = disp_new - disp (v2/HAKAI_j.jl:625-628)
+            std::vector<double> a(fn), b(fn);
+            HIPCHK(hipMemcpyAsync(a.data(), c->d_u[c->cur], fn * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(b.data(), c->d_u[1 - c->cur], fn * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (size_t i = 0; i < fn; ++i) {
+                const double dd = a[i] - b[i];
+                st->velo[i] = dd / c->last_dt;
+            }
+        }
+    }
+    if (st->Q) {
+        if (c->q_from_buf) {
+            HIPCHK(hipMemcpyAsync(st->Q, c->d_qbuf, fn * sizeof(double), hipMemcpyDeviceToHost, s));
+        } else {
+            double* tmp = nullptr;
+            HIPCHK(dalloc(&tmp, fn));
+            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, tmp, c->nN, s));
+            HIPCHK(hipMemcpyAsync(st->Q, tmp, fn * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            dfree(tmp);
+        }
+    }
+    if (st->integ_stress || st->integ_strain) {
+        double* tmp = nullptr;
+        HIPCHK(dalloc(&tmp, 6 * nGP));
+        if (st->integ_stress) {
+            HIPCHK(hk::launch_soa_to_aos6(c->d_stress, tmp, (long long)nGP, c->ld, s));
+            HIPCHK(hipMemcpyAsync(st->integ_stress, tmp, 6 * nGP * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        if (st->integ_strain) {
+            HIPCHK(hk::launch_soa_to_aos6(c->d_strain, tmp, (long long)nGP, c->ld, s));
+            HIPCHK(hipMemcpyAsync(st->integ_strain, tmp, 6 * nGP * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        dfree(tmp);
+    }
+    if (st->integ_yield_stress)
+        HIPCHK(hipMemcpyAsync(st->integ_yield_stress, c->d_yield, nGP * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->integ_eq_plastic_strain)
+        HIPCHK(hipMemcpyAsync(st->integ_eq_plastic_strain, c->d_eqps, nGP * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->integ_triax_stress)
+        HIPCHK(hipMemcpyAsync(st->integ_triax_stress, c->d_triax, nGP * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->element_flag) {
+        std::vector<int> f((size_t)c->nE);
+        HIPCHK(hipMemcpyAsync(f.data(), c->d_flag, c->nE * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (long long e = 0; e < c->nE; ++e) st->element_flag[e] = (f[e] == 1) ? 1 : 0;
+    }
+    if (st->Qe) HIPCHK(hipMemcpyAsync(st->Qe, c->d_fe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step before upload_model/reset_state");
+    if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step: n_steps=%lld d_time=%g", (long long)n_steps, d_time);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    for (int64_t it = 0; it < n_steps; ++it) {
+        const double t = t_first + (double)it;
+        EventPair ep;
+        // nodal update (:562-567), Q from the previous step's element forces (:668-675)
+        hk::NodalArgs na;
+        na.u = c->d_u[c->cur];
+        na.u_pre_out = c->d_u[1 - c->cur];
+        na.mass = c->d_mass;
+        na.inc_ptr = c->d_inc_ptr;
+        na.inc = c->d_inc;
+        na.fe = c->d_fe;
+        na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
+        na.fext = nullptr;
+        na.nN = c->nN;
+        na.dt = d_time;
+        int rc = hkc::comm_pre_nodal(c);
+        if (rc) return rc;
+        hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
+        HIPCHK(hk::launch_nodal(na, s));
+        hkc::prof_end(c, &ep);
+        // multi-GPU: interface nodes are redone with the cross-rank assembled Q
+        rc = hkc::comm_post_nodal(c, d_time);
+        if (rc) return rc;
+        // boundary conditions (:585-617)
+        if (c->nbc > 0) {
+            hk::BCArgs ba;
+            ba.dof = c->d_bc_dof;
+            ba.grp = c->d_bc_grp;
+            ba.val = c->d_bc_val;
+            ba.n = c->nbc;
+            ba.amp_n = c->d_amp_n;
+            ba.amp_off = c->d_amp_off;
+            ba.amp_t = c->d_amp_t;
+            ba.amp_v = c->d_amp_v;
+            ba.out = c->d_u[1 - c->cur];
+            ba.ct = t * d_time;
+            hkc::prof_begin(c, HAKAI_K_BC, &ep);
+            HIPCHK(hk::launch_bc(ba, s));
+            hkc::prof_end(c, &ep);
+        }
+        c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
+        c->q_from_buf = false;
+        // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
+        hk::ElemArgs ea;
+        ea.coord = c->d_coord;
+        ea.u = c->d_u[c->cur];
+        ea.u_pre = c->d_u[1 - c->cur];
+        ea.conn = c->d_conn;
+        ea.flag = c->d_flag;
+        ea.mat = c->d_mat;
+        ea.mats = c->d_mats;
+        ea.stress = c->d_stress;
+        ea.strain = c->d_strain;
+        ea.eqps = c->d_eqps;
+        ea.yield = c->d_yield;
+        ea.triax = c->d_triax;
+        ea.fe = c->d_fe;
+        ea.vol = nullptr;
+        ea.nE = c->nE;
+        ea.ld = c->ld;
+        ea.del_count = c->d_del_count;
+        ea.del_log = c->d_del_log;
+        ea.del_cap = c->del_cap;
+        ea.t_step = t;
+        ea.negjac = c->d_negjac;
+        hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
+        HIPCHK(hk::launch_element(ea, c->has_ductile, it == n_steps - 1, s));
+        hkc::prof_end(c, &ep);
+        rc = hkc::comm_post_element(c);
+        if (rc) return rc;
+        c->steps_done++;
+        c->last_dt = d_time;
+    }
+    return 0;
+}
+
+int hakai_sync(hakai_ctx* c) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int hakai_deleted(hakai_ctx* c, int64_t* n_deleted, int64_t* log, int64_t cap) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    HIPCHK(hipSetDevice(c->device));
+    int cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, c->d_del_count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (n_deleted) *n_deleted = cnt;
+    if (log && cap > 0 && cnt > 0) {
+        const long long m = std::min<long long>(std::min<long long>(cnt, cap), c->del_cap);
+        HIPCHK(hipMemcpy(log, c->d_del_log, 2 * m * sizeof(long long), hipMemcpyDeviceToHost));
+        // the kernel appends in completion order; the reference deletes in element order per step
+        std::vector<std::pair<long long, long long>> v((size_t)m);
+        for (long long i = 0; i < m; ++i) v[i] = std::make_pair(log[2 * i], log[2 * i + 1]);
+        std::sort(v.begin(), v.end());
+        for (long long i = 0; i < m; ++i) {
+            log[2 * i] = v[i].first;
+            log[2 * i + 1] = v[i].second;
+        }
+    }
+    return 0;
+}
+
+int hakai_negative_jacobians(hakai_ctx* c, int64_t* n) {
+    if (!c || !n) return fail(HAKAI_ERR_ARG, "null");
+    HIPCHK(hipSetDevice(c->device));
+    unsigned long long v = 0;
+    HIPCHK(hipMemcpyAsync(&v, c->d_negjac, sizeof v, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *n = (int64_t)v;
+    return 0;
+}
+
+int hakai_node_stress_strain(hakai_ctx* c, double* node_stress, double* node_strain, double* node_eqps,
+                             double* node_mises, double* node_triax) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->state_ok) return fail(HAKAI_ERR_STATE, "node_stress_strain without state");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t nN = (size_t)c->nN;
+    double *ns = nullptr, *nn = nullptr, *ne = nullptr, *nm = nullptr, *nt = nullptr;
+    HIPCHK(dalloc(&ns, 6 * nN));
+    HIPCHK(dalloc(&nn, 6 * nN));
+    HIPCHK(dalloc(&ne, nN));
+    HIPCHK(dalloc(&nm, nN));
+    HIPCHK(dalloc(&nt, nN));
+    HIPCHK(hk::launch_node_average(c->d_inc_ptr, c->d_inc, c->d_stress, c->d_strain, c->d_eqps, c->d_triax, c->ld,
+                                   c->nN, ns, nn, ne, nm, nt, s));
+    if (node_stress) HIPCHK(hipMemcpyAsync(node_stress, ns, 6 * nN * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (node_strain) HIPCHK(hipMemcpyAsync(node_strain, nn, 6 * nN * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (node_eqps) HIPCHK(hipMemcpyAsync(node_eqps, ne, nN * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (node_mises) HIPCHK(hipMemcpyAsync(node_mises, nm, nN * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (node_triax) HIPCHK(hipMemcpyAsync(node_triax, nt, nN * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    dfree(ns);
+    dfree(nn);
+    dfree(ne);
+    dfree(nm);
+    dfree(nt);
+    return 0;
+}
+
+int hakai_profile_enable(hakai_ctx* c, int on) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (!on) prof_harvest(c);
+    c->prof = on != 0;
+    for (int k = 0; k < HAKAI_K_COUNT; ++k) {
+        c->k_ms[k] = 0;
+        c->k_n[k] = 0;
+    }
+    return 0;
+}
+
+int hakai_profile_read(hakai_ctx* c, int kernel, double* total_ms, int64_t* launches) {
+    if (!c || kernel < 0 || kernel >= HAKAI_K_COUNT) return fail(HAKAI_ERR_ARG, "bad profile query");
+    (void)hipSetDevice(c->device);
+    prof_harvest(c);
+    if (total_ms) *total_ms = c->k_ms[kernel];
+    if (launches) *launches = c->k_n[kernel];
+    return 0;
+}
+
+// ---- stateless literal drop-ins -----------------------------------------------------------------
+int hakai_stress_hexa(int device, int64_t nNode, int64_t nElement, double* Qe, double* integ_stress,
+                      double* integ_strain, double* integ_yield_stress, double* integ_eq_plastic_strain,
+                      const double* position, const double* d_disp, const int64_t* elementmat,
+                      const int64_t* element_flag, int32_t integ_num, int32_t nMat, const hakai_material_t* mats,
+                      const int64_t* element_material, double* elementVolume) {
+    if (integ_num != 8) return fail(HAKAI_ERR_ARG, "integ_num must be 8 (v2/HAKAI_j.jl:177)");
+    if (!Qe || !integ_stress || !integ_strain || !integ_yield_stress || !integ_eq_plastic_strain || !position ||
+        !d_disp || !element_flag)
+        return fail(HAKAI_ERR_ARG, "stress_hexa: null array");
+    hakai_ctx* c = nullptr;
+    int r = hakai_create(&c, device);
+    if (r) return r;
+    struct Guard {
+        hakai_ctx* c;
+        ~Guard() { hakai_destroy(c); }
+    } guard{c};
+    // position = coord + 0 and d_disp = 0 - (-d_disp): the element kernel reproduces both exactly
+    std::vector<double> ones(3 * (size_t)nNode, 1.0);
+    r = hakai_upload_model(c, nNode, position, nElement, elementmat, element_material, nMat, mats, ones.data());
+    if (r) return r;
+    std::vector<double> zero(3 * (size_t)nNode, 0.0), mdu(3 * (size_t)nNode);
+    for (size_t i = 0; i < mdu.size(); ++i) mdu[i] = -d_disp[i];
+    hakai_state_t st;
+    std::memset(&st, 0, sizeof st);
+    st.disp = zero.data();
+    st.disp_pre = mdu.data();
+    st.integ_stress = integ_stress;
+    st.integ_strain = integ_strain;
+    st.integ_yield_stress = integ_yield_stress;
+    st.integ_eq_plastic_strain = integ_eq_plastic_strain;
+    st.element_flag = const_cast<int64_t*>(element_flag);
+    r = hakai_upload_state(c, &st);
+    if (r) return r;
+    hipStream_t s = c->stream;
+    double* d_vol = nullptr;
+    HIPCHK(dalloc(&d_vol, (size_t)nElement));
+    HIPCHK(hipMemsetAsync(c->d_fe, 0, 24 * (size_t)nElement * sizeof(double), s));
+    hk::ElemArgs ea;
+    ea.coord = c->d_coord;
+    ea.u = c->d_u[c->cur];
+    ea.u_pre = c->d_u[1 - c->cur];
+    ea.conn = c->d_conn;
+    ea.flag = c->d_flag;
+    ea.mat = c->d_mat;
+    ea.mats = c->d_mats;
+    ea.stress = c->d_stress;
+    ea.strain = c->d_strain;
+    ea.eqps = c->d_eqps;
+    ea.yield = c->d_yield;
+    ea.triax = c->d_triax;
+    ea.fe = c->d_fe;
+    ea.vol = d_vol;
+    ea.nE = c->nE;
+    ea.ld = c->ld;
+    ea.del_count = c->d_del_count;
+    ea.del_log = c->d_del_log;
+    ea.del_cap = c->del_cap;
+    ea.t_step = 0;
+    ea.negjac = c->d_negjac;
+    HIPCHK(hk::launch_element(ea, false, false, s));
+    std::vector<double> fe(24 * (size_t)nElement), vol((size_t)nElement);
+    HIPCHK(hipMemcpyAsync(fe.data(), c->d_fe, fe.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(vol.data(), d_vol, vol.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    dfree(d_vol);
+    c->steps_done = 1;
+    c->last_dt = 1.0;
+    hakai_state_t out;
+    std::memset(&out, 0, sizeof out);
+    out.integ_stress = integ_stress;
+    out.integ_strain = integ_strain;
+    out.integ_yield_stress = integ_yield_stress;
+    out.integ_eq_plastic_strain = integ_eq_plastic_strain;
+    r = hakai_download_state(c, &out);
+    if (r) return r;
+    for (int64_t e = 0; e < nElement; ++e) {
+        if (element_flag[e] == 0) continue;
+        for (int j = 0; j < 24; ++j) Qe[24 * e + j] += fe[24 * e + j];
+        if (elementVolume) elementVolume[e] = vol[e];
+    }
+    return 0;
+}
+
+int hakai_triax_stress(int device, int64_t nGP, const double* integ_stress, double* integ_triax_stress) {
+    if (nGP < 0 || (nGP > 0 && (!integ_stress || !integ_triax_stress))) return fail(HAKAI_ERR_ARG, "triax: bad args");
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= device || device < 0)
+        return fail(HAKAI_ERR_DEVICE, "no HIP device %d: no CPU fallback", device);
+    HIPCHK(hipSetDevice(device));
+    if (nGP == 0) return 0;
+    double *st = nullptr, *tx = nullptr;
+    HIPCHK(dalloc(&st, 6 * (size_t)nGP));
+    HIPCHK(dalloc(&tx, (size_t)nGP));
+    HIPCHK(hipMemcpy(st, integ_stress, 6 * nGP * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hk::launch_triax_aos(st, tx, nGP, 0));
+    HIPCHK(hipMemcpy(integ_triax_stress, tx, nGP * sizeof(double), hipMemcpyDeviceToHost));
+    dfree(st);
+    dfree(tx);
+    return 0;
+}
+
+}  // extern "C"
+
+// accessors used by other translation units of the library
+namespace hkc {
+long long ctx_nN(hakai_ctx* c) { return c->nN; }
+}

@@ -1,0 +1,332 @@
+// hakai_comm.cpp -- multi-GPU interface exchange over RCCL (xGMI), one process per GPU.
+//
+// Elements are partitioned into contiguous global-id ranges, one per rank (z-slabs for the
+// synthetic bars). A node on the boundary between rank r (lower element ids) and r+1 is present
+// on both. The reference assembles Q serially in element order (v2/HAKAI_j.jl:669-675), so the
+// global order of contributions at such a node is: all of rank r's, then all of rank r+1's.
+// Each step, after the element kernel:
+//   rank r   sends   P_r  = its own contributions summed in order (3 doubles per node)   -> r+1
+//   rank r+1 sends   c_1..c_m, its own contributions one by one (nslot x 3 doubles)      -> r
+// and BOTH ranks form Q = ((P_r + c_1) + c_2) + ... , i.e. exactly the single-GPU summation, so an
+// N-GPU run is bit-identical to the 1-GPU run. One grouped ncclSend/ncclRecv round per step on a
+// second stream; the interior nodal update runs meanwhile and only the interface nodes wait.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <vector>
+
+#include "hakai_internal.hpp"
+
+namespace hkc {
+
+struct Comm {
+    ncclComm_t nc = nullptr;
+    int rank = 0, nranks = 1;
+    hipStream_t cs = nullptr;
+    hipEvent_t ev_packed = nullptr, ev_done = nullptr;
+    int nslot = 0;
+    int n_up = 0, n_dn = 0;      // up: this rank is the lower side (neighbour rank+1); dn: upper side
+    int* d_up = nullptr;         // local node ids
+    int* d_dn = nullptr;
+    double* d_up_sendP = nullptr;   // [n_up][3]
+    double* d_up_recvC = nullptr;   // [n_up][nslot][3]
+    double* d_dn_sendC = nullptr;   // [n_dn][nslot][3]
+    double* d_dn_recvP = nullptr;   // [n_dn][3]
+    double* d_saved = nullptr;      // u_pre of interface nodes [n_up+n_dn][3]
+    bool pending = false;
+};
+
+}  // namespace hkc
+
+using hkc::fail;
+using hkc::hip_fail;
+
+#define HIPCHK(x)                                      \
+    do {                                               \
+        hipError_t _e = (x);                           \
+        if (_e != hipSuccess) return hip_fail(_e, #x); \
+    } while (0)
+#define NCCLCHK(x)                                                                        \
+    do {                                                                                  \
+        ncclResult_t _r = (x);                                                            \
+        if (_r != ncclSuccess) return fail(HAKAI_ERR_COMM, "%s: %s", #x, ncclGetErrorString(_r)); \
+    } while (0)
+
+namespace {
+
+__global__ void k_save_upre(const int* up, int n_up, const int* dn, int n_dn, const double* upre, double* saved) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_up + n_dn) return;
+    const long long n = j < n_up ? up[j] : dn[j - n_up];
+    saved[3 * j + 0] = upre[3 * n + 0];
+    saved[3 * j + 1] = upre[3 * n + 1];
+    saved[3 * j + 2] = upre[3 * n + 2];
+}
+
+__global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
+                       const double* fe, int nslot, double* up_sendP, double* dn_sendC) {
+#pragma clang fp contract(off)
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_up) {
+        const int n = up[j];
+        double q0 = 0.0, q1 = 0.0, q2 = 0.0;
+        for (int i = ptr[n]; i < ptr[n + 1]; ++i) {
+            const double* f = fe + 3 * (long long)inc[i];
+            q0 += f[0];
+            q1 += f[1];
+            q2 += f[2];
+        }
+        up_sendP[3 * j + 0] = q0;
+        up_sendP[3 * j + 1] = q1;
+        up_sendP[3 * j + 2] = q2;
+    } else if (j < n_up + n_dn) {
+        const int jj = j - n_up;
+        const int n = dn[jj];
+        const int b = ptr[n], m = ptr[n + 1] - b;
+        double* o = dn_sendC + (long long)3 * nslot * jj;
+        for (int s = 0; s < nslot; ++s) {
+            if (s < m) {
+                const double* f = fe + 3 * (long long)inc[b + s];
+                o[3 * s + 0] = f[0];
+                o[3 * s + 1] = f[1];
+                o[3 * s + 2] = f[2];
+            } else {
+                o[3 * s + 0] = 0.0;
+                o[3 * s + 1] = 0.0;
+                o[3 * s + 2] = 0.0;
+            }
+        }
+    }
+}
+
+// Re-does the central-difference update (v2/HAKAI_j.jl:564, same expression as k_nodal) for the
+// interface nodes with the cross-rank Q.
+__global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
+                      const double* fe, int nslot, const double* up_sendP, const double* up_recvC,
+                      const double* dn_recvP, const double* saved, const double* u, double* out, const double* mass,
+                      double dt) {
+#pragma clang fp contract(off)
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_up + n_dn) return;
+    double Q[3];
+    long long n;
+    if (j < n_up) {
+        n = up[j];
+        for (int c = 0; c < 3; ++c) Q[c] = up_sendP[3 * j + c];
+        const double* r = up_recvC + (long long)3 * nslot * j;
+        for (int s = 0; s < nslot; ++s)
+            for (int c = 0; c < 3; ++c) Q[c] += r[3 * s + c];
+    } else {
+        const int jj = j - n_up;
+        n = dn[jj];
+        for (int c = 0; c < 3; ++c) Q[c] = dn_recvP[3 * jj + c];
+        const int b = ptr[n], m = ptr[n + 1] - b;
+        for (int s = 0; s < nslot; ++s) {
+            if (s < m) {
+                const double* f = fe + 3 * (long long)inc[b + s];
+                for (int c = 0; c < 3; ++c) Q[c] += f[c];
+            } else {
+                for (int c = 0; c < 3; ++c) Q[c] += 0.0;
+            }
+        }
+    }
+    const double m_ = mass[n];
+    const double dC = 0.0 * m_;
+    const double mdt2 = m_ / (dt * dt);
+    const double inv = 1.0 / (mdt2 + dC / 2.0 / dt);
+    for (int c = 0; c < 3; ++c) {
+        const double uc = u[3 * n + c];
+        const double up_ = saved[3 * j + c];
+        out[3 * n + c] = inv * (0.0 - Q[c] + mdt2 * (2.0 * uc - up_) + dC / 2.0 / dt * up_);
+    }
+}
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc((void**)p, n * sizeof(T));
+}
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+void free_iface(hkc::Comm* m) {
+    dfree(m->d_up);
+    dfree(m->d_dn);
+    dfree(m->d_up_sendP);
+    dfree(m->d_up_recvC);
+    dfree(m->d_dn_sendC);
+    dfree(m->d_dn_recvP);
+    dfree(m->d_saved);
+    m->n_up = m->n_dn = 0;
+    m->pending = false;
+}
+
+}  // namespace
+
+namespace hkc {
+
+void comm_destroy(hakai_ctx* c) {
+    Comm* m = c->comm;
+    if (!m) return;
+    if (m->cs) (void)hipStreamSynchronize(m->cs);
+    free_iface(m);
+    if (m->nc) (void)ncclCommDestroy(m->nc);
+    if (m->ev_packed) (void)hipEventDestroy(m->ev_packed);
+    if (m->ev_done) (void)hipEventDestroy(m->ev_done);
+    if (m->cs) (void)hipStreamDestroy(m->cs);
+    delete m;
+    c->comm = nullptr;
+}
+
+int comm_reset(hakai_ctx* c) {
+    if (c->comm) c->comm->pending = false;
+    return 0;
+}
+
+int comm_pre_nodal(hakai_ctx* c) {
+    Comm* m = c->comm;
+    if (!m || m->n_up + m->n_dn == 0 || !m->pending) return 0;
+    const int n = m->n_up + m->n_dn;
+    hipLaunchKernelGGL(k_save_upre, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
+                       c->d_u[1 - c->cur], m->d_saved);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int comm_post_nodal(hakai_ctx* c, double d_time) {
+    Comm* m = c->comm;
+    if (!m || m->n_up + m->n_dn == 0 || !m->pending) return 0;
+    m->pending = false;
+    HIPCHK(hipStreamWaitEvent(c->stream, m->ev_done, 0));
+    if (c->q_from_buf) return 0;  // uploaded Q already holds the global sum
+    const int n = m->n_up + m->n_dn;
+    EventPair ep;
+    prof_begin(c, HAKAI_K_EXCHANGE, &ep);
+    hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
+                       c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP, m->d_up_recvC, m->d_dn_recvP, m->d_saved,
+                       c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, d_time);
+    prof_end(c, &ep);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int comm_post_element(hakai_ctx* c) {
+    Comm* m = c->comm;
+    if (!m || m->n_up + m->n_dn == 0) return 0;
+    const int n = m->n_up + m->n_dn;
+    hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
+                       c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP, m->d_dn_sendC);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(m->ev_packed, c->stream));
+    HIPCHK(hipStreamWaitEvent(m->cs, m->ev_packed, 0));
+    NCCLCHK(ncclGroupStart());
+    if (m->n_up) {
+        NCCLCHK(ncclSend(m->d_up_sendP, (size_t)3 * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
+        NCCLCHK(ncclRecv(m->d_up_recvC, (size_t)3 * m->nslot * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
+    }
+    if (m->n_dn) {
+        NCCLCHK(ncclSend(m->d_dn_sendC, (size_t)3 * m->nslot * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
+        NCCLCHK(ncclRecv(m->d_dn_recvP, (size_t)3 * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(m->ev_done, m->cs));
+    m->pending = true;
+    return 0;
+}
+
+}  // namespace hkc
+
+extern "C" {
+
+int hakai_comm_unique_id(uint8_t id[128]) {
+    if (!id) return fail(HAKAI_ERR_ARG, "null id");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, 128);
+    return 0;
+}
+
+int hakai_comm_init(hakai_ctx* c, int rank, int nranks, const uint8_t id[128]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(HAKAI_ERR_ARG, "comm_init: bad args");
+    HIPCHK(hipSetDevice(c->device));
+    hkc::comm_destroy(c);
+    hkc::Comm* m = new hkc::Comm();
+    m->rank = rank;
+    m->nranks = nranks;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    ncclResult_t r = ncclCommInitRank(&m->nc, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete m;
+        return fail(HAKAI_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    if (hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_packed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess) {
+        c->comm = m;
+        hkc::comm_destroy(c);
+        return fail(HAKAI_ERR_DEVICE, "comm_init: stream/event creation failed");
+    }
+    c->comm = m;
+    return 0;
+}
+
+int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_node, const int32_t* rank_lo,
+                        const int32_t* rank_hi) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    hkc::Comm* m = c->comm;
+    if (!m) return fail(HAKAI_ERR_STATE, "set_interface before comm_init");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_interface before upload_model");
+    if (n_shared < 0 || (n_shared > 0 && (!local_node || !rank_lo || !rank_hi)))
+        return fail(HAKAI_ERR_ARG, "set_interface: bad arrays");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(m->cs));
+    free_iface(m);
+    std::vector<int> up, dn;
+    for (int64_t j = 0; j < n_shared; ++j) {
+        if (rank_hi[j] != rank_lo[j] + 1)
+            return fail(HAKAI_ERR_ARG, "set_interface: node shared by ranks %d..%d; only adjacent-rank sharing is supported",
+                        rank_lo[j], rank_hi[j]);
+        if (local_node[j] < 0 || local_node[j] >= c->nN) return fail(HAKAI_ERR_ARG, "set_interface: node out of range");
+        if (rank_lo[j] == m->rank) up.push_back((int)local_node[j]);
+        else if (rank_hi[j] == m->rank) dn.push_back((int)local_node[j]);
+        else return fail(HAKAI_ERR_ARG, "set_interface: node %lld not shared with this rank", (long long)local_node[j]);
+    }
+    if ((!up.empty() && m->rank + 1 >= m->nranks) || (!dn.empty() && m->rank == 0))
+        return fail(HAKAI_ERR_ARG, "set_interface: neighbour rank does not exist");
+    // slots = max incidences the upper side holds at a shared node (agreed by all ranks)
+    std::vector<int> ptr((size_t)c->nN + 1);
+    HIPCHK(hipMemcpy(ptr.data(), c->d_inc_ptr, ptr.size() * sizeof(int), hipMemcpyDeviceToHost));
+    int nslot = 0;
+    for (int n : dn) nslot = std::max(nslot, ptr[n + 1] - ptr[n]);
+    int* d_ns = nullptr;
+    HIPCHK(dalloc(&d_ns, 1));
+    HIPCHK(hipMemcpy(d_ns, &nslot, sizeof(int), hipMemcpyHostToDevice));
+    NCCLCHK(ncclAllReduce(d_ns, d_ns, 1, ncclInt32, ncclMax, m->nc, m->cs));
+    HIPCHK(hipStreamSynchronize(m->cs));
+    HIPCHK(hipMemcpy(&nslot, d_ns, sizeof(int), hipMemcpyDeviceToHost));
+    dfree(d_ns);
+    m->nslot = nslot;
+    m->n_up = (int)up.size();
+    m->n_dn = (int)dn.size();
+    HIPCHK(dalloc(&m->d_up, up.size()));
+    HIPCHK(dalloc(&m->d_dn, dn.size()));
+    HIPCHK(dalloc(&m->d_up_sendP, 3 * up.size()));
+    HIPCHK(dalloc(&m->d_up_recvC, 3 * (size_t)nslot * up.size()));
+    HIPCHK(dalloc(&m->d_dn_sendC, 3 * (size_t)nslot * dn.size()));
+    HIPCHK(dalloc(&m->d_dn_recvP, 3 * dn.size()));
+    HIPCHK(dalloc(&m->d_saved, 3 * (up.size() + dn.size())));
+    if (!up.empty()) HIPCHK(hipMemcpy(m->d_up, up.data(), up.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!dn.empty()) HIPCHK(hipMemcpy(m->d_dn, dn.data(), dn.size() * sizeof(int), hipMemcpyHostToDevice));
+    m->pending = false;
+    return 0;
+}
+
+}  // extern "C"

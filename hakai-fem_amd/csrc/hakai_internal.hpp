@@ -1,0 +1,88 @@
+// hakai_internal.hpp -- context definition shared by the translation units of libhakai_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/hakai_hip.h"
+#include "hakai_device.hpp"
+
+namespace hkc {
+struct Comm;  // multi-GPU state (hakai_comm.cpp)
+int fail(int code, const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+}  // namespace hkc
+
+struct EventPair {
+    hipEvent_t a, b;
+    int kernel;
+};
+
+struct hakai_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // model
+    long long nN = 0, nE = 0, ld = 0;
+    double* d_coord = nullptr;
+    double* d_u[2] = {nullptr, nullptr};
+    int cur = 0;  // d_u[cur] = disp, d_u[1-cur] = disp_pre
+    double* d_mass = nullptr;
+    int* d_conn = nullptr;
+    int* d_flag = nullptr;
+    int* d_mat = nullptr;
+    hk::DevMat* d_mats = nullptr;
+    std::vector<hk::DevMat> h_mats;
+    bool has_ductile = false;
+    double* d_stress = nullptr;
+    double* d_strain = nullptr;
+    double* d_eqps = nullptr;
+    double* d_yield = nullptr;
+    double* d_triax = nullptr;
+    double* d_fe = nullptr;
+    int* d_inc_ptr = nullptr;
+    int* d_inc = nullptr;
+    // bc
+    int nbc = 0;
+    int* d_bc_dof = nullptr;
+    int* d_bc_grp = nullptr;
+    double* d_bc_val = nullptr;
+    int* d_amp_n = nullptr;
+    int* d_amp_off = nullptr;
+    double* d_amp_t = nullptr;
+    double* d_amp_v = nullptr;
+    // state extras
+    double* d_qbuf = nullptr;
+    bool q_from_buf = false;
+    std::vector<double> h_velo0;  // velo as uploaded / set by IC, valid until the first step
+    long long steps_done = 0;
+    double last_dt = 0.0;
+    int* d_del_count = nullptr;
+    long long* d_del_log = nullptr;
+    int del_cap = 1 << 20;
+    unsigned long long* d_negjac = nullptr;
+    bool model_ok = false;
+    bool state_ok = false;
+    // external force (contact) -- null until contact is enabled
+    double* d_fext = nullptr;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<EventPair> ev_pending;
+    double k_ms[HAKAI_K_COUNT] = {0, 0, 0, 0};
+    long long k_n[HAKAI_K_COUNT] = {0, 0, 0, 0};
+    // multi-GPU
+    hkc::Comm* comm = nullptr;
+};
+
+
+namespace hkc {
+void prof_begin(hakai_ctx* c, int kernel, EventPair* p);
+void prof_end(hakai_ctx* c, EventPair* p);
+void comm_destroy(hakai_ctx* c);
+int comm_reset(hakai_ctx* c);
+// Multi-GPU hooks used by hakai_step (no-ops without a communicator).
+int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface nodes
+int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
+int comm_post_element(hakai_ctx* c);                 // pack interface forces, start exchange
+}  // namespace hkc

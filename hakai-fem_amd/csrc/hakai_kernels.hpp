@@ -1,0 +1,81 @@
+// hakai_kernels.hpp -- host-side launch interface of the gfx950 kernels (internal to the library).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hakai_device.hpp"
+
+namespace hk {
+
+struct ElemArgs {
+    const double* coord;   // 3nN reference position
+    const double* u;       // disp  (after this step's update)
+    const double* u_pre;   // disp_pre (= disp of the previous step) -> d_disp = u - u_pre
+    const int* conn;       // 8nE, 0-based
+    int* flag;             // nE: 1 active, 2 deleted in the previous step (fe still live), 0 deleted
+    const int* mat;        // nE, 0-based
+    const DevMat* mats;
+    double* stress;        // SoA [6][ld]
+    double* strain;        // SoA [6][ld]
+    double* eqps;          // [ld]
+    double* yield;         // [ld]
+    double* triax;         // [ld]
+    double* fe;            // element nodal forces [nE][8][3] (= Qe column of the reference)
+    double* vol;           // optional current volume per element (elementVolume, :1169)
+    long long nE;
+    long long ld;
+    int* del_count;
+    long long* del_log;    // (step, element 1-based) pairs
+    int del_cap;
+    double t_step;
+    unsigned long long* negjac;
+};
+
+struct NodalArgs {
+    const double* u;       // disp
+    double* u_pre_out;     // in: disp_pre, out: disp_new (ping-pong buffers, no copies)
+    const double* mass;    // per node lumped mass (diag_M of each dof)
+    const int* inc_ptr;    // CSR node -> incidences (8e+i), ascending element order
+    const int* inc;
+    const double* fe;
+    const double* qbuf;    // if non-null: Q taken from this 3nN buffer (uploaded state), not from fe
+    const double* fext;    // external force 3nN or null (= 0)
+    long long nN;
+    double dt;
+};
+
+struct BCArgs {
+    const int* dof;        // 0-based dof
+    const int* grp;
+    const double* val;
+    int n;
+    const int* amp_n;
+    const int* amp_off;
+    const double* amp_t;
+    const double* amp_v;
+    double* out;           // disp_new
+    double ct;             // current time t*d_time
+};
+
+hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
+hipError_t launch_nodal(const NodalArgs& a, hipStream_t s);
+hipError_t launch_bc(const BCArgs& a, hipStream_t s);
+
+// Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
+hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
+                           hipStream_t s);
+// AoS [gp][6] <-> SoA [6][ld] conversions used at upload/download.
+hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, long long ld, hipStream_t s);
+hipError_t launch_soa_to_aos6(const double* soa, double* aos, long long nGP, long long ld, hipStream_t s);
+// Fresh state: stress/strain/eqps/triax 0, yield from material, flags 1.
+hipError_t launch_reset_gp(double* stress, double* strain, double* eqps, double* yield, double* triax, int* flag,
+                           const int* mat, const DevMat* mats, long long nE, long long ld, hipStream_t s);
+// Stand-alone triaxiality (cal_triax_stress) on an AoS [gp][6] stress array.
+hipError_t launch_triax_aos(const double* stress_aos, double* triax, long long nGP, hipStream_t s);
+// Output: node averages of GP quantities (cal_node_stress_strain).
+hipError_t launch_node_average(const int* inc_ptr, const int* inc, const double* stress, const double* strain,
+                               const double* eqps, const double* triax, long long ld, long long nN,
+                               double* node_stress, double* node_strain, double* node_eqps, double* node_mises,
+                               double* node_triax, hipStream_t s);
+
+}  // namespace hk

@@ -1,0 +1,97 @@
+"""Element partitioning for multi-GPU runs (one process per GPU).
+
+Ranks own contiguous global element-id ranges, so the reference's serial element-order force
+assembly (v2/HAKAI_j.jl:669-675) visits, at a node shared by ranks r and r+1, all of rank r's
+contributions before rank r+1's. The library's interface exchange (hakai_comm.cpp) uses that to keep
+the N-rank result bit-identical to one rank. Lumped mass at shared nodes is computed from the rank's
+elements plus one halo layer, in global element order, so it is bit-identical to the global mass.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import mesh as _mesh
+from .model import Model
+
+
+def partition_ranges(n: int, world: int) -> list[tuple[int, int]]:
+    """Split n items into `world` contiguous ranges (first ranks take the remainder)."""
+    q, r = divmod(n, world)
+    out, s = [], 0
+    for i in range(world):
+        e = s + q + (1 if i < r else 0)
+        out.append((s, e))
+        s = e
+    return out
+
+
+def _bar_layers(nx, ny, k0, k1, coord_global):
+    """Nodes of layers k0..k1 (inclusive) and elements of layers k0..k1-1 of a structured bar,
+    renumbered locally (1-based). coord_global: (nN_global, 3)."""
+    npl = (nx + 1) * (ny + 1)
+    coord = coord_global[k0 * npl:(k1 + 1) * npl].copy()
+    nzl = k1 - k0
+    iz, iy, ix = np.meshgrid(np.arange(nzl), np.arange(ny), np.arange(nx), indexing="ij")
+    ix, iy, iz = ix.ravel(), iy.ravel(), iz.ravel()
+    n = lambda a, b, c: _mesh.node_id(ix + a, iy + b, iz + c, nx, ny)  # noqa: E731
+    elem = np.stack([n(0, 0, 0), n(1, 0, 0), n(1, 1, 0), n(0, 1, 0),
+                     n(0, 0, 1), n(1, 0, 1), n(1, 1, 1), n(0, 1, 1)], axis=1).astype(np.int64)
+    return np.ascontiguousarray(coord), np.ascontiguousarray(elem)
+
+
+def slab_partition(glob: Model, rank: int, world: int, nx: int, ny: int):
+    """Split a structured nx x ny x nz bar model (from hakai.mesh.bar_model) into z-slabs.
+
+    Returns (local Model, local diag_M (3 nN_local), (local_node, rank_lo, rank_hi))."""
+    npl = (nx + 1) * (ny + 1)
+    nz = glob.nElement // (nx * ny)
+    assert nz * nx * ny == glob.nElement and (nz + 1) * npl == glob.nNode, "not a structured bar"
+    k0, k1 = partition_ranges(nz, world)[rank]
+    if k1 - k0 < 2 and world > 1:
+        raise ValueError("each slab needs >= 2 element layers (a node may be shared by two ranks only)")
+    coord, elem = _bar_layers(nx, ny, k0, k1, glob.coordmat)
+    # lumped mass with one halo layer each side, elements in global order
+    h0, h1 = max(0, k0 - 1), min(nz, k1 + 1)
+    hc, he = _bar_layers(nx, ny, h0, h1, glob.coordmat)
+    mat = glob.element_material[h0 * nx * ny:h1 * nx * ny].copy()
+    halo = Model(hc, he, mat, glob.materials, mass_scaling=glob.mass_scaling)
+    hdiag, _ = halo.lumped_mass()
+    off = (k0 - h0) * npl
+    diag = np.ascontiguousarray(hdiag[3 * off:3 * (off + coord.shape[0])])
+    # boundary conditions / initial velocity restricted to the local node range
+    g0 = k0 * npl                      # global 0-based id of local node 0
+    nloc = coord.shape[0]
+
+    def to_local_dofs(d):
+        d = np.asarray(d, np.int64)
+        n0 = (d - 1) // 3
+        keep = (n0 >= g0) & (n0 < g0 + nloc)
+        return d[keep] - 3 * g0
+
+    bc = []
+    for g in glob.bc:
+        ents = [(to_local_dofs(d), v) for d, v in g.entries]
+        ents = [(d, v) for d, v in ents if len(d)]
+        if ents:
+            bc.append(type(g)(ents, g.amp_time, g.amp_value))
+    icn = (glob.ic_dofs - 1) // 3
+    keep = (icn >= g0) & (icn < g0 + nloc)
+    local = Model(coord, elem, glob.element_material[k0 * nx * ny:k1 * nx * ny].copy(), glob.materials, bc,
+                  glob.ic_dofs[keep] - 3 * g0, glob.ic_values[keep], glob.d_time, glob.end_time, glob.mass_scaling,
+                  name=f"{glob.name}[rank {rank}/{world}]")
+    # interface: bottom layer shared with rank-1, top layer with rank+1 (ascending global id)
+    ln, lo, hi = [], [], []
+    if rank > 0:
+        ln.append(np.arange(0, npl))
+        lo.append(np.full(npl, rank - 1))
+        hi.append(np.full(npl, rank))
+    if rank < world - 1:
+        ln.append(np.arange(nloc - npl, nloc))
+        lo.append(np.full(npl, rank))
+        hi.append(np.full(npl, rank + 1))
+    iface = (np.concatenate(ln).astype(np.int64) if ln else np.zeros(0, np.int64),
+             np.concatenate(lo).astype(np.int32) if lo else np.zeros(0, np.int32),
+             np.concatenate(hi).astype(np.int32) if hi else np.zeros(0, np.int32))
+    local.global_node_offset = g0
+    local.global_element_offset = k0 * nx * ny
+    return local, diag, iface

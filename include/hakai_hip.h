@@ -1,0 +1,205 @@
+/*
+ * hakai_hip.h -- C ABI of libhakai_hip.so: the MI355X (gfx950) explicit-dynamics inner loop of
+ * HAKAI (yozoyugen/HAKAI-fem v0.0.2), behind HAKAI's own driver surface
+ * (HAKAI("*.inp") -> temp/fileNNN.vtk).
+ *
+ * Reference files (read-only, /root/reference):  "v2/" = HAKAI-v0.0.2/Julia/
+ *   v2/HAKAI_j.jl        solver; time loop :487-951
+ *   v2/readInpFile_j.jl  .inp reader, :152-1113
+ *
+ * Conventions (identical to the reference's Julia arrays):
+ *   - reals are FP64; index arrays are int64 and 1-BASED (elementmat, element_material, dofs);
+ *   - coordmat/position are 3 x nNode column-major (x of node n at [3(n-1)]);
+ *   - nodal vectors are 3nNode with dof = 3(n-1)+c;
+ *   - integ_stress/integ_strain are 6 x 8nElement column-major, Voigt (xx,yy,zz,xy,yz,xz),
+ *     Gauss point index 8(e-1)+i;  integ_* scalars are 8nElement;  Qe is 24 x nElement.
+ * The library owns all device memory and converts layout (Julia AoS <-> device SoA, int64 1-based
+ * <-> int32 0-based) at upload/download; it never frees caller memory.
+ * Errors: every int-returning call returns 0 on success and a negative code on failure;
+ * hakai_last_error() gives the message (thread-local). A context is used by one host thread.
+ * There is no CPU fallback: compute entry points fail with HAKAI_ERR_DEVICE when no gfx950 device
+ * is present.
+ */
+#ifndef HAKAI_HIP_H
+#define HAKAI_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HAKAI_ABI_VERSION 1
+
+enum {
+    HAKAI_OK = 0,
+    HAKAI_ERR_ARG = -1,      /* bad argument / shape */
+    HAKAI_ERR_DEVICE = -2,   /* no device, HIP failure */
+    HAKAI_ERR_IO = -3,       /* file open / parse */
+    HAKAI_ERR_STATE = -4,    /* call order (e.g. step before upload_model) */
+    HAKAI_ERR_MODEL = -5,    /* a case the reference itself rejects (e.g. 1-row *Plastic -> BoundsError) */
+    HAKAI_ERR_COMM = -6      /* RCCL */
+};
+
+typedef struct hakai_ctx hakai_ctx;
+
+/* One material as readInpFile builds it (MaterialType, v2/readInpFile_j.jl:84-96). G, Dmat
+ * (v2/HAKAI_j.jl:143-160) and Hd (v2/readInpFile_j.jl:763-768) are derived inside. */
+typedef struct {
+    double density, young, poisson;
+    int32_t n_plastic;      /* rows of *Plastic (yield stress, eq. plastic strain); 0 = elastic */
+    const double* plastic;  /* row-major [n_plastic][2] */
+    int32_t n_ductile;      /* rows of *Damage Initiation, criterion=DUCTILE; 0 = no deletion */
+    const double* ductile;  /* row-major [n_ductile][3] (fracture strain, triaxiality, rate) */
+} hakai_material_t;
+
+/* Boundary conditions, flattened BCType list (v2/readInpFile_j.jl:98-104, :843-957).
+ * Group g is one *Boundary block; its entries are (dof list, value) lines applied in order, later
+ * groups overwrite earlier ones (v2/HAKAI_j.jl:585-617). amp_n[g] == 0 means no amplitude. */
+typedef struct {
+    int32_t n_groups;
+    const int32_t* amp_n;      /* [n_groups] */
+    const int64_t* amp_off;    /* [n_groups] into amp_time / amp_value */
+    const double* amp_time;
+    const double* amp_value;
+    const int64_t* entry_off;  /* [n_groups+1] */
+    const double* entry_value; /* [n_entries] */
+    const int64_t* dof_off;    /* [n_entries+1] into dofs */
+    const int64_t* dofs;       /* 1-based dofs */
+} hakai_bc_t;
+
+/* Per-step state in the reference layout (v2/HAKAI_j.jl:225-230, :430-456). Any pointer may be
+ * NULL to skip that array. velo is derived (d_disp/d_time, :628) on download. */
+typedef struct {
+    double* disp;                    /* 3nN */
+    double* disp_pre;                /* 3nN */
+    double* velo;                    /* 3nN */
+    double* Q;                       /* 3nN, internal force of the last step (used by the next) */
+    double* integ_stress;            /* 6 x 8nE */
+    double* integ_strain;            /* 6 x 8nE */
+    double* integ_yield_stress;      /* 8nE */
+    double* integ_eq_plastic_strain; /* 8nE */
+    double* integ_triax_stress;      /* 8nE */
+    int64_t* element_flag;           /* nE (1 = active, 0 = deleted) */
+    double* Qe;                      /* 24 x nE element internal forces of the last step (:1330-1340) */
+} hakai_state_t;
+
+/* ---- library / device --------------------------------------------------------------------- */
+int hakai_abi_version(void);
+const char* hakai_last_error(void);
+/* Number of visible HIP devices (0 on a host without GPU). */
+int hakai_device_count(int* n);
+
+/* ---- persistent device context (replaces the Julia-side state of hakai(), v2/HAKAI_j.jl:81-480) */
+int hakai_create(hakai_ctx** ctx, int device);
+int hakai_destroy(hakai_ctx* ctx);
+
+/* Model: mesh, materials, lumped mass (diag_M is per dof, 3nN, as v2/HAKAI_j.jl:202-215 builds
+ * it; the three dofs of a node must carry the same mass, as the reference always produces). */
+int hakai_upload_model(hakai_ctx* ctx, int64_t nNode, const double* coordmat, int64_t nElement,
+                       const int64_t* elementmat, const int64_t* element_material, int32_t nMat,
+                       const hakai_material_t* mats, const double* diag_M);
+int hakai_set_bc(hakai_ctx* ctx, const hakai_bc_t* bc);
+
+/* Fresh state on device: disp = disp_pre = Q = 0, stress/strain/eqps/triax = 0, element_flag = 1,
+ * yield = first *Plastic row (v2/HAKAI_j.jl:225-239, :430-465), then the initial velocity field
+ * (ic_dofs 1-based, one value per dof): disp_pre[dof] = -v*d_time, velo[dof] = v (:233-239). */
+int hakai_reset_state(hakai_ctx* ctx, int64_t n_ic, const int64_t* ic_dofs, const double* ic_values,
+                      double d_time);
+int hakai_upload_state(hakai_ctx* ctx, const hakai_state_t* st);
+int hakai_download_state(hakai_ctx* ctx, hakai_state_t* st);
+
+/* n_steps iterations of the time-loop body v2/HAKAI_j.jl:497-764 (contact-free decks) for
+ * t = t_first .. t_first+n_steps-1 (t is Float64 like `for t = 1:time_num`). Asynchronous with
+ * respect to the host until hakai_sync / a download. */
+int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
+int hakai_sync(hakai_ctx* ctx);
+/* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
+int hakai_deleted(hakai_ctx* ctx, int64_t* n_deleted, int64_t* log, int64_t cap);
+/* Negative-Jacobian events seen by the element kernel (reference prints a warning, :1736-1739). */
+int hakai_negative_jacobians(hakai_ctx* ctx, int64_t* n);
+
+/* GP -> node averages for output, on device (cal_node_stress_strain, v2/HAKAI_j.jl:3408-3486).
+ * node_stress/node_strain are nN x 6 row-major; any pointer may be NULL. */
+int hakai_node_stress_strain(hakai_ctx* ctx, double* node_stress, double* node_strain,
+                             double* node_eq_plastic_strain, double* node_mises_stress,
+                             double* node_triax_stress);
+
+/* ---- stateless literal drop-ins (host arrays, reference layout, in place; PCIe-bound, for parity) */
+/* cal_stress_hexa(Qe, integ_stress, integ_strain, integ_yield_stress, integ_eq_plastic_strain,
+ *   position, d_disp, elementmat, element_flag, integ_num, Pusai_mat, MATERIAL, element_material,
+ *   elementMinSize, elementVolume)  -- v2/HAKAI_j.jl:1033-1036 (called at :664-667).
+ * Qe is accumulated into (the reference zeroes it first at :662); integ_num must be 8;
+ * Pusai_mat and elementMinSize are implied (the kernel builds Pusai in registers). */
+int hakai_stress_hexa(int device, int64_t nNode, int64_t nElement, double* Qe, double* integ_stress,
+                      double* integ_strain, double* integ_yield_stress, double* integ_eq_plastic_strain,
+                      const double* position, const double* d_disp, const int64_t* elementmat,
+                      const int64_t* element_flag, int32_t integ_num, int32_t nMat,
+                      const hakai_material_t* mats, const int64_t* element_material, double* elementVolume);
+/* cal_triax_stress(integ_stress, integ_triax_stress) -- v2/HAKAI_j.jl:982 (called at :677). */
+int hakai_triax_stress(int device, int64_t nGP, const double* integ_stress, double* integ_triax_stress);
+
+/* ---- host-side setup helpers (no GPU) ------------------------------------------------------ */
+/* Element volumes and lumped mass, v2/HAKAI_j.jl:183-218 (diag_M per dof, 3nN). */
+int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, const int64_t* elementmat,
+                      const int64_t* element_material, int32_t nMat, const hakai_material_t* mats,
+                      double mass_scaling, double* diag_M, double* elementVolume);
+
+/* ---- profiling: per-kernel device time measured with HIP events on the context's stream ---- */
+enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_COUNT = 4 };
+int hakai_profile_enable(hakai_ctx* ctx, int on);
+int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
+
+/* ---- multi-GPU: one process per GPU, contiguous element ranges, RCCL over xGMI -------------- */
+int hakai_comm_unique_id(uint8_t id[128]);
+/* Attach a communicator (ncclCommInitRank) to a context created on this rank's device. */
+int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128]);
+/* Interface description for this rank's local model ("multi-GPU"):
+ * shared nodes (local 0-based ids, sorted by global id) with the rank range [lo, hi] of ranks
+ * whose elements touch each node (hi == lo+1 for slab partitions). */
+int hakai_set_interface(hakai_ctx* ctx, int64_t n_shared, const int64_t* local_node, const int32_t* rank_lo,
+                        const int32_t* rank_hi);
+
+/* ---- driver surface: .inp reader, VTK writer, HAKAI(fname) ---------------------------------- */
+/* Flattened ModelType (v2/readInpFile_j.jl:129-150) as the solver consumes it. Owned by the
+ * library; free with hakai_inp_free. */
+typedef struct {
+    int64_t nNode;
+    const double* coordmat;           /* 3 x nNode */
+    int64_t nElement;
+    const int64_t* elementmat;        /* 8 x nElement, 1-based */
+    const int64_t* element_material;  /* nElement, 1-based */
+    const int64_t* element_instance;  /* nElement, 1-based */
+    int32_t nMat;
+    const hakai_material_t* materials;
+    double d_time, end_time, mass_scaling;
+    int32_t contact_flag;             /* 0 none, 1 *Contact, 2 self-contact option */
+    hakai_bc_t bc;
+    int64_t n_ic_dofs;                /* initial velocity: dofs (1-based) and values, in IC order */
+    const int64_t* ic_dofs;
+    const double* ic_values;
+    int32_t n_instance;
+    const int64_t* instance_node_offset;    /* [n_instance] */
+    const int64_t* instance_element_offset; /* [n_instance] */
+    const int64_t* instance_nElement;       /* [n_instance] */
+} hakai_inp_model_t;
+
+int hakai_inp_read(const char* path, hakai_inp_model_t** out);
+void hakai_inp_free(hakai_inp_model_t* m);
+
+/* Legacy-ASCII VTK writer with the reference's content (write_vtk, v2/HAKAI_j.jl:3517-3717):
+ * writes <dir>/file%03d.vtk. node arrays as produced by hakai_node_stress_strain. */
+int hakai_write_vtk(const char* dir, int index, int64_t nNode, const double* coordmat, int64_t nElement,
+                    const int64_t* elementmat, const int64_t* element_flag, const double* disp,
+                    const double* velo, const double* node_stress, const double* node_strain,
+                    const double* node_eq_plastic_strain, const double* node_mises_stress,
+                    const double* node_triax_stress);
+
+/* HAKAI(fname) (v2/HAKAI_j.jl:81-978): read, set up, run the whole step loop on `device`, write
+ * out_dir/file000.vtk .. file100.vtk every floor(time_num/100) steps. verbose=1 prints the
+ * reference's progress lines. Returns 0 or <0. */
+int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbose);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,93 @@
+"""The driver-surface .inp reader (C++ in libhakai_hip.so) against the reference decks and an
+independent pure-Python restatement of the parts of readInpFile the solver consumes."""
+import os
+
+import numpy as np
+import pytest
+
+import hakai
+from hakai import mesh
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+TENSILE = os.path.join(HERE, "golden", "Tensile5e.inp")
+REF_DIR = "/root/reference/HAKAI-v0.0.2/input"
+
+
+def test_tensile5e_reader_matches_code_model():
+    a = hakai.read_inp(TENSILE)
+    b = mesh.tensile5e_model()
+    assert a.nNode == 24 and a.nElement == 5
+    assert np.array_equal(a.coordmat, b.coordmat)
+    assert np.array_equal(a.elementmat, b.elementmat)
+    assert np.array_equal(a.element_material, b.element_material)
+    assert (a.d_time, a.end_time, a.mass_scaling, a.contact_flag) == (5e-7, 0.01, 1.0, 0)
+    assert a.n_steps == 20000
+    assert len(a.materials) == 3
+    for x, y in zip(a.materials, b.materials):
+        assert (x.density, x.young, x.poisson) == (y.density, y.young, y.poisson)
+        assert np.array_equal(x.plastic, y.plastic) and np.array_equal(x.ductile, y.ductile)
+    assert len(a.bc) == len(b.bc) == 2
+    for g, h in zip(a.bc, b.bc):
+        assert len(g.entries) == len(h.entries)
+        for (d1, v1), (d2, v2) in zip(g.entries, h.entries):
+            assert np.array_equal(d1, d2) and v1 == v2
+    assert np.array_equal(a.bc[1].amp_time, [0., 0.01]) and np.array_equal(a.bc[1].amp_value, [0., 1.])
+
+
+def _py_nodes_elems(path):
+    """Independent minimal restatement: *Part/*Node/*Element blocks and *Instance offsets."""
+    lines = open(path).read().split("\n")
+    parts, insts = {}, []
+    i = 0
+    while i < len(lines):
+        l = lines[i]
+        if "*Part, name=" in l:
+            name = l.replace(" ", "").split(",")[1].split("name=")[1]
+            j = i + 1
+            while "*Node" not in lines[j]:
+                j += 1
+            nodes = []
+            j += 1
+            while "*" not in lines[j]:
+                nodes.append([float(x) for x in lines[j].replace(" ", "").split(",") if x][1:4])
+                j += 1
+            while "*Element" not in lines[j]:
+                j += 1
+            els = []
+            j += 1
+            while "*" not in lines[j]:
+                els.append([int(x) for x in lines[j].replace(" ", "").split(",") if x][1:9])
+                j += 1
+            parts[name] = (np.array(nodes), np.array(els, np.int64))
+        if "*Instance" in l:
+            s = l.replace(" ", "").split(",")
+            insts.append((s[2].split("part=")[1], [t.replace(" ", "") for t in
+                                                    lines[i + 1:lines.index("*End Instance", i)]]))
+        i += 1
+    return parts, insts
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DIR), reason="reference decks not present")
+@pytest.mark.parametrize("deck", ["car-crash-N2k.inp", "car-wall-N2k.inp"])
+def test_multi_instance_decks(deck):
+    path = os.path.join(REF_DIR, deck)
+    m = hakai.read_inp(path)
+    parts, insts = _py_nodes_elems(path)
+    coords, elems, off = [], [], 0
+    for pname, tr in insts:
+        c, e = parts[pname]
+        c = c.copy()
+        for t in reversed(tr):
+            s = [x for x in t.split(",") if x]
+            if len(s) == 3:
+                c = c + np.array([float(x) for x in s])
+        coords.append(c)
+        elems.append(e + off)
+        off += c.shape[0]
+    assert np.allclose(m.coordmat, np.vstack(coords), rtol=0, atol=1e-9)
+    assert np.array_equal(m.elementmat, np.vstack(elems))
+    assert m.contact_flag >= 1
+    assert m.mass_scaling == 100.0
+    assert len(m.ic_dofs) > 0 and np.all(m.ic_dofs >= 1)
+    diag, vol = m.lumped_mass()
+    assert np.all(diag > 0)
