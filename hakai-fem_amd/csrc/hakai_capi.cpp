@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -83,6 +84,8 @@ static void free_model(hakai_ctx* c) {
     dfree(c->d_fe);
     dfree(c->d_inc_ptr);
     dfree(c->d_inc);
+    dfree(c->d_inc8);
+    dfree(c->d_del_step);
     dfree(c->d_qbuf);
     dfree(c->d_fext);
     c->model_ok = false;
@@ -185,6 +188,37 @@ void prof_end(hakai_ctx* c, EventPair* p) {
 }
 }  // namespace hkc
 
+
+// Kernel arguments of the element update for the context's current buffers.
+static hk::ElemArgs elem_args(hakai_ctx* c) {
+    hk::ElemArgs ea;
+    std::memset(&ea, 0, sizeof ea);
+    ea.coord = c->d_coord;
+    ea.u = c->d_u[c->cur];
+    ea.u_pre = c->d_u[1 - c->cur];
+    ea.conn = c->d_conn;
+    ea.flag = c->d_flag;
+    ea.mat = c->d_mat;
+    ea.mats = c->d_mats;
+    ea.stress = c->d_stress;
+    ea.strain = c->d_strain;
+    ea.eqps = c->d_eqps;
+    ea.yield = c->d_yield;
+    ea.triax = c->d_triax;
+    ea.fe = c->d_fe;
+    ea.vol = nullptr;
+    ea.nE = c->nE;
+    ea.nEp = c->nEp;
+    ea.ld = c->ld;
+    ea.del_step = c->d_del_step;
+    ea.step_i = 0;
+    ea.any_plastic = c->any_plastic ? 1 : 0;
+    ea.variant = c->elem_variant;
+    ea.pipe_blocks = c->pipe_blocks;
+    ea.nmat = c->nmat;
+    return ea;
+}
+
 // ---------------------------------------------------------------------------------------------
 extern "C" {
 
@@ -214,18 +248,17 @@ int hakai_create(hakai_ctx** out, int device) {
                     prop.gcnArchName);
     hakai_ctx* c = new hakai_ctx();
     c->device = device;
+    if (const char* v = std::getenv("HAKAI_ELEM_MINW")) c->elem_variant = std::atoi(v);
+    if (const char* v = std::getenv("HAKAI_PIPE_BLOCKS")) c->pipe_blocks = std::atoi(v);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return hip_fail(e, "hipStreamCreate");
     }
-    if (dalloc(&c->d_del_count, 1) != hipSuccess || dalloc(&c->d_del_log, 2 * (size_t)c->del_cap) != hipSuccess ||
-        dalloc(&c->d_negjac, 1) != hipSuccess) {
+    if (dalloc(&c->d_negjac, 1) != hipSuccess) {
         delete c;
         return fail(HAKAI_ERR_DEVICE, "hipMalloc for context bookkeeping failed");
     }
-    (void)hipMemsetAsync(c->d_del_count, 0, sizeof(int), c->stream);
-    (void)hipMemsetAsync(c->d_negjac, 0, sizeof(unsigned long long), c->stream);
     *out = c;
     return 0;
 }
@@ -238,8 +271,6 @@ int hakai_destroy(hakai_ctx* c) {
     hkc::comm_destroy(c);
     hkc::free_model(c);
     hkc::free_bc(c);
-    dfree(c->d_del_count);
-    dfree(c->d_del_log);
     dfree(c->d_negjac);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -260,8 +291,9 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     (void)hipStreamSynchronize(c->stream);
     hkc::free_model(c);
     const long long nN = nNode, nE = nElement;
+    const long long nEp = ((nE + 31) / 32) * 32;  // whole 32-element batches; padding behaves as deleted
     // host-side conversions
-    std::vector<int> conn((size_t)(8 * nE)), mat((size_t)nE);
+    std::vector<int> conn((size_t)(8 * nEp), 0), mat((size_t)nEp, 0);
     for (long long e = 0; e < nE; ++e) {
         for (int i = 0; i < 8; ++i) {
             const int64_t n = elementmat[8 * e + i];
@@ -280,13 +312,17 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
         mass[n] = m0;
     }
     c->h_mats.assign((size_t)nMat, DevMat());
+    c->nmat = nMat;
     c->has_ductile = false;
     for (int i = 0; i < nMat; ++i) {
         int r = hkc::build_devmat(mats[i], c->h_mats[i]);
         if (r) return r;
     }
-    for (long long e = 0; e < nE; ++e)
+    c->any_plastic = false;
+    for (long long e = 0; e < nE; ++e) {
         if (c->h_mats[mat[e]].nd > 0) c->has_ductile = true;
+        if (c->h_mats[mat[e]].npp > 0) c->any_plastic = true;
+    }
     // node -> (8e+i) incidence CSR in ascending element order (counting sort keeps the order)
     std::vector<int> ptr((size_t)nN + 1, 0), inc((size_t)(8 * nE));
     for (long long j = 0; j < 8 * nE; ++j) ptr[conn[j] + 1]++;
@@ -295,24 +331,34 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
         std::vector<int> fill(ptr.begin(), ptr.end() - 1);
         for (long long j = 0; j < 8 * nE; ++j) inc[fill[conn[j]]++] = (int)j;
     }
+    int maxinc = 0;
+    for (long long n = 0; n < nN; ++n) maxinc = std::max(maxinc, ptr[n + 1] - ptr[n]);
+    std::vector<int> inc8;
+    if (maxinc <= 8) {  // padded table for the unrolled gather; pad -> zero row 8nE of fe
+        inc8.assign(8 * (size_t)nN, (int)(8 * nEp));
+        for (long long n = 0; n < nN; ++n)
+            for (int j = ptr[n]; j < ptr[n + 1]; ++j) inc8[8 * n + (j - ptr[n])] = inc[j];
+    }
     c->nN = nN;
     c->nE = nE;
-    c->ld = ((8 * nE + 63) / 64) * 64;
+    c->nEp = nEp;
+    c->ld = 8 * nEp;
     const size_t ld = (size_t)c->ld;
     HIPCHK(dalloc(&c->d_coord, 3 * (size_t)nN));
     HIPCHK(dalloc(&c->d_u[0], 3 * (size_t)nN));
     HIPCHK(dalloc(&c->d_u[1], 3 * (size_t)nN));
     HIPCHK(dalloc(&c->d_mass, (size_t)nN));
-    HIPCHK(dalloc(&c->d_conn, 8 * (size_t)nE));
-    HIPCHK(dalloc(&c->d_flag, (size_t)nE));
-    HIPCHK(dalloc(&c->d_mat, (size_t)nE));
+    HIPCHK(dalloc(&c->d_conn, 8 * (size_t)nEp));
+    HIPCHK(dalloc(&c->d_flag, (size_t)nEp));
+    HIPCHK(dalloc(&c->d_mat, (size_t)nEp));
+    HIPCHK(dalloc(&c->d_del_step, (size_t)nEp + 1));
     HIPCHK(dalloc(&c->d_mats, (size_t)nMat));
     HIPCHK(dalloc(&c->d_stress, 6 * ld));
     HIPCHK(dalloc(&c->d_strain, 6 * ld));
     HIPCHK(dalloc(&c->d_eqps, ld));
     HIPCHK(dalloc(&c->d_yield, ld));
     HIPCHK(dalloc(&c->d_triax, ld));
-    HIPCHK(dalloc(&c->d_fe, 24 * (size_t)nE));
+    HIPCHK(dalloc(&c->d_fe, 24 * (size_t)nEp + 3));  // + zero row for padded gathers
     HIPCHK(dalloc(&c->d_inc_ptr, (size_t)nN + 1));
     HIPCHK(dalloc(&c->d_inc, 8 * (size_t)nE));
     HIPCHK(dalloc(&c->d_qbuf, 3 * (size_t)nN));
@@ -320,12 +366,16 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     HIPCHK(hipMemcpyAsync(c->d_coord, coordmat, 3 * nN * sizeof(double), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_mass, mass.data(), nN * sizeof(double), hipMemcpyHostToDevice, s));
     if (nE) {
-        HIPCHK(hipMemcpyAsync(c->d_conn, conn.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->d_mat, mat.data(), nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_conn, conn.data(), 8 * nEp * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_mat, mat.data(), nEp * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_inc, inc.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(c->d_mats, c->h_mats.data(), nMat * sizeof(DevMat), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_inc_ptr, ptr.data(), (nN + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!inc8.empty()) {
+        HIPCHK(dalloc(&c->d_inc8, inc8.size()));
+        HIPCHK(hipMemcpyAsync(c->d_inc8, inc8.data(), inc8.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipStreamSynchronize(s));  // host vectors go out of scope
     c->model_ok = true;
     c->state_ok = false;
@@ -399,11 +449,10 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     c->cur = 0;
     HIPCHK(hipMemsetAsync(c->d_u[0], 0, fn * sizeof(double), s));
     HIPCHK(hipMemsetAsync(c->d_u[1], 0, fn * sizeof(double), s));
-    HIPCHK(hipMemsetAsync(c->d_fe, 0, 24 * (size_t)c->nE * sizeof(double), s));
-    HIPCHK(hipMemsetAsync(c->d_del_count, 0, sizeof(int), s));
-    HIPCHK(hipMemsetAsync(c->d_negjac, 0, sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(c->d_fe, 0, (24 * (size_t)c->nEp + 3) * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(c->d_del_step, 0, ((size_t)c->nEp + 1) * sizeof(int), s));
     HIPCHK(hk::launch_reset_gp(c->d_stress, c->d_strain, c->d_eqps, c->d_yield, c->d_triax, c->d_flag, c->d_mat,
-                               c->d_mats, c->nE, c->ld, s));
+                               c->d_mats, c->nE, c->nEp, c->ld, s));
     c->h_velo0.assign(fn, 0.0);
     c->q_from_buf = false;
     c->steps_done = 0;
@@ -563,6 +612,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.mass = c->d_mass;
         na.inc_ptr = c->d_inc_ptr;
         na.inc = c->d_inc;
+        na.inc8 = c->d_inc8;
         na.fe = c->d_fe;
         na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
         na.fext = nullptr;
@@ -596,28 +646,8 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
         c->q_from_buf = false;
         // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
-        hk::ElemArgs ea;
-        ea.coord = c->d_coord;
-        ea.u = c->d_u[c->cur];
-        ea.u_pre = c->d_u[1 - c->cur];
-        ea.conn = c->d_conn;
-        ea.flag = c->d_flag;
-        ea.mat = c->d_mat;
-        ea.mats = c->d_mats;
-        ea.stress = c->d_stress;
-        ea.strain = c->d_strain;
-        ea.eqps = c->d_eqps;
-        ea.yield = c->d_yield;
-        ea.triax = c->d_triax;
-        ea.fe = c->d_fe;
-        ea.vol = nullptr;
-        ea.nE = c->nE;
-        ea.ld = c->ld;
-        ea.del_count = c->d_del_count;
-        ea.del_log = c->d_del_log;
-        ea.del_cap = c->del_cap;
-        ea.t_step = t;
-        ea.negjac = c->d_negjac;
+        hk::ElemArgs ea = elem_args(c);
+        ea.step_i = (int)t;
         hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
         HIPCHK(hk::launch_element(ea, c->has_ductile, it == n_steps - 1, s));
         hkc::prof_end(c, &ep);
@@ -638,29 +668,59 @@ int hakai_sync(hakai_ctx* c) {
 
 int hakai_deleted(hakai_ctx* c, int64_t* n_deleted, int64_t* log, int64_t cap) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "deleted before upload_model");
     HIPCHK(hipSetDevice(c->device));
-    int cnt = 0;
-    HIPCHK(hipMemcpyAsync(&cnt, c->d_del_count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    std::vector<int> ds((size_t)c->nE);
+    if (c->nE) HIPCHK(hipMemcpyAsync(ds.data(), c->d_del_step, c->nE * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (n_deleted) *n_deleted = cnt;
-    if (log && cap > 0 && cnt > 0) {
-        const long long m = std::min<long long>(std::min<long long>(cnt, cap), c->del_cap);
-        HIPCHK(hipMemcpy(log, c->d_del_log, 2 * m * sizeof(long long), hipMemcpyDeviceToHost));
-        // the kernel appends in completion order; the reference deletes in element order per step
-        std::vector<std::pair<long long, long long>> v((size_t)m);
-        for (long long i = 0; i < m; ++i) v[i] = std::make_pair(log[2 * i], log[2 * i + 1]);
-        std::sort(v.begin(), v.end());
-        for (long long i = 0; i < m; ++i) {
+    // (step, element) in the reference's print order: by step, then element (v2/HAKAI_j.jl:701-736)
+    std::vector<std::pair<long long, long long>> v;
+    for (long long e = 0; e < c->nE; ++e)
+        if (ds[e] > 0) v.push_back(std::make_pair((long long)ds[e], e + 1 + c->elem_offset));
+    std::sort(v.begin(), v.end());
+    if (n_deleted) *n_deleted = (int64_t)v.size();
+    if (log)
+        for (long long i = 0; i < (long long)v.size() && i < cap; ++i) {
             log[2 * i] = v[i].first;
             log[2 * i + 1] = v[i].second;
         }
+    return 0;
+}
+
+int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return fail(HAKAI_ERR_ARG, "set_tuning: null");
+    if (!std::strcmp(key, "elem_minw")) {
+        if (value != 2 && value != 3 && value != 4) return fail(HAKAI_ERR_ARG, "elem_minw must be 2, 3 or 4");
+        c->elem_variant = (int)value;
+        return 0;
     }
+    if (!std::strcmp(key, "elem_pipe_blocks")) {
+        if (value < 0 || value > 65536) return fail(HAKAI_ERR_ARG, "elem_pipe_blocks out of range");
+        c->pipe_blocks = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "nodal_padded")) {
+        if (!value) {
+            dfree(c->d_inc8);
+            return 0;
+        }
+        return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
+    }
+    return fail(HAKAI_ERR_ARG, "unknown tuning key '%s'", key);
+}
+
+int hakai_set_element_offset(hakai_ctx* c, int64_t element_offset) {
+    if (!c || element_offset < 0) return fail(HAKAI_ERR_ARG, "set_element_offset: bad args");
+    c->elem_offset = element_offset;
     return 0;
 }
 
 int hakai_negative_jacobians(hakai_ctx* c, int64_t* n) {
     if (!c || !n) return fail(HAKAI_ERR_ARG, "null");
+    if (!c->state_ok) return fail(HAKAI_ERR_STATE, "negative_jacobians without state");
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->d_negjac, 0, sizeof(unsigned long long), c->stream));
+    HIPCHK(hk::launch_negjac(elem_args(c), c->d_negjac, c->stream));
     unsigned long long v = 0;
     HIPCHK(hipMemcpyAsync(&v, c->d_negjac, sizeof v, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -753,30 +813,11 @@ int hakai_stress_hexa(int device, int64_t nNode, int64_t nElement, double* Qe, d
     if (r) return r;
     hipStream_t s = c->stream;
     double* d_vol = nullptr;
-    HIPCHK(dalloc(&d_vol, (size_t)nElement));
+    HIPCHK(dalloc(&d_vol, (size_t)c->nEp));
     HIPCHK(hipMemsetAsync(c->d_fe, 0, 24 * (size_t)nElement * sizeof(double), s));
-    hk::ElemArgs ea;
-    ea.coord = c->d_coord;
-    ea.u = c->d_u[c->cur];
-    ea.u_pre = c->d_u[1 - c->cur];
-    ea.conn = c->d_conn;
-    ea.flag = c->d_flag;
-    ea.mat = c->d_mat;
-    ea.mats = c->d_mats;
-    ea.stress = c->d_stress;
-    ea.strain = c->d_strain;
-    ea.eqps = c->d_eqps;
-    ea.yield = c->d_yield;
-    ea.triax = c->d_triax;
-    ea.fe = c->d_fe;
+    hk::ElemArgs ea = elem_args(c);
     ea.vol = d_vol;
-    ea.nE = c->nE;
-    ea.ld = c->ld;
-    ea.del_count = c->d_del_count;
-    ea.del_log = c->d_del_log;
-    ea.del_cap = c->del_cap;
-    ea.t_step = 0;
-    ea.negjac = c->d_negjac;
+    ea.pipe_blocks = 0;
     HIPCHK(hk::launch_element(ea, false, false, s));
     std::vector<double> fe(24 * (size_t)nElement), vol((size_t)nElement);
     HIPCHK(hipMemcpyAsync(fe.data(), c->d_fe, fe.size() * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -15,6 +15,7 @@ namespace hk {
 
 constexpr int kMaxPlastic = 64;
 constexpr int kMaxDuctile = 32;
+constexpr int kMaxLdsMats = 8;   // materials staged in LDS by the pipelined element kernel
 
 // Per-material constants, derived on the host exactly like hakai() does (v2/HAKAI_j.jl:143-172)
 // and readInpFile builds Hd (v2/readInpFile_j.jl:763-768).

@@ -23,7 +23,7 @@ struct hakai_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // model
-    long long nN = 0, nE = 0, ld = 0;
+    long long nN = 0, nE = 0, nEp = 0, ld = 0;
     double* d_coord = nullptr;
     double* d_u[2] = {nullptr, nullptr};
     int cur = 0;  // d_u[cur] = disp, d_u[1-cur] = disp_pre
@@ -42,6 +42,11 @@ struct hakai_ctx {
     double* d_fe = nullptr;
     int* d_inc_ptr = nullptr;
     int* d_inc = nullptr;
+    int* d_inc8 = nullptr;       // padded incidence table, null if a node has > 8 incidences
+    int elem_variant = 2;        // k_element occupancy variant (HAKAI_ELEM_MINW)
+    int pipe_blocks = 512;       // persistent pipelined element kernel grid (0 = simple kernel)
+    int nmat = 0;
+    long long elem_offset = 0;   // global id of local element 0
     // bc
     int nbc = 0;
     int* d_bc_dof = nullptr;
@@ -57,10 +62,9 @@ struct hakai_ctx {
     std::vector<double> h_velo0;  // velo as uploaded / set by IC, valid until the first step
     long long steps_done = 0;
     double last_dt = 0.0;
-    int* d_del_count = nullptr;
-    long long* d_del_log = nullptr;
-    int del_cap = 1 << 20;
+    int* d_del_step = nullptr;   // [nEp+1] deletion step per element (0 = never), [nEp] dump slot
     unsigned long long* d_negjac = nullptr;
+    bool any_plastic = false;
     bool model_ok = false;
     bool state_ok = false;
     // external force (contact) -- null until contact is enabled

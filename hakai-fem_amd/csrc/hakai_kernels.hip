@@ -11,6 +11,8 @@
 // disp/disp_pre are ping-pong buffers and the element kernel forms coord+u and u-u_pre on the fly.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "hakai_kernels.hpp"
 
 namespace hk {
@@ -25,101 +27,115 @@ __device__ constexpr double kSy[8] = {-1., -1., 1., 1., -1., -1., 1., 1.};
 __device__ constexpr double kSz[8] = {-1., -1., -1., -1., 1., 1., 1., 1.};
 
 // ---------------------------------------------------------------------------------------------
-// Element kernel: one 8-lane group per hex8 element, lane k = Gauss point k (gc order of
+// Element update: one 8-lane group per hex8 element, lane k = Gauss point k (gc order of
 // v2/HAKAI_j.jl:1913-1920: k bits = (xi, eta, zeta) signs).
 //
 // Math (identical to the reference's Bfinal algebra, reorganised so no 6x24 matrix is formed):
 //   P_k   = J_k^{-1} Pusai_k                    (dN_i/dx at GP k, signed det_k)
 //   bbar_i = sum_k det_k P_k[:,i] / (3V),  V = sum_k |det_k|      (= BVbar rows 1-3, :1766-1780)
 //   de    = sym(grad du) + (sum_i bbar_i.du_i - div_k(du)/3) (1,1,1,0,0,0)     (= Bfinal*d_u)
-//   f_i  += det_k ( sigma P_k[:,i] - P_k[:,i] tr(sigma)/3 ) ;  f_i += (sum_k det_k tr sigma_k) bbar_i
+//   f_i  += det_k (sigma_k - tr_k/3 I) P_k[:,i] ;  f_i += (sum_k det_k tr sigma_k) bbar_i
 //                                                                            (= sum_k det_k Bfinal' sigma)
 // ---------------------------------------------------------------------------------------------
-template <bool DO_DELETE, bool STORE_TRIAX>
-__global__ __launch_bounds__(kBlock) void k_element(ElemArgs a) {
-    __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
-    const int tid = threadIdx.x;
-    const int k = tid & 7;
-    const int grp = tid >> 3;
-    const long long e = (long long)xcd_remap(blockIdx.x, gridDim.x) * kEPB + grp;
-    if (e >= a.nE) return;  // whole 8-lane groups leave together
-    const int fl = a.flag[e];
-    if (fl != 1) {
-        if (fl == 2) {  // deleted last step: its Qe becomes 0 from now on (reference skips it, :1116)
-            double* f = a.fe + 24 * e + 3 * k;
-            f[0] = 0.0;
-            f[1] = 0.0;
-            f[2] = 0.0;
-            a.triax[8 * e + k] = 0.0;  // triaxiality of zero stress (:1012-1014)
-            if (k == 0) a.flag[e] = 0;
-        }
-        return;
-    }
-    const long long gp = 8 * e + k;
-    const long long ld = a.ld;
-    const DevMat* M = a.mats + a.mat[e];
-    const int npp = M->npp;
-    const int nd = DO_DELETE ? M->nd : 0;
 
-    // ---- gather this lane's node: position = coord + u (:650-652), d_disp = u - u_pre (:625)
-    const long long n = a.conn[8 * e + k];
-    double xo[3], duo[3];
+// Everything one lane needs from HBM for one element, gathered ahead of the compute.
+struct ElemIn {
+    int n, fl, mt;       // stage A: local node, element flag, material
+    double x[3], du[3];  // stage B: this lane's node: position = coord + u, d_disp = u - u_pre
+    double sig[6], eps[6], eqp, ys;
+};
+
+// Element arrays are padded to whole 32-element batches; padding elements carry flag 0 (they
+// behave like deleted elements), so every load and store below is unconditional: the compiler can
+// then count outstanding memory operations exactly and keep prefetches in flight across the
+// stores of the previous batch (a conditional store makes its vmcnt accounting fall back to 0).
+__device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int k, ElemIn& in) {
+    in.fl = a.flag[e];
+    in.n = a.conn[8 * e + k];
+    in.mt = a.mat[e];
+}
+
+template <bool ANY_PLASTIC>
+__device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int k, ElemIn& in) {
+    const long long gp = 8 * e + k, ld = a.ld, n = in.n;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double uc = a.u[3 * n + c];
-        xo[c] = a.coord[3 * n + c] + uc;
-        duo[c] = uc - a.u_pre[3 * n + c];
+        in.x[c] = a.coord[3 * n + c] + uc;
+        in.du[c] = uc - a.u_pre[3 * n + c];
     }
-    // ---- Gauss-point state, issued early (coalesced SoA, 512 B per wave per component)
-    double sig[6], eps[6];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) sig[c] = a.stress[c * ld + gp];
+    for (int c = 0; c < 6; ++c) in.sig[c] = a.stress[c * ld + gp];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) eps[c] = a.strain[c * ld + gp];
-    double eqp = 0.0, ys = 0.0;
-    if (npp > 0 || nd > 0) eqp = a.eqps[gp];
-    if (npp > 0) ys = a.yield[gp];
+    for (int c = 0; c < 6; ++c) in.eps[c] = a.strain[c * ld + gp];
+    in.eqp = 0.0;
+    in.ys = 0.0;
+    if (ANY_PLASTIC) {
+        in.eqp = a.eqps[gp];
+        in.ys = a.yield[gp];
+    }
+}
+
+// One element step for the 8 lanes of a group (every group runs it; the element flag selects what
+// is stored):  flag 1 -> full update;  flag 2 (deleted in the previous step) -> Qe and triaxiality
+// become 0 and the flag 0 (the reference skips deleted elements, :1116, and their stress is zero);
+// flag 0 -> state written back unchanged, Qe 0.
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL>
+__device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __restrict__ mats, long long e, int k,
+                                          double* nd8, const ElemIn& in) {
+    const DevMat* M = mats + in.mt;
+    const bool active = in.fl == 1;
+    const long long gp = 8 * e + k;
+    const long long ld = a.ld;
+    const int npp = M->npp;
+    const int nd = DO_DELETE ? M->nd : 0;
+    double eqp = in.eqp, ys = in.ys;
 
     // ---- share the 8 nodes of the element through LDS (this 8-lane group only, same wave:
     // LDS operations of one wave complete in order, so a wavefront-scope fence suffices).
-    double* nd8 = s_nd + grp * kLdsStride;
-    nd8[6 * k + 0] = xo[0];
-    nd8[6 * k + 1] = xo[1];
-    nd8[6 * k + 2] = xo[2];
-    nd8[6 * k + 3] = duo[0];
-    nd8[6 * k + 4] = duo[1];
-    nd8[6 * k + 5] = duo[2];
+    nd8[6 * k + 0] = in.x[0];
+    nd8[6 * k + 1] = in.x[1];
+    nd8[6 * k + 2] = in.x[2];
+    nd8[6 * k + 3] = in.du[0];
+    nd8[6 * k + 4] = in.du[1];
+    nd8[6 * k + 5] = in.du[2];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---- shape-function derivatives at GP k (cal_Pusai_hexa, v2/HAKAI_j.jl:1924-1934)
+    // ---- shape-function derivatives at GP k (cal_Pusai_hexa, v2/HAKAI_j.jl:1924-1934):
+    // dN_i/dxi = sx_i (1/8)(1+eta sy_i)(1+zeta sz_i) etc. Only 4 magnitudes per direction exist,
+    // formed exactly as the reference does ((1/8)*(1+..))*(1+..); the node signs fold into the FMAs.
     const double g = 1.0 / __builtin_sqrt(3.0);
     const double gz = (k & 4) ? g : -g, et = (k & 2) ? g : -g, tu = (k & 1) ? g : -g;
-    const double Ap = 1.0 + gz, Am = 1.0 - gz, Bp = 1.0 + et, Bm = 1.0 - et, Cp = 1.0 + tu, Cm = 1.0 - tu;
-    double pxi[8], pet[8], pze[8];
+    const double A[2] = {1.0 - gz, 1.0 + gz}, B[2] = {1.0 - et, 1.0 + et}, C[2] = {1.0 - tu, 1.0 + tu};
+    double mBC[2][2], mAC[2][2], mAB[2][2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double A = kSx[i] > 0 ? Ap : Am, B = kSy[i] > 0 ? Bp : Bm, C = kSz[i] > 0 ? Cp : Cm;
-        pxi[i] = 1.0 / 8.0 * kSx[i] * B * C;
-        pet[i] = 1.0 / 8.0 * kSy[i] * A * C;
-        pze[i] = 1.0 / 8.0 * kSz[i] * A * B;
-    }
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            mBC[p][q] = 1.0 / 8.0 * B[p] * C[q];
+            mAC[p][q] = 1.0 / 8.0 * A[p] * C[q];
+            mAB[p][q] = 1.0 / 8.0 * A[p] * B[q];
+        }
+#define HK_PXI(i) (kSx[i] * mBC[kSy[i] > 0][kSz[i] > 0])
+#define HK_PET(i) (kSy[i] * mAC[kSx[i] > 0][kSz[i] > 0])
+#define HK_PZE(i) (kSz[i] * mAB[kSx[i] > 0][kSy[i] > 0])
     // ---- Jacobian (:1424-1434), determinant and cofactor inverse (:1436-1455)
     double J[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const double X0 = nd8[6 * i + 0], X1 = nd8[6 * i + 1], X2 = nd8[6 * i + 2];
-        J[0][0] += pxi[i] * X0; J[0][1] += pxi[i] * X1; J[0][2] += pxi[i] * X2;
-        J[1][0] += pet[i] * X0; J[1][1] += pet[i] * X1; J[1][2] += pet[i] * X2;
-        J[2][0] += pze[i] * X0; J[2][1] += pze[i] * X1; J[2][2] += pze[i] * X2;
+        const double p0 = HK_PXI(i), p1 = HK_PET(i), p2 = HK_PZE(i);
+        J[0][0] += p0 * X0; J[0][1] += p0 * X1; J[0][2] += p0 * X2;
+        J[1][0] += p1 * X0; J[1][1] += p1 * X1; J[1][2] += p1 * X2;
+        J[2][0] += p2 * X0; J[2][1] += p2 * X1; J[2][2] += p2 * X2;
     }
-    const double det = J[0][0] * J[1][1] * J[2][2] + J[0][1] * J[1][2] * J[2][0] + J[0][2] * J[1][0] * J[2][1] -
-                       J[0][0] * J[1][2] * J[2][1] - J[0][1] * J[1][0] * J[2][2] - J[0][2] * J[1][1] * J[2][0];
-    if (det < 0.0 && a.negjac) atomicAdd(a.negjac, 1ull);
+    const double c11 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+    const double c21 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+    const double c31 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+    const double det = J[0][0] * c11 + J[0][1] * c21 + J[0][2] * c31;
     const double rd = 1.0 / det;
-    const double i11 = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) * rd;
-    const double i21 = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) * rd;
-    const double i31 = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) * rd;
+    const double i11 = c11 * rd, i21 = c21 * rd, i31 = c31 * rd;
     const double i12 = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) * rd;
     const double i22 = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) * rd;
     const double i32 = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) * rd;
@@ -129,10 +145,14 @@ __global__ __launch_bounds__(kBlock) void k_element(ElemArgs a) {
     double P[8][3];  // dN_i/dx_c at GP k
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        P[i][0] = i11 * pxi[i] + i12 * pet[i] + i13 * pze[i];
-        P[i][1] = i21 * pxi[i] + i22 * pet[i] + i23 * pze[i];
-        P[i][2] = i31 * pxi[i] + i32 * pet[i] + i33 * pze[i];
+        const double p0 = HK_PXI(i), p1 = HK_PET(i), p2 = HK_PZE(i);
+        P[i][0] = i11 * p0 + i12 * p1 + i13 * p2;
+        P[i][1] = i21 * p0 + i22 * p1 + i23 * p2;
+        P[i][2] = i31 * p0 + i32 * p1 + i33 * p2;
     }
+#undef HK_PXI
+#undef HK_PET
+#undef HK_PZE
 
     // ---- volume and B-bar (cal_BVbar_hexa, :1705-1784): V = sum |det|, bbar_k owned by lane k
     const double V = allreduce8(fabs(det));
@@ -148,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_element(ElemArgs a) {
     const double r3V = 1.0 / (3.0 * V);
     const double bb0 = wbar[0] * r3V, bb1 = wbar[1] * r3V, bb2 = wbar[2] * r3V;
     // mean volumetric strain increment / 3 over the element
-    const double sdot = allreduce8(bb0 * duo[0] + bb1 * duo[1] + bb2 * duo[2]);
+    const double sdot = allreduce8(bb0 * in.du[0] + bb1 * in.du[1] + bb2 * in.du[2]);
 
     // ---- strain increment at GP k (= Bfinal * d_u, :1204)
     double Gm[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
@@ -162,11 +182,12 @@ __global__ __launch_bounds__(kBlock) void k_element(ElemArgs a) {
             Gm[2][c] += d2 * P[i][c];
         }
     }
-    const double th3 = (Gm[0][0] + Gm[1][1] + Gm[2][2]) / 3.0;
+    constexpr double kThird = 1.0 / 3.0;
+    const double vol = sdot - (Gm[0][0] + Gm[1][1] + Gm[2][2]) * kThird;
     double de[6];
-    de[0] = Gm[0][0] - th3 + sdot;
-    de[1] = Gm[1][1] - th3 + sdot;
-    de[2] = Gm[2][2] - th3 + sdot;
+    de[0] = Gm[0][0] + vol;
+    de[1] = Gm[1][1] + vol;
+    de[2] = Gm[2][2] + vol;
     de[3] = Gm[0][1] + Gm[1][0];
     de[4] = Gm[1][2] + Gm[2][1];
     de[5] = Gm[0][2] + Gm[2][0];
@@ -174,129 +195,249 @@ __global__ __launch_bounds__(kBlock) void k_element(ElemArgs a) {
     // ---- elastic trial (:1205, :1220) and J2 radial return (:1227-1285)
     const double Dn = M->Dn, Do = M->Do, Ds = M->Ds;
     double fin[6];
-    fin[0] = sig[0] + (Dn * de[0] + Do * (de[1] + de[2]));
-    fin[1] = sig[1] + (Dn * de[1] + Do * (de[0] + de[2]));
-    fin[2] = sig[2] + (Dn * de[2] + Do * (de[0] + de[1]));
-    fin[3] = sig[3] + Ds * de[3];
-    fin[4] = sig[4] + Ds * de[4];
-    fin[5] = sig[5] + Ds * de[5];
-    if (npp > 0) {
-        const double mean = (fin[0] + fin[1] + fin[2]) / 3.0;
-        const double d0 = fin[0] - mean, d1 = fin[1] - mean, d2 = fin[2] - mean;
-        const double q = sqrt(1.5 * (d0 * d0 + d1 * d1 + d2 * d2 +
-                                     2.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5])));
-        if (q > ys) {
-            int p = npp - 2;  // segment search (:1255-1264), 0-based p = p_index-1
-            for (int j = 1; j < npp; ++j) {
-                if (eqp <= M->pl_eps[j]) {
-                    p = j - 1;
+    fin[0] = in.sig[0] + (Dn * de[0] + Do * (de[1] + de[2]));
+    fin[1] = in.sig[1] + (Dn * de[1] + Do * (de[0] + de[2]));
+    fin[2] = in.sig[2] + (Dn * de[2] + Do * (de[0] + de[1]));
+    fin[3] = in.sig[3] + Ds * de[3];
+    fin[4] = in.sig[4] + Ds * de[4];
+    fin[5] = in.sig[5] + Ds * de[5];
+    const double mean = (fin[0] + fin[1] + fin[2]) * kThird;
+    double dv0 = fin[0] - mean, dv1 = fin[1] - mean, dv2 = fin[2] - mean;
+    const double q =
+        sqrt(1.5 * (dv0 * dv0 + dv1 * dv1 + dv2 * dv2 + 2.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5])));
+    double sc = 1.0;
+    if (ANY_PLASTIC && npp > 0 && q > ys) {
+        int p = npp - 2;  // segment search (:1255-1264), 0-based p = p_index-1
+        for (int j = 1; j < npp; ++j) {
+            if (eqp <= M->pl_eps[j]) {
+                p = j - 1;
+                break;
+            }
+        }
+        const double H = M->Hd[p];
+        const double dep = (q - ys) / (3.0 * M->G + H);
+        sc = (ys + H * dep) / q;
+        dv0 *= sc;
+        dv1 *= sc;
+        dv2 *= sc;
+        fin[0] = dv0 + mean;
+        fin[1] = dv1 + mean;
+        fin[2] = dv2 + mean;
+        fin[3] *= sc;
+        fin[4] *= sc;
+        fin[5] *= sc;
+        eqp += dep;
+        ys += H * dep;
+    }
+    double eps[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) eps[c] = in.eps[c] + de[c];
+
+    // ---- triaxiality (cal_triax_stress, :995-1018): mean / Mises of the final stress. The Mises
+    // of the returned stress is sc*q (radial return scales the deviator), so no second sqrt.
+    const double oeq = q * sc;
+    const double tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
+    bool kill = false;
+    if (DO_DELETE && nd > 0) {
+        const double v_e = allreduce8(eqp) * 0.125;
+        const double t_e = allreduce8(tri) * 0.125;
+        if (!(t_e < 0.0)) {  // ductile table (:720-733)
+            double fr = M->du_eps[nd - 1];
+            for (int j = 0; j + 1 < nd; ++j) {
+                if (t_e >= M->du_tri[j] && t_e < M->du_tri[j + 1]) {
+                    fr = M->du_eps[j] + (M->du_eps[j + 1] - M->du_eps[j]) / (M->du_tri[j + 1] - M->du_tri[j]) *
+                                            (t_e - M->du_tri[j]);
                     break;
                 }
             }
-            const double H = M->Hd[p];
-            const double dep = (q - ys) / (3.0 * M->G + H);
-            const double sc = (ys + H * dep) / q;
-            fin[0] = d0 * sc + mean;
-            fin[1] = d1 * sc + mean;
-            fin[2] = d2 * sc + mean;
-            fin[3] *= sc;
-            fin[4] *= sc;
-            fin[5] *= sc;
-            eqp += dep;
-            ys += H * dep;
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) eps[c] += de[c];
-
-    // ---- triaxiality (cal_triax_stress, :995-1018) in invariant form and ductile deletion (:701-758)
-    bool kill = false;
-    if (DO_DELETE || STORE_TRIAX) {
-        const double mean = (fin[0] + fin[1] + fin[2]) / 3.0;
-        const double a01 = fin[0] - fin[1], a12 = fin[1] - fin[2], a20 = fin[2] - fin[0];
-        const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) +
-                                3.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5]));
-        const double tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
-        if (STORE_TRIAX) a.triax[gp] = tri;
-        if (nd > 0) {
-            const double v_e = allreduce8(eqp) / 8.0;
-            const double t_e = allreduce8(tri) / 8.0;
-            if (!(t_e < 0.0)) {
-                double fr = M->du_eps[nd - 1];
-                for (int j = 0; j + 1 < nd; ++j) {
-                    if (t_e >= M->du_tri[j] && t_e < M->du_tri[j + 1]) {
-                        fr = M->du_eps[j] + (M->du_eps[j + 1] - M->du_eps[j]) / (M->du_tri[j + 1] - M->du_tri[j]) *
-                                                (t_e - M->du_tri[j]);
-                        break;
-                    }
-                }
-                kill = v_e >= fr;
-            }
+            kill = active && v_e >= fr;
         }
     }
 
-    // ---- internal force (Qe[:,e] += detJ * Bfinal' * sigma, :1330-1340), reduce-scattered so lane k
-    // writes the 3 components of local node k.
-    const double tr3 = (fin[0] + fin[1] + fin[2]) / 3.0;
+    // ---- internal force (Qe[:,e] += detJ * Bfinal' * sigma, :1330-1340), reduce-scattered so
+    // lane k writes the 3 components of local node k.
     double fk[3];
     {
+        const double w00 = det * dv0, w11 = det * dv1, w22 = det * dv2;
+        const double w01 = det * fin[3], w12 = det * fin[4], w02 = det * fin[5];
         double v[8][3];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const double px = P[i][0], py = P[i][1], pz = P[i][2];
-            v[i][0] = det * (fin[0] * px + fin[3] * py + fin[5] * pz - px * tr3);
-            v[i][1] = det * (fin[3] * px + fin[1] * py + fin[4] * pz - py * tr3);
-            v[i][2] = det * (fin[5] * px + fin[4] * py + fin[2] * pz - pz * tr3);
+            v[i][0] = w00 * px + w01 * py + w02 * pz;
+            v[i][1] = w01 * px + w11 * py + w12 * pz;
+            v[i][2] = w02 * px + w12 * py + w22 * pz;
         }
         reduce_scatter8(v, fk, k);
     }
-    const double S = allreduce8(det * (3.0 * tr3));
-    double* fo = a.fe + 24 * e + 3 * k;
-    fo[0] = fk[0] + S * bb0;
-    fo[1] = fk[1] + S * bb1;
-    fo[2] = fk[2] + S * bb2;
-    if (a.vol && k == 0) a.vol[e] = V;
+    const double S = allreduce8(det * (3.0 * mean));
 
-    // ---- state write-back (:1281-1282, :1304-1323); deletion zeroes stress/strain (:742-756)
-    if (kill) {
+    // ---- unconditional write-back (selects, no branches)
+    double* fo = a.fe + 24 * e + 3 * k;
+    fo[0] = active ? fk[0] + S * bb0 : 0.0;
+    fo[1] = active ? fk[1] + S * bb1 : 0.0;
+    fo[2] = active ? fk[2] + S * bb2 : 0.0;
+    if (WITH_VOL) a.vol[e] = V;
+    // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            fin[c] = 0.0;
-            eps[c] = 0.0;
-        }
-        if (k == 0) {
-            a.flag[e] = 2;
-            const int slot = atomicAdd(a.del_count, 1);
-            if (slot < a.del_cap) {
-                a.del_log[2 * slot + 0] = (long long)a.t_step;
-                a.del_log[2 * slot + 1] = e + 1;
-            }
-        }
+    for (int c = 0; c < 6; ++c) {
+        a.stress[c * ld + gp] = kill ? 0.0 : (active ? fin[c] : in.sig[c]);
+        a.strain[c * ld + gp] = kill ? 0.0 : (active ? eps[c] : in.eps[c]);
     }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) a.stress[c * ld + gp] = fin[c];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) a.strain[c * ld + gp] = eps[c];
-    if (npp > 0) {
-        a.eqps[gp] = eqp;
-        a.yield[gp] = ys;
+    if (ANY_PLASTIC) {
+        a.eqps[gp] = active ? eqp : in.eqp;
+        a.yield[gp] = active ? ys : in.ys;
+    }
+    if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
+    if (DO_DELETE) {
+        a.flag[e] = kill ? 2 : (in.fl == 2 ? 0 : in.fl);        // 8 lanes, same value
+        int* ds = kill ? a.del_step + e : a.del_step + a.nEp;  // deletion step, or a dump slot
+        *ds = a.step_i;
+    }
+}
+
+// One batch of 32 elements per block (simple form; used by the literal drop-in and for A/B).
+template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
+    __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
+    const int k = threadIdx.x & 7;
+    const int grp = threadIdx.x >> 3;
+    const long long e = (long long)xcd_remap(blockIdx.x, gridDim.x) * kEPB + grp;
+    ElemIn in;
+    load_stage_a(a, e, k, in);
+    load_stage_b<true>(a, e, k, in);
+    elem_step<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride, in);
+}
+
+// Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
+// issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
+// before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
+// Material tables are staged in LDS (segment searches hit LDS, not L2).
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS>
+__global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
+    __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
+    __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
+    const int k = threadIdx.x & 7;
+    const int grp = threadIdx.x >> 3;
+    if (LDS_MATS) {
+        const int words = a.nmat * (int)(sizeof(DevMat) / sizeof(double));
+        const double* src = reinterpret_cast<const double*>(a.mats);
+        double* dst = reinterpret_cast<double*>(s_mats);
+        for (int w = threadIdx.x; w < words; w += kBlock) dst[w] = src[w];
+        __syncthreads();
+    }
+    const DevMat* mats = LDS_MATS ? s_mats : a.mats;
+    double* nd8 = s_nd + grp * kLdsStride;
+    const long long nb = a.nEp / kEPB;
+    const long long lb = xcd_remap(blockIdx.x, gridDim.x);
+    const long long b0 = lb * nb / gridDim.x, b1 = (lb + 1) * nb / gridDim.x;
+    if (b0 >= b1) return;  // block-uniform
+    // batches past the end are clamped to the last one (loaded, never computed)
+    auto elem_of = [&](long long b) { return (b < b1 ? b : b1 - 1) * kEPB + grp; };
+
+    ElemIn cur, nxt;
+    load_stage_a(a, elem_of(b0), k, cur);
+    load_stage_a(a, elem_of(b0 + 1), k, nxt);
+    load_stage_b<ANY_PLASTIC>(a, elem_of(b0), k, cur);
+    for (long long b = b0; b < b1; ++b) {
+        ElemIn nn;
+        load_stage_a(a, elem_of(b + 2), k, nn);
+        load_stage_b<ANY_PLASTIC>(a, elem_of(b + 1), k, nxt);
+        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false>(a, mats, elem_of(b), k, nd8, cur);
+        cur = nxt;
+        nxt = nn;
+    }
+}
+
+template <int MINW>
+static void launch_element_w(const ElemArgs& a, bool do_delete, bool store_triax, bool with_vol, unsigned grid,
+                             hipStream_t s) {
+    if (with_vol) {
+        hipLaunchKernelGGL((k_element<false, false, true, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+    } else if (do_delete) {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element<true, true, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element<true, false, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+    } else {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element<false, true, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element<false, false, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+    }
+}
+
+template <bool ANY_PLASTIC, bool LDS_MATS>
+static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (do_delete) {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
+    } else {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
     }
 }
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
     if (a.nE <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)((a.nE + kEPB - 1) / kEPB);
-    if (do_delete) {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element<true, true>), dim3(grid), dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element<true, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    } else {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element<false, true>), dim3(grid), dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element<false, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    const long long nb = a.nEp / kEPB;
+    if (a.pipe_blocks > 0 && !a.vol) {
+        const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
+        const bool lds = a.nmat <= kMaxLdsMats;
+        if (a.any_plastic) {
+            if (lds) launch_element_p<true, true>(a, do_delete, store_triax, grid, s);
+            else launch_element_p<true, false>(a, do_delete, store_triax, grid, s);
+        } else {
+            if (lds) launch_element_p<false, true>(a, do_delete, store_triax, grid, s);
+            else launch_element_p<false, false>(a, do_delete, store_triax, grid, s);
+        }
+        return hipGetLastError();
     }
+    const unsigned grid = (unsigned)nb;
+    switch (a.variant) {
+        case 3: launch_element_w<3>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        case 4: launch_element_w<4>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        default: launch_element_w<2>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+    }
+    return hipGetLastError();
+}
+
+// Negative-Jacobian diagnostic (the reference prints a warning, v2/HAKAI_j.jl:1736-1739): counts
+// Gauss points of active elements with det J < 0 at the current configuration. Off the hot path.
+__global__ void k_negjac(ElemArgs a, unsigned long long* count) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 8 * a.nE) return;
+    const long long e = t >> 3;
+    const int k = t & 7;
+    if (a.flag[e] != 1) return;
+    const double g = 1.0 / __builtin_sqrt(3.0);
+    const double gz = (k & 4) ? g : -g, et = (k & 2) ? g : -g, tu = (k & 1) ? g : -g;
+    double J[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
+    for (int i = 0; i < 8; ++i) {
+        const long long n = a.conn[8 * e + i];
+        const double p0 = 0.125 * kSx[i] * (1.0 + et * kSy[i]) * (1.0 + tu * kSz[i]);
+        const double p1 = 0.125 * kSy[i] * (1.0 + gz * kSx[i]) * (1.0 + tu * kSz[i]);
+        const double p2 = 0.125 * kSz[i] * (1.0 + gz * kSx[i]) * (1.0 + et * kSy[i]);
+        for (int c = 0; c < 3; ++c) {
+            const double X = a.coord[3 * n + c] + a.u[3 * n + c];
+            J[0][c] += p0 * X;
+            J[1][c] += p1 * X;
+            J[2][c] += p2 * X;
+        }
+    }
+    const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) +
+                       J[0][1] * (J[1][2] * J[2][0] - J[1][0] * J[2][2]) +
+                       J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+    if (det < 0.0) atomicAdd(count, 1ull);
+}
+
+hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s) {
+    if (a.nE <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_negjac, dim3((unsigned)((8 * a.nE + 255) / 256)), dim3(256), 0, s, a, count);
     return hipGetLastError();
 }
 
@@ -306,25 +447,12 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
 // (v2/HAKAI_j.jl:669-675) -- deterministic, no atomics, bit-identical Q.
 // The update expression is the reference's (:564) with diag_C = 0 (:217-218), evaluated without
 // contraction so it matches the reference bit for bit.
+// Fast path: a padded [nN][8] incidence table (16-B vector loads, all 8 gathers in flight; padding
+// points at a zero row of fe, and x + 0.0 == x leaves the sum unchanged). Nodes with more than 8
+// incidences (unstructured meshes) use the CSR path.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
+__device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, double Q0, double Q1, double Q2) {
 #pragma clang fp contract(off)
-    const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
-    if (n >= a.nN) return;
-    double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0;
-    if (a.qbuf) {
-        Q0 = a.qbuf[3 * n + 0];
-        Q1 = a.qbuf[3 * n + 1];
-        Q2 = a.qbuf[3 * n + 2];
-    } else {
-        const int j0 = a.inc_ptr[n], j1 = a.inc_ptr[n + 1];
-        for (int j = j0; j < j1; ++j) {
-            const double* f = a.fe + 3 * (long long)a.inc[j];
-            Q0 += f[0];
-            Q1 += f[1];
-            Q2 += f[2];
-        }
-    }
     const double m = a.mass[n];
     const double dt = a.dt;
     const double dC = 0.0 * m;  // diag_C .= diag_M * C, C = 0
@@ -338,6 +466,45 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
         const double up = a.u_pre_out[3 * n + c];
         a.u_pre_out[3 * n + c] = inv * (f - Q[c] + mdt2 * (2.0 * uc - up) + dC / 2.0 / dt * up);
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
+#pragma clang fp contract(off)
+    const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    if (n >= a.nN) return;
+    double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0;
+    if (a.qbuf) {
+        Q0 = a.qbuf[3 * n + 0];
+        Q1 = a.qbuf[3 * n + 1];
+        Q2 = a.qbuf[3 * n + 2];
+    } else if (a.inc8) {
+        const int4 lo = reinterpret_cast<const int4*>(a.inc8)[2 * n];
+        const int4 hi = reinterpret_cast<const int4*>(a.inc8)[2 * n + 1];
+        const int idx[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        double f[8][3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const double* p = a.fe + 3 * (long long)idx[j];
+            f[j][0] = p[0];
+            f[j][1] = p[1];
+            f[j][2] = p[2];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            Q0 += f[j][0];
+            Q1 += f[j][1];
+            Q2 += f[j][2];
+        }
+    } else {
+        const int j0 = a.inc_ptr[n], j1 = a.inc_ptr[n + 1];
+        for (int j = j0; j < j1; ++j) {
+            const double* f = a.fe + 3 * (long long)a.inc[j];
+            Q0 += f[0];
+            Q1 += f[1];
+            Q2 += f[2];
+        }
+    }
+    nodal_update(a, n, Q0, Q1, Q2);
 }
 
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
@@ -432,9 +599,9 @@ hipError_t launch_soa_to_aos6(const double* soa, double* aos, long long nGP, lon
 }
 
 __global__ void k_reset_gp(double* stress, double* strain, double* eqps, double* yield, double* triax, int* flag,
-                           const int* mat, const DevMat* mats, long long nE, long long ld) {
+                           const int* mat, const DevMat* mats, long long nE, long long nEp, long long ld) {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= 8 * nE) return;
+    if (g >= 8 * nEp) return;
     const long long e = g >> 3;
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -444,15 +611,15 @@ __global__ void k_reset_gp(double* stress, double* strain, double* eqps, double*
     eqps[g] = 0.0;
     triax[g] = 0.0;
     const DevMat* M = mats + mat[e];
-    yield[g] = (M->npp > 0) ? M->yield0 : 0.0;
-    if ((g & 7) == 0) flag[e] = 1;
+    yield[g] = (e < nE && M->npp > 0) ? M->yield0 : 0.0;
+    if ((g & 7) == 0) flag[e] = e < nE ? 1 : 0;  // padding elements behave as deleted
 }
 
 hipError_t launch_reset_gp(double* stress, double* strain, double* eqps, double* yield, double* triax, int* flag,
-                           const int* mat, const DevMat* mats, long long nE, long long ld, hipStream_t s) {
-    if (nE <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_reset_gp, dim3((unsigned)((8 * nE + 255) / 256)), dim3(256), 0, s, stress, strain, eqps,
-                       yield, triax, flag, mat, mats, nE, ld);
+                           const int* mat, const DevMat* mats, long long nE, long long nEp, long long ld, hipStream_t s) {
+    if (nEp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reset_gp, dim3((unsigned)((8 * nEp + 255) / 256)), dim3(256), 0, s, stress, strain, eqps,
+                       yield, triax, flag, mat, mats, nE, nEp, ld);
     return hipGetLastError();
 }
 

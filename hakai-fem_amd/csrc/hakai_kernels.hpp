@@ -22,13 +22,15 @@ struct ElemArgs {
     double* triax;         // [ld]
     double* fe;            // element nodal forces [nE][8][3] (= Qe column of the reference)
     double* vol;           // optional current volume per element (elementVolume, :1169)
-    long long nE;
-    long long ld;
-    int* del_count;
-    long long* del_log;    // (step, element 1-based) pairs
-    int del_cap;
-    double t_step;
-    unsigned long long* negjac;
+    long long nE;          // elements
+    long long nEp;         // elements padded to whole 32-element batches (padding: flag 0)
+    long long ld;          // Gauss-point stride of the SoA arrays (8 nEp)
+    int* del_step;         // [nEp+1] step at which each element was deleted (0 = never); [nEp] = dump
+    int step_i;            // current step number
+    int any_plastic;       // some material has a *Plastic table (eqps/yield are live)
+    int variant;           // occupancy variant of the simple kernel: min waves per SIMD (2, 3, 4)
+    int pipe_blocks;        // > 0: persistent pipelined kernel with this many blocks
+    int nmat;               // materials (staged in LDS when <= kMaxLdsMats)
 };
 
 struct NodalArgs {
@@ -37,6 +39,7 @@ struct NodalArgs {
     const double* mass;    // per node lumped mass (diag_M of each dof)
     const int* inc_ptr;    // CSR node -> incidences (8e+i), ascending element order
     const int* inc;
+    const int* inc8;       // padded [nN][8] table (pad -> zero row 8nEp) or null (use CSR)
     const double* fe;
     const double* qbuf;    // if non-null: Q taken from this 3nN buffer (uploaded state), not from fe
     const double* fext;    // external force 3nN or null (= 0)
@@ -58,6 +61,7 @@ struct BCArgs {
 };
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
+hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s);
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s);
 hipError_t launch_bc(const BCArgs& a, hipStream_t s);
 
@@ -69,7 +73,7 @@ hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, lon
 hipError_t launch_soa_to_aos6(const double* soa, double* aos, long long nGP, long long ld, hipStream_t s);
 // Fresh state: stress/strain/eqps/triax 0, yield from material, flags 1.
 hipError_t launch_reset_gp(double* stress, double* strain, double* eqps, double* yield, double* triax, int* flag,
-                           const int* mat, const DevMat* mats, long long nE, long long ld, hipStream_t s);
+                           const int* mat, const DevMat* mats, long long nE, long long nEp, long long ld, hipStream_t s);
 // Stand-alone triaxiality (cal_triax_stress) on an AoS [gp][6] stress array.
 hipError_t launch_triax_aos(const double* stress_aos, double* triax, long long nGP, hipStream_t s);
 // Output: node averages of GP quantities (cal_node_stress_strain).

@@ -151,10 +151,16 @@ class Solver:
         check(self.L.hakai_profile_read(self.ctx, kernel, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def set_tuning(self, key: str, value: int):
+        check(self.L.hakai_set_tuning(self.ctx, key.encode(), int(value)))
+
     # -- multi-GPU ---------------------------------------------------------------------------------
     def comm_init(self, rank: int, nranks: int, uid: bytes):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.L.hakai_comm_init(self.ctx, rank, nranks, buf))
+
+    def set_element_offset(self, offset: int):
+        check(self.L.hakai_set_element_offset(self.ctx, int(offset)))
 
     def set_interface(self, local_node: np.ndarray, rank_lo: np.ndarray, rank_hi: np.ndarray):
         ln = np.ascontiguousarray(local_node, np.int64)

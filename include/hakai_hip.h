@@ -115,7 +115,8 @@ int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
 int hakai_deleted(hakai_ctx* ctx, int64_t* n_deleted, int64_t* log, int64_t cap);
-/* Negative-Jacobian events seen by the element kernel (reference prints a warning, :1736-1739). */
+/* Gauss points of active elements with det J < 0 in the current configuration (the reference
+ * prints a warning and takes |det J|, :1736-1739). Diagnostic, runs a separate kernel. */
 int hakai_negative_jacobians(hakai_ctx* ctx, int64_t* n);
 
 /* GP -> node averages for output, on device (cal_node_stress_strain, v2/HAKAI_j.jl:3408-3486).
@@ -148,6 +149,10 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
 enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_COUNT = 4 };
 int hakai_profile_enable(hakai_ctx* ctx, int on);
 int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
+/* Tuning knobs for A/B measurements: "elem_pipe_blocks" (>0: persistent software-pipelined
+ * element kernel on that many blocks, default 512; 0: one-batch-per-block kernel), "elem_minw"
+ * (2|3|4: occupancy variant of the one-batch kernel), "nodal_padded" (0: CSR gather). */
+int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: one process per GPU, contiguous element ranges, RCCL over xGMI -------------- */
 int hakai_comm_unique_id(uint8_t id[128]);
@@ -158,6 +163,8 @@ int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128])
  * whose elements touch each node (hi == lo+1 for slab partitions). */
 int hakai_set_interface(hakai_ctx* ctx, int64_t n_shared, const int64_t* local_node, const int32_t* rank_lo,
                         const int32_t* rank_hi);
+/* Global id offset of this rank's element 0 (deletion log reports global 1-based ids). */
+int hakai_set_element_offset(hakai_ctx* ctx, int64_t element_offset);
 
 /* ---- driver surface: .inp reader, VTK writer, HAKAI(fname) ---------------------------------- */
 /* Flattened ModelType (v2/readInpFile_j.jl:129-150) as the solver consumes it. Owned by the

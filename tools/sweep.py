@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""A/B timing of tuning variants on C3 in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+  python tools/sweep.py --variants "simple:elem_pipe_blocks=0;pipe512:elem_pipe_blocks=512"
+Each variant is name:key=value[,key=value]; keys are hakai_set_tuning keys. Prints the median and
+min per-step kernel times (HIP events) and whole-step wall time per variant."""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hakai-fem_amd"))
+from hakai import mesh  # noqa: E402
+from hakai._abi import K_ELEMENT, K_NODAL  # noqa: E402
+from hakai.solver import Solver  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--layers", type=int, default=5000)
+ap.add_argument("--steps", type=int, default=40)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--variants", default="simple:elem_pipe_blocks=0;pipe512:elem_pipe_blocks=512")
+a = ap.parse_args()
+
+variants = []
+for spec in a.variants.split(";"):
+    name, _, kv = spec.partition(":")
+    settings = [(k, int(v)) for k, v in (x.split("=") for x in kv.split(",") if x)]
+    variants.append((name, settings))
+
+m = mesh.bar_model(20, 20, a.layers, mesh.steel_ductile(), lambda z, L: 5e5 * z / L, name="C3")
+diag, _ = m.lumped_mass()
+sv = Solver(m, diag_M=diag)
+sv.step(1, 400)
+sv.sync()
+t = 401
+res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
+for r in range(a.rounds):
+    for name, settings in variants:
+        for k, v in settings:
+            sv.set_tuning(k, v)
+        sv.profile(True)
+        sv.sync()
+        t0 = time.perf_counter()
+        sv.step(t, a.steps)
+        sv.sync()
+        dt = time.perf_counter() - t0
+        t += a.steps
+        el, nd = sv.profile_read(K_ELEMENT), sv.profile_read(K_NODAL)
+        sv.profile(False)
+        res[name]["el"].append(el[0] / el[1])
+        res[name]["nd"].append(nd[0] / nd[1])
+        res[name]["step"].append(dt / a.steps * 1e3)
+for name, d in res.items():
+    print(f"{name:10s} element {statistics.median(d['el']):.4f} ms (min {min(d['el']):.4f})  "
+          f"nodal {statistics.median(d['nd']):.4f} ms  step {statistics.median(d['step']):.4f} ms")
