@@ -600,6 +600,8 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step before upload_model/reset_state");
     if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step: n_steps=%lld d_time=%g", (long long)n_steps, d_time);
+    if (n_steps > 1 && hkc::comm_is_local(c))
+        return fail(HAKAI_ERR_ARG, "step: an in-process group is stepped one step per call, rank by rank");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     for (int64_t it = 0; it < n_steps; ++it) {
@@ -651,7 +653,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
         HIPCHK(hk::launch_element(ea, c->has_ductile, it == n_steps - 1, s));
         hkc::prof_end(c, &ep);
-        rc = hkc::comm_post_element(c);
+        rc = hkc::comm_post_element(c, (long long)t);
         if (rc) return rc;
         c->steps_done++;
         c->last_dt = d_time;

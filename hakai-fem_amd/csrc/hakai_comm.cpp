@@ -1,4 +1,5 @@
-// hakai_comm.cpp -- multi-GPU interface exchange over RCCL (xGMI), one process per GPU.
+// hakai_comm.cpp -- multi-GPU interface exchange, one process per GPU over RCCL (xGMI), or an
+// in-process group of contexts (tests, several subdomains per device).
 //
 // Elements are partitioned into contiguous global-id ranges, one per rank (z-slabs for the
 // synthetic bars). A node on the boundary between rank r (lower element ids) and r+1 is present
@@ -10,32 +11,51 @@
 // and BOTH ranks form Q = ((P_r + c_1) + c_2) + ... , i.e. exactly the single-GPU summation, so an
 // N-GPU run is bit-identical to the 1-GPU run. One grouped ncclSend/ncclRecv round per step on a
 // second stream; the interior nodal update runs meanwhile and only the interface nodes wait.
+// Send buffers alternate by step parity so a receiver may pull step t's data while the sender
+// already packs step t+1 (needed by the in-process transport, harmless for RCCL).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "hakai_internal.hpp"
 
 namespace hkc {
 
+struct LocalGroup;
+
 struct Comm {
+    int mode = 0;  // 0 RCCL, 1 in-process group
     ncclComm_t nc = nullptr;
+    LocalGroup* group = nullptr;
+    long long group_key = 0;
     int rank = 0, nranks = 1;
     hipStream_t cs = nullptr;
-    hipEvent_t ev_packed = nullptr, ev_done = nullptr;
+    hipEvent_t ev_packed[2] = {nullptr, nullptr}, ev_done = nullptr;
     int nslot = 0;
-    int n_up = 0, n_dn = 0;      // up: this rank is the lower side (neighbour rank+1); dn: upper side
-    int* d_up = nullptr;         // local node ids
+    int n_up = 0, n_dn = 0;          // up: this rank is the lower side (neighbour rank+1); dn: upper side
+    int* d_up = nullptr;             // local node ids
     int* d_dn = nullptr;
-    double* d_up_sendP = nullptr;   // [n_up][3]
-    double* d_up_recvC = nullptr;   // [n_up][nslot][3]
-    double* d_dn_sendC = nullptr;   // [n_dn][nslot][3]
-    double* d_dn_recvP = nullptr;   // [n_dn][3]
-    double* d_saved = nullptr;      // u_pre of interface nodes [n_up+n_dn][3]
+    double* d_up_sendP[2] = {nullptr, nullptr};  // [n_up][3]
+    double* d_up_recvC = nullptr;                // [n_up][nslot][3]
+    double* d_dn_sendC[2] = {nullptr, nullptr};  // [n_dn][nslot][3]
+    double* d_dn_recvP = nullptr;                // [n_dn][3]
+    double* d_saved = nullptr;                   // u_pre of interface nodes [n_up+n_dn][3]
     bool pending = false;
+    int pending_par = 0;
 };
+
+struct LocalGroup {
+    int nranks = 0;
+    std::vector<hakai_ctx*> ctx;
+    int refs = 0;
+};
+
+static std::mutex g_groups_mu;
+static std::map<long long, LocalGroup*> g_groups;
 
 }  // namespace hkc
 
@@ -157,13 +177,34 @@ void dfree(T*& p) {
 void free_iface(hkc::Comm* m) {
     dfree(m->d_up);
     dfree(m->d_dn);
-    dfree(m->d_up_sendP);
+    for (int p = 0; p < 2; ++p) {
+        dfree(m->d_up_sendP[p]);
+        dfree(m->d_dn_sendC[p]);
+    }
     dfree(m->d_up_recvC);
-    dfree(m->d_dn_sendC);
     dfree(m->d_dn_recvP);
     dfree(m->d_saved);
     m->n_up = m->n_dn = 0;
     m->pending = false;
+}
+
+hkc::Comm* peer(hkc::Comm* m, int r) {
+    if (!m->group || r < 0 || r >= m->nranks) return nullptr;
+    hakai_ctx* c = m->group->ctx[r];
+    return c ? c->comm : nullptr;
+}
+
+int comm_common_init(hakai_ctx* c, hkc::Comm* m) {
+    if (hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_packed[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_packed[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess) {
+        c->comm = m;
+        hkc::comm_destroy(c);
+        return fail(HAKAI_ERR_DEVICE, "comm_init: stream/event creation failed");
+    }
+    c->comm = m;
+    return 0;
 }
 
 }  // namespace
@@ -174,13 +215,27 @@ void comm_destroy(hakai_ctx* c) {
     Comm* m = c->comm;
     if (!m) return;
     if (m->cs) (void)hipStreamSynchronize(m->cs);
+    (void)hipStreamSynchronize(c->stream);
     free_iface(m);
     if (m->nc) (void)ncclCommDestroy(m->nc);
-    if (m->ev_packed) (void)hipEventDestroy(m->ev_packed);
+    if (m->group) {
+        std::lock_guard<std::mutex> lk(g_groups_mu);
+        m->group->ctx[m->rank] = nullptr;
+        if (--m->group->refs == 0) {
+            g_groups.erase(m->group_key);
+            delete m->group;
+        }
+    }
+    for (int p = 0; p < 2; ++p)
+        if (m->ev_packed[p]) (void)hipEventDestroy(m->ev_packed[p]);
     if (m->ev_done) (void)hipEventDestroy(m->ev_done);
     if (m->cs) (void)hipStreamDestroy(m->cs);
     delete m;
     c->comm = nullptr;
+}
+
+bool comm_is_local(const hakai_ctx* c) {
+    return c->comm && c->comm->mode == 1 && c->comm->n_up + c->comm->n_dn > 0;
 }
 
 int comm_reset(hakai_ctx* c) {
@@ -202,40 +257,63 @@ int comm_post_nodal(hakai_ctx* c, double d_time) {
     Comm* m = c->comm;
     if (!m || m->n_up + m->n_dn == 0 || !m->pending) return 0;
     m->pending = false;
-    HIPCHK(hipStreamWaitEvent(c->stream, m->ev_done, 0));
-    if (c->q_from_buf) return 0;  // uploaded Q already holds the global sum
-    const int n = m->n_up + m->n_dn;
+    const int par = m->pending_par;
     EventPair ep;
     prof_begin(c, HAKAI_K_EXCHANGE, &ep);
-    hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
-                       c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP, m->d_up_recvC, m->d_dn_recvP, m->d_saved,
-                       c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, d_time);
+    if (m->mode == 0) {
+        HIPCHK(hipStreamWaitEvent(c->stream, m->ev_done, 0));
+    } else {  // pull the neighbours' packed buffers of the previous step
+        if (m->n_up) {
+            Comm* p = peer(m, m->rank + 1);
+            if (!p) return fail(HAKAI_ERR_COMM, "local group: rank %d missing", m->rank + 1);
+            HIPCHK(hipStreamWaitEvent(c->stream, p->ev_packed[par], 0));
+            HIPCHK(hipMemcpyAsync(m->d_up_recvC, p->d_dn_sendC[par], sizeof(double) * 3 * m->nslot * m->n_up,
+                                  hipMemcpyDeviceToDevice, c->stream));
+        }
+        if (m->n_dn) {
+            Comm* p = peer(m, m->rank - 1);
+            if (!p) return fail(HAKAI_ERR_COMM, "local group: rank %d missing", m->rank - 1);
+            HIPCHK(hipStreamWaitEvent(c->stream, p->ev_packed[par], 0));
+            HIPCHK(hipMemcpyAsync(m->d_dn_recvP, p->d_up_sendP[par], sizeof(double) * 3 * m->n_dn,
+                                  hipMemcpyDeviceToDevice, c->stream));
+        }
+    }
+    if (!c->q_from_buf) {  // an uploaded Q already holds the global sum
+        const int n = m->n_up + m->n_dn;
+        hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
+                           c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
+                           m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, d_time);
+        HIPCHK(hipGetLastError());
+    }
     prof_end(c, &ep);
-    HIPCHK(hipGetLastError());
     return 0;
 }
 
-int comm_post_element(hakai_ctx* c) {
+int comm_post_element(hakai_ctx* c, long long step) {
     Comm* m = c->comm;
     if (!m || m->n_up + m->n_dn == 0) return 0;
+    const int par = (int)(step & 1);
     const int n = m->n_up + m->n_dn;
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
-                       c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP, m->d_dn_sendC);
+                       c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP[par], m->d_dn_sendC[par]);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(m->ev_packed, c->stream));
-    HIPCHK(hipStreamWaitEvent(m->cs, m->ev_packed, 0));
-    NCCLCHK(ncclGroupStart());
-    if (m->n_up) {
-        NCCLCHK(ncclSend(m->d_up_sendP, (size_t)3 * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
-        NCCLCHK(ncclRecv(m->d_up_recvC, (size_t)3 * m->nslot * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
+    HIPCHK(hipEventRecord(m->ev_packed[par], c->stream));
+    if (m->mode == 0) {
+        HIPCHK(hipStreamWaitEvent(m->cs, m->ev_packed[par], 0));
+        NCCLCHK(ncclGroupStart());
+        if (m->n_up) {
+            NCCLCHK(ncclSend(m->d_up_sendP[par], (size_t)3 * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
+            NCCLCHK(ncclRecv(m->d_up_recvC, (size_t)3 * m->nslot * m->n_up, ncclDouble, m->rank + 1, m->nc, m->cs));
+        }
+        if (m->n_dn) {
+            NCCLCHK(ncclSend(m->d_dn_sendC[par], (size_t)3 * m->nslot * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
+            NCCLCHK(ncclRecv(m->d_dn_recvP, (size_t)3 * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
+        }
+        NCCLCHK(ncclGroupEnd());
+        HIPCHK(hipEventRecord(m->ev_done, m->cs));
     }
-    if (m->n_dn) {
-        NCCLCHK(ncclSend(m->d_dn_sendC, (size_t)3 * m->nslot * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
-        NCCLCHK(ncclRecv(m->d_dn_recvP, (size_t)3 * m->n_dn, ncclDouble, m->rank - 1, m->nc, m->cs));
-    }
-    NCCLCHK(ncclGroupEnd());
-    HIPCHK(hipEventRecord(m->ev_done, m->cs));
     m->pending = true;
+    m->pending_par = par;
     return 0;
 }
 
@@ -266,15 +344,35 @@ int hakai_comm_init(hakai_ctx* c, int rank, int nranks, const uint8_t id[128]) {
         delete m;
         return fail(HAKAI_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
-    if (hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_packed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess) {
-        c->comm = m;
-        hkc::comm_destroy(c);
-        return fail(HAKAI_ERR_DEVICE, "comm_init: stream/event creation failed");
+    return comm_common_init(c, m);
+}
+
+int hakai_comm_init_local(hakai_ctx* c, int rank, int nranks, int64_t group_key) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(HAKAI_ERR_ARG, "comm_init_local: bad args");
+    HIPCHK(hipSetDevice(c->device));
+    hkc::comm_destroy(c);
+    hkc::Comm* m = new hkc::Comm();
+    m->mode = 1;
+    m->rank = rank;
+    m->nranks = nranks;
+    m->group_key = group_key;
+    {
+        std::lock_guard<std::mutex> lk(hkc::g_groups_mu);
+        hkc::LocalGroup*& g = hkc::g_groups[group_key];
+        if (!g) {
+            g = new hkc::LocalGroup();
+            g->nranks = nranks;
+            g->ctx.assign(nranks, nullptr);
+        }
+        if (g->nranks != nranks || g->ctx[rank]) {
+            delete m;
+            return fail(HAKAI_ERR_ARG, "comm_init_local: group %lld size/rank clash", (long long)group_key);
+        }
+        g->ctx[rank] = c;
+        g->refs++;
+        m->group = g;
     }
-    c->comm = m;
-    return 0;
+    return comm_common_init(c, m);
 }
 
 int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_node, const int32_t* rank_lo,
@@ -301,26 +399,35 @@ int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_nod
     }
     if ((!up.empty() && m->rank + 1 >= m->nranks) || (!dn.empty() && m->rank == 0))
         return fail(HAKAI_ERR_ARG, "set_interface: neighbour rank does not exist");
-    // slots = max incidences the upper side holds at a shared node (agreed by all ranks)
+    // Slots = max incidences the upper side holds at a shared node. For RCCL all ranks agree via an
+    // all-reduce; a local group uses the structural bound 8 (hex8: <= 8 incidences per node on
+    // structured meshes, padded with zeros, which leaves the sums unchanged).
     std::vector<int> ptr((size_t)c->nN + 1);
     HIPCHK(hipMemcpy(ptr.data(), c->d_inc_ptr, ptr.size() * sizeof(int), hipMemcpyDeviceToHost));
     int nslot = 0;
     for (int n : dn) nslot = std::max(nslot, ptr[n + 1] - ptr[n]);
-    int* d_ns = nullptr;
-    HIPCHK(dalloc(&d_ns, 1));
-    HIPCHK(hipMemcpy(d_ns, &nslot, sizeof(int), hipMemcpyHostToDevice));
-    NCCLCHK(ncclAllReduce(d_ns, d_ns, 1, ncclInt32, ncclMax, m->nc, m->cs));
-    HIPCHK(hipStreamSynchronize(m->cs));
-    HIPCHK(hipMemcpy(&nslot, d_ns, sizeof(int), hipMemcpyDeviceToHost));
-    dfree(d_ns);
+    if (m->mode == 0) {
+        int* d_ns = nullptr;
+        HIPCHK(dalloc(&d_ns, 1));
+        HIPCHK(hipMemcpy(d_ns, &nslot, sizeof(int), hipMemcpyHostToDevice));
+        NCCLCHK(ncclAllReduce(d_ns, d_ns, 1, ncclInt32, ncclMax, m->nc, m->cs));
+        HIPCHK(hipStreamSynchronize(m->cs));
+        HIPCHK(hipMemcpy(&nslot, d_ns, sizeof(int), hipMemcpyDeviceToHost));
+        dfree(d_ns);
+    } else {
+        if (nslot > 8) return fail(HAKAI_ERR_ARG, "local group: node with %d incidences on the upper side", nslot);
+        nslot = 8;
+    }
     m->nslot = nslot;
     m->n_up = (int)up.size();
     m->n_dn = (int)dn.size();
     HIPCHK(dalloc(&m->d_up, up.size()));
     HIPCHK(dalloc(&m->d_dn, dn.size()));
-    HIPCHK(dalloc(&m->d_up_sendP, 3 * up.size()));
+    for (int p = 0; p < 2; ++p) {
+        HIPCHK(dalloc(&m->d_up_sendP[p], 3 * up.size()));
+        HIPCHK(dalloc(&m->d_dn_sendC[p], 3 * (size_t)nslot * dn.size()));
+    }
     HIPCHK(dalloc(&m->d_up_recvC, 3 * (size_t)nslot * up.size()));
-    HIPCHK(dalloc(&m->d_dn_sendC, 3 * (size_t)nslot * dn.size()));
     HIPCHK(dalloc(&m->d_dn_recvP, 3 * dn.size()));
     HIPCHK(dalloc(&m->d_saved, 3 * (up.size() + dn.size())));
     if (!up.empty()) HIPCHK(hipMemcpy(m->d_up, up.data(), up.size() * sizeof(int), hipMemcpyHostToDevice));

@@ -88,5 +88,6 @@ int comm_reset(hakai_ctx* c);
 // Multi-GPU hooks used by hakai_step (no-ops without a communicator).
 int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface nodes
 int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
-int comm_post_element(hakai_ctx* c);                 // pack interface forces, start exchange
+int comm_post_element(hakai_ctx* c, long long step); // pack interface forces, start exchange
+bool comm_is_local(const hakai_ctx* c);              // in-process group with interfaces
 }  // namespace hkc

@@ -103,6 +103,7 @@ def lib() -> ctypes.CDLL:
         "hakai_set_tuning": (c_int, [c_void_p, c_char_p, c_int64]),
         "hakai_comm_unique_id": (c_int, [POINTER(c_uint8)]),
         "hakai_comm_init": (c_int, [c_void_p, c_int, c_int, POINTER(c_uint8)]),
+        "hakai_comm_init_local": (c_int, [c_void_p, c_int, c_int, c_int64]),
         "hakai_set_interface": (c_int, [c_void_p, c_int64, PI64, PI32, PI32]),
         "hakai_set_element_offset": (c_int, [c_void_p, c_int64]),
         "hakai_inp_read": (c_int, [c_char_p, POINTER(POINTER(InpModelT))]),
@@ -127,7 +128,7 @@ def exported_symbols() -> list[str]:
         "hakai_download_state", "hakai_step", "hakai_sync", "hakai_deleted", "hakai_negative_jacobians",
         "hakai_node_stress_strain", "hakai_stress_hexa", "hakai_triax_stress", "hakai_lumped_mass",
         "hakai_profile_enable", "hakai_profile_read", "hakai_set_tuning", "hakai_comm_unique_id", "hakai_comm_init",
-        "hakai_set_interface", "hakai_set_element_offset", "hakai_inp_read", "hakai_inp_free", "hakai_write_vtk", "hakai_run_inp",
+        "hakai_comm_init_local", "hakai_set_interface", "hakai_set_element_offset", "hakai_inp_read", "hakai_inp_free", "hakai_write_vtk", "hakai_run_inp",
     ]
 
 

@@ -159,6 +159,10 @@ class Solver:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.L.hakai_comm_init(self.ctx, rank, nranks, buf))
 
+    def comm_init_local(self, rank: int, nranks: int, group_key: int):
+        """Join an in-process group (same device); step the group with ``step_group``."""
+        check(self.L.hakai_comm_init_local(self.ctx, rank, nranks, int(group_key)))
+
     def set_element_offset(self, offset: int):
         check(self.L.hakai_set_element_offset(self.ctx, int(offset)))
 
@@ -168,6 +172,13 @@ class Solver:
         hi = np.ascontiguousarray(rank_hi, np.int32)
         check(self.L.hakai_set_interface(self.ctx, len(ln), ptr(ln, I64), ptr(lo, ctypes.c_int32),
                                          ptr(hi, ctypes.c_int32)))
+
+
+def step_group(solvers: list[Solver], t_first: float, n_steps: int):
+    """Advance an in-process group (hakai_comm_init_local) in lockstep: one step per rank per call."""
+    for i in range(int(n_steps)):
+        for sv in solvers:
+            sv.step(t_first + i, 1)
 
 
 def comm_unique_id() -> bytes:

@@ -158,6 +158,11 @@ int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
 int hakai_comm_unique_id(uint8_t id[128]);
 /* Attach a communicator (ncclCommInitRank) to a context created on this rank's device. */
 int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128]);
+/* In-process group: contexts in one process that pass the same group_key exchange interface
+ * forces with device copies instead of RCCL (several subdomains on one device; the same pack /
+ * sum / fix kernels as the RCCL path). The host must step all ranks in lockstep (rank 0..n-1,
+ * one hakai_step call of equal length each) on the same device. */
+int hakai_comm_init_local(hakai_ctx* ctx, int rank, int nranks, int64_t group_key);
 /* Interface description for this rank's local model ("multi-GPU"):
  * shared nodes (local 0-based ids, sorted by global id) with the rank range [lo, hi] of ranks
  * whose elements touch each node (hi == lo+1 for slab partitions). */

@@ -1,0 +1,137 @@
+"""Multi-rank path on CPU: the slab partition (hakai.dist) and the interface-exchange protocol of
+hakai_comm.cpp, run over torch.distributed `gloo` with world_size 2 and 3.
+
+The protocol claim: at a node shared by ranks r < r+1, rank r sends P = its own contributions summed
+in element order, rank r+1 sends its contributions one by one (zero padded to nslot), and both form
+((P + c1) + c2) + ... -- bit-identical to the reference's serial element-order assembly
+(v2/HAKAI_j.jl:669-675) over the whole mesh. Element forces here are seeded random vectors: the
+claim is about summation order only.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+from hakai import dist
+from util import fast_deletion_bar
+
+NX = NY = 2
+
+def _serial_Q(nN, elementmat, Qe):
+    Q = np.zeros(3 * nN)
+    for e in range(elementmat.shape[0]):
+        for i in range(8):
+            n = elementmat[e, i] - 1
+            for c in range(3):
+                Q[3 * n + c] += Qe[e, 3 * i + c]
+    return Q
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+def _worker(rank, world, port, nz, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        glob = fast_deletion_bar(NX, NY, nz)
+        loc, diag, (ln, lo, hi) = dist.slab_partition(glob, rank, world, NX, NY)
+        rng = np.random.default_rng(1234)
+        Qe_glob = rng.normal(0, 1.0, size=(glob.nElement, 24))
+        e0 = loc.global_element_offset
+        Qe = Qe_glob[e0:e0 + loc.nElement]
+        # own contributions per local node, in element order (the device CSR incidence order)
+        contrib = [[] for _ in range(loc.nNode)]
+        for e in range(loc.nElement):
+            for i in range(8):
+                contrib[loc.elementmat[e, i] - 1].append(Qe[e, 3 * i:3 * i + 3])
+        Q = np.zeros(3 * loc.nNode)
+        for n in range(loc.nNode):
+            for f in contrib[n]:
+                Q[3 * n:3 * n + 3] += f
+        up = ln[lo == rank]
+        dn = ln[hi == rank]
+        nslot = torch.tensor([max([len(contrib[n]) for n in dn], default=0)])
+        tdist.all_reduce(nslot, op=tdist.ReduceOp.MAX)
+        nslot = int(nslot)
+        P = np.array([Q[3 * n:3 * n + 3] for n in up]).reshape(-1, 3)
+        C = np.zeros((len(dn), nslot, 3))
+        for j, n in enumerate(dn):
+            for s, f in enumerate(contrib[n]):
+                C[j, s] = f
+        ops, recvC, recvP = [], None, None
+        if len(up):
+            recvC = torch.zeros(len(up), nslot, 3, dtype=torch.float64)
+            ops += [tdist.P2POp(tdist.isend, torch.from_numpy(P.copy()), rank + 1),
+                    tdist.P2POp(tdist.irecv, recvC, rank + 1)]
+        if len(dn):
+            recvP = torch.zeros(len(dn), 3, dtype=torch.float64)
+            ops += [tdist.P2POp(tdist.isend, torch.from_numpy(C.copy()), rank - 1),
+                    tdist.P2POp(tdist.irecv, recvP, rank - 1)]
+        for r in tdist.batch_isend_irecv(ops):
+            r.wait()
+        for j, n in enumerate(up):
+            q = P[j].copy()
+            for s in range(nslot):
+                q = q + recvC[j, s].numpy()
+            Q[3 * n:3 * n + 3] = q
+        for j, n in enumerate(dn):
+            q = recvP[j].numpy().copy()
+            for s in range(nslot):
+                q = q + C[j, s]
+            Q[3 * n:3 * n + 3] = q
+        Qref = _serial_Q(glob.nNode, glob.elementmat, Qe_glob)
+        n0 = loc.global_node_offset
+        gdiag, _ = glob.lumped_mass()
+        ok_q = np.array_equal(Q, Qref[3 * n0:3 * (n0 + loc.nNode)])
+        ok_m = np.array_equal(diag, gdiag[3 * n0:3 * (n0 + loc.nNode)])
+        ok_x = np.array_equal(loc.coordmat, glob.coordmat[n0:n0 + loc.nNode])
+        ok_e = np.array_equal(loc.elementmat + n0, glob.elementmat[e0:e0 + loc.nElement])
+        ret[rank] = (ok_q, ok_m, ok_x, ok_e, len(up), len(dn))
+    finally:
+        tdist.destroy_process_group()
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_interface_protocol_bitexact(world):
+    ctx = mp.get_context("spawn")
+    ret = ctx.Manager().dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 12, ret))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    for r in range(world):
+        ok_q, ok_m, ok_x, ok_e, nu, nd = ret[r]
+        assert ok_q, f"rank {r}: interface Q differs from the serial assembly"
+        assert ok_m, f"rank {r}: halo lumped mass differs from the global mass"
+        assert ok_x and ok_e
+        assert nu == (NX + 1) * (NY + 1) * (r < world - 1)
+        assert nd == (NX + 1) * (NY + 1) * (r > 0)
+
+def test_partition_covers_mesh_and_bcs():
+    glob = fast_deletion_bar(NX, NY, 12)
+    for world in (1, 2, 3, 4):
+        parts = [dist.slab_partition(glob, r, world, NX, NY) for r in range(world)]
+        assert sum(p[0].nElement for p in parts) == glob.nElement
+        # every constrained global dof appears in the local BCs of each rank holding that node
+        for loc, _, _ in parts:
+            n0 = loc.global_node_offset
+            gd = {int(d) for g in glob.bc for d, _ in g.entries for d in d
+                  if n0 <= (d - 1) // 3 < n0 + loc.nNode}
+            ld = {int(d) + 3 * n0 for g in loc.bc for d, _ in g.entries for d in d}
+            assert gd == ld
+
+def test_partition_ranges():
+    assert dist.partition_ranges(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    with pytest.raises(ValueError):
+        dist.slab_partition(fast_deletion_bar(NX, NY, 4), 1, 3, NX, NY)
