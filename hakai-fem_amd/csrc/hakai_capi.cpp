@@ -68,6 +68,7 @@ static void dfree(T*& p) {
 namespace hkc {
 
 static void free_model(hakai_ctx* c) {
+    contact_destroy(c);
     dfree(c->d_coord);
     dfree(c->d_u[0]);
     dfree(c->d_u[1]);
@@ -377,6 +378,11 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
         HIPCHK(hipMemcpyAsync(c->d_inc8, inc8.data(), inc8.size() * sizeof(int), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));  // host vectors go out of scope
+    c->h_coord.assign(coordmat, coordmat + 3 * nN);
+    c->h_conn.assign(conn.begin(), conn.begin() + 8 * nE);
+    c->h_mat.assign(mat.begin(), mat.begin() + nE);
+    c->h_young.resize((size_t)nMat);
+    for (int i = 0; i < nMat; ++i) c->h_young[i] = mats[i].young;
     c->model_ok = true;
     c->state_ok = false;
     return hakai_reset_state(c, 0, nullptr, nullptr, 1.0);
@@ -469,6 +475,8 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
         HIPCHK(hipMemcpyAsync(c->d_u[1 - c->cur], dpre.data(), fn * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    hkc::contact_state_reset(c, c->h_velo0.data());
+    HIPCHK(hipStreamSynchronize(s));
     c->state_ok = true;
     return 0;
 }
@@ -511,6 +519,11 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
         std::vector<int> f((size_t)c->nE);
         for (long long e = 0; e < c->nE; ++e) f[e] = st->element_flag[e] != 0 ? 1 : 0;
         HIPCHK(hipMemcpyAsync(c->d_flag, f.data(), c->nE * sizeof(int), hipMemcpyHostToDevice, s));
+        // deleted before the upload: step unknown (-1), never reported by hakai_deleted, but the
+        // faces its deletion exposed are live for contact
+        std::vector<int> ds((size_t)c->nE);
+        for (long long e = 0; e < c->nE; ++e) ds[e] = f[e] ? 0 : -1;
+        HIPCHK(hipMemcpyAsync(c->d_del_step, ds.data(), c->nE * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
         // fe of elements uploaded as deleted must not contribute
         std::vector<double> z;
@@ -524,6 +537,10 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
     hkc::comm_reset(c);
+    if (c->contact) {
+        hkc::contact_state_reset(c, c->h_velo0.empty() ? nullptr : c->h_velo0.data());
+        HIPCHK(hipStreamSynchronize(s));
+    }
     c->state_ok = true;
     return 0;
 }
@@ -620,7 +637,15 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.fext = nullptr;
         na.nN = c->nN;
         na.dt = d_time;
-        int rc = hkc::comm_pre_nodal(c);
+        int rc = 0;
+        if (c->contact) {  // contact force into external_force (:500-560)
+            hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
+            rc = hkc::contact_step(c, t, d_time);
+            hkc::prof_end(c, &ep);
+            if (rc) return rc;
+            na.fext = c->d_fext;
+        }
+        rc = hkc::comm_pre_nodal(c);
         if (rc) return rc;
         hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
         HIPCHK(hk::launch_nodal(na, s));
@@ -658,7 +683,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         c->steps_done++;
         c->last_dt = d_time;
     }
-    return 0;
+    return hkc::contact_check(c);
 }
 
 int hakai_sync(hakai_ctx* c) {

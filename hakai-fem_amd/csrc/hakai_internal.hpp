@@ -9,7 +9,8 @@
 #include "hakai_device.hpp"
 
 namespace hkc {
-struct Comm;  // multi-GPU state (hakai_comm.cpp)
+struct Comm;     // multi-GPU state (hakai_comm.cpp)
+struct Contact;  // contact search state (hakai_contact.hip)
 int fail(int code, const char* fmt, ...);
 int hip_fail(hipError_t e, const char* what);
 }  // namespace hkc
@@ -67,8 +68,14 @@ struct hakai_ctx {
     bool any_plastic = false;
     bool model_ok = false;
     bool state_ok = false;
+    // host copies kept for setup work that needs the mesh (contact surfaces)
+    std::vector<double> h_coord;  // 3nN
+    std::vector<int> h_conn;      // 8nE, 0-based
+    std::vector<int> h_mat;       // nE, 0-based
+    std::vector<double> h_young;  // per material
     // external force (contact) -- null until contact is enabled
     double* d_fext = nullptr;
+    hkc::Contact* contact = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -90,4 +97,9 @@ int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface 
 int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
 int comm_post_element(hakai_ctx* c, long long step); // pack interface forces, start exchange
 bool comm_is_local(const hakai_ctx* c);              // in-process group with interfaces
+// Contact (no-ops without hakai_set_contact).
+void contact_destroy(hakai_ctx* c);
+void contact_state_reset(hakai_ctx* c, const double* velo0_host);
+int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
+int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
 }  // namespace hkc

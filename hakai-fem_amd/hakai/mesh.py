@@ -92,6 +92,40 @@ def config_c5(layers: int = 1600, n: int = 100) -> Model:
     return bar_model(n, n, layers, steel_ductile(), -1e5, name=f"C5-{n}x{n}x{layers}")
 
 
+def two_body_model(plate=(8, 8, 2), impactor=(4, 4, 4), gap=0.1, v=-1e5, material: Material | None = None,
+                   perturb=0.0, seed=0, d_time=1e-7, n_steps=1000, contact_flag=1, myu=None,
+                   name="two_body") -> Model:
+    """Two instances: a plate (instance 1) clamped on its bottom face and an impactor block
+    (instance 2) above it, centred in x/y, `gap` mm away, with initial velocity v along z.
+    All-exterior contact (*Contact, no *Contact Pair). myu overrides the reference's friction 0.25
+    (BASELINE C4 runs frictionless: myu=0)."""
+    mat = material or steel_ductile()
+    px, py, pz = plate
+    ix, iy, iz = impactor
+    c1, e1 = hex_bar(px, py, pz, perturb=perturb, seed=seed)
+    c2, e2 = hex_bar(ix, iy, iz, perturb=perturb, seed=seed + 1, z0=pz + gap)
+    c2[:, 0] += (px - ix) / 2.0
+    c2[:, 1] += (py - iy) / 2.0
+    n1 = c1.shape[0]
+    coord = np.concatenate([c1, c2])
+    elem = np.concatenate([e1, e2 + n1])
+    inst = np.concatenate([np.ones(e1.shape[0], np.int64), np.full(e2.shape[0], 2, np.int64)])
+    imp_nodes = np.arange(n1 + 1, coord.shape[0] + 1, dtype=np.int64)
+    params = None if myu is None else (float(myu), 1.0, 1.0, 0.0, 0.0)
+    return Model(coord, elem, np.ones(elem.shape[0], np.int64), [mat], bc=[encastre(plane_nodes(px, py, 0))],
+                 ic_dofs=imp_nodes * 3, ic_values=np.full(imp_nodes.shape[0], float(v)), d_time=d_time,
+                 end_time=d_time * n_steps, contact_flag=contact_flag, element_instance=inst, name=name,
+                 contact_params=params)
+
+
+def config_c4(scale: int = 1) -> Model:
+    """C4: plate 200x200x50 + impactor 100x100x200 (2 M hex each), gap 0.1 mm, impactor
+    v = -1e5 mm/s, elastoplastic steel, all-exterior contact, frictionless (myu = 0).
+    scale > 1 divides every edge count (tests)."""
+    return two_body_model((200 // scale, 200 // scale, 50 // scale), (100 // scale, 100 // scale, 200 // scale),
+                          gap=0.1, v=-1e5, myu=0.0, name="C4")
+
+
 def tensile5e_model() -> Model:
     """The Tensile5e.inp deck (HAKAI-v0.0.0/input/Tensile5e.inp) rebuilt in code: 5 hex, 24 nodes,
     ENCASTRE on Set-2, y-displacement 10*amp on Set-3. Used when the .inp file is not at hand

@@ -51,6 +51,9 @@ class Model:
     contact_flag: int = 0
     element_instance: np.ndarray | None = None
     name: str = "model"
+    # cal_contact_force constants (myu, kc_o, kc_s, Cr_o, Cr_s); None = the reference's
+    # hard-coded (0.25, 1, 1, 0, 0) (v2/HAKAI_j.jl:2255-2259)
+    contact_params: tuple | None = None
 
     def __post_init__(self):
         self.coordmat = np.ascontiguousarray(self.coordmat, dtype=np.float64)

@@ -70,6 +70,12 @@ class Solver:
         bc, keep = model.c_bc()
         check(self.L.hakai_set_bc(self.ctx, ctypes.byref(bc)))
         del keep
+        if getattr(model, "contact_flag", 0) >= 1:
+            inst = model.element_instance
+            inst = np.ones(model.nElement, np.int64) if inst is None else np.ascontiguousarray(inst, np.int64)
+            check(self.L.hakai_set_contact(self.ctx, int(model.contact_flag), ptr(inst, I64)))
+            if getattr(model, "contact_params", None) is not None:
+                check(self.L.hakai_set_contact_params(self.ctx, *[float(x) for x in model.contact_params]))
         self.reset()
 
     # -- lifecycle ---------------------------------------------------------------------------
@@ -141,6 +147,22 @@ class Solver:
         check(self.L.hakai_node_stress_strain(self.ctx, ptr(ns), ptr(nn), ptr(ne), ptr(nm), ptr(nt)))
         return dict(node_stress=ns, node_strain=nn, node_eq_plastic_strain=ne, node_mises_stress=nm,
                     node_triax_stress=nt)
+
+    # -- contact ----------------------------------------------------------------------------------
+    def contact_info(self):
+        """Pairs [(i_instance, j_instance, n_nodes_i, n_triangles, n_nodes_j)], (min, max) element size."""
+        n = ctypes.c_int32(0)
+        info = np.zeros(5 * 4096, np.int64)
+        sizes = np.zeros(2)
+        check(self.L.hakai_contact_info(self.ctx, ctypes.byref(n), ptr(info, I64), 4096, ptr(sizes)))
+        return [tuple(int(x) for x in info[5 * p:5 * p + 5]) for p in range(n.value)], tuple(sizes)
+
+    def contact_force(self, t: float, d_time: float | None = None) -> np.ndarray:
+        """cal_contact_force at the current device state (external_force of step t), 3nN."""
+        f = np.zeros(3 * self.model.nNode)
+        check(self.L.hakai_contact_force(self.ctx, float(t), float(self.model.dt if d_time is None else d_time),
+                                         ptr(f)))
+        return f
 
     # -- profiling (HIP events on the context's own stream) ------------------------------------
     def profile(self, on: bool = True):

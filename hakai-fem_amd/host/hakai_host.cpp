@@ -583,6 +583,9 @@ void parse(const char* path, Owned& o) {
             contact_flag = 2;
             break;
         }
+    int n_contact_pairs = 0;  // explicit *Contact Pair blocks (:1063-1102)
+    for (long long i = 1; i <= n; ++i)
+        if (has(line(i), "*Contact Pair,")) ++n_contact_pairs;
 
     // ---- flatten into the C view
     o.coord = coordmat;
@@ -647,6 +650,7 @@ void parse(const char* path, Owned& o) {
     p.end_time = end_time;
     p.mass_scaling = mass_scaling;
     p.contact_flag = contact_flag;
+    p.n_contact_pairs = n_contact_pairs;
     p.bc.n_groups = (int32_t)BCS.size();
     p.bc.amp_n = o.amp_n.data();
     p.bc.amp_off = o.amp_off.data();
@@ -821,8 +825,9 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
         std::printf("nNode:%lld\nnElement:%lld\ncontact_flag:%d\n", (long long)M->nNode, (long long)M->nElement,
                     M->contact_flag);
     }
-    if (M->contact_flag >= 1)
-        return fail(HAKAI_ERR_MODEL, "%s: contact decks (*Contact) are not yet supported by the device path", fname);
+    if (M->contact_flag >= 1 && M->n_contact_pairs > 0)
+        return fail(HAKAI_ERR_MODEL, "%s: *Contact Pair surfaces are not supported yet (all-exterior contact is)",
+                    fname);
     const long long nN = M->nNode, nE = M->nElement;
     const double d_time = M->d_time * std::sqrt(M->mass_scaling);  // v2/HAKAI_j.jl:114
     const double time_num = M->end_time / d_time;
@@ -842,6 +847,7 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
                                 diag_M.data())))
         return r;
     if ((r = hakai_set_bc(c, &M->bc))) return r;
+    if (M->contact_flag >= 1 && (r = hakai_set_contact(c, M->contact_flag, M->element_instance))) return r;
     if ((r = hakai_reset_state(c, M->n_ic_dofs, M->ic_dofs, M->ic_values, d_time))) return r;
     const long long n_steps = time_num >= 1.0 ? (long long)std::floor(time_num) : 0;
     const long long d_out = (long long)std::floor(time_num / 100);  // output_num = 100 (:471-472)

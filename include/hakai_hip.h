@@ -146,13 +146,31 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
                       double mass_scaling, double* diag_M, double* elementVolume);
 
 /* ---- profiling: per-kernel device time measured with HIP events on the context's stream ---- */
-enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_COUNT = 4 };
+enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_CONTACT = 4,
+       HAKAI_K_COUNT = 5 };
 int hakai_profile_enable(hakai_ctx* ctx, int on);
 int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
 /* Tuning knobs for A/B measurements: "elem_pipe_blocks" (>0: persistent software-pipelined
  * element kernel on that many blocks, default 512; 0: one-batch-per-block kernel), "elem_minw"
  * (2|3|4: occupancy variant of the one-batch kernel), "nodal_padded" (0: CSR gather). */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
+
+/* ---- contact: all-exterior instance-vs-instance penalty contact --------- */
+/* Enables contact for the uploaded model: contact_flag as readInpFile sets it (1 = *Contact,
+ * 2 = HAKAIoption=self-contact; v2/readInpFile_j.jl:1046-1060), element_instance = instance
+ * (1-based, contiguous element blocks) of each element. Builds the exterior surfaces and pairs
+ * (v2/HAKAI_j.jl:244-421, :1944-2164) and, once, every face an element deletion can expose
+ * (:2167-2245, :766-804). *Contact Pair decks are not supported yet. Then every hakai_step
+ * computes cal_contact_force (:2248-2706) into the external force before the nodal update. */
+int hakai_set_contact(hakai_ctx* ctx, int32_t contact_flag, const int64_t* element_instance);
+/* The constants hard-coded at v2/HAKAI_j.jl:2255-2259 (defaults myu 0.25, kc_o 1, kc_s 1,
+ * Cr_o 0, Cr_s 0). BASELINE's C4 runs frictionless: myu = 0. */
+int hakai_set_contact_params(hakai_ctx* ctx, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s);
+/* Pairs (CT entries): info[5p..5p+4] = (i_instance, j_instance, #nodes_i, #triangles, #nodes_j)
+ * at setup; sizes = (elementMinSize, elementMaxSize). */
+int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t cap, double* sizes);
+/* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
+int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);
 
 /* ---- multi-GPU: one process per GPU, contiguous element ranges, RCCL over xGMI -------------- */
 int hakai_comm_unique_id(uint8_t id[128]);
@@ -193,6 +211,7 @@ typedef struct {
     const int64_t* instance_node_offset;    /* [n_instance] */
     const int64_t* instance_element_offset; /* [n_instance] */
     const int64_t* instance_nElement;       /* [n_instance] */
+    int32_t n_contact_pairs;                /* *Contact Pair blocks (explicit surfaces; not supported yet) */
 } hakai_inp_model_t;
 
 int hakai_inp_read(const char* path, hakai_inp_model_t** out);

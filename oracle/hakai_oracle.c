@@ -496,12 +496,22 @@ static double bc_amp(const hko_model* m, int32_t g, double current_time) {
 
 int hko_run(const hko_model* m, hko_state* s, const double* diag_M, double t_first, int64_t n_steps,
             int nthreads, int64_t* del_log, int64_t del_cap, int64_t* del_n) {
+    return hko_run_contact(m, s, diag_M, t_first, n_steps, nthreads, del_log, del_cap, del_n, NULL, NULL);
+}
+
+int hko_run_contact(const hko_model* m, hko_state* s, const double* diag_M, double t_first, int64_t n_steps,
+                    int nthreads, int64_t* del_log, int64_t del_cap, int64_t* del_n, hko_contact* ct,
+                    const int64_t* element_instance) {
     const int64_t nN = m->nN, nE = m->nE, fn = 3 * nN;
     const double d_time = m->d_time;
+    int64_t* deleted = ct ? (int64_t*)malloc(sizeof(int64_t) * (size_t)(nE > 0 ? nE : 1)) : NULL;
     for (int64_t it = 0; it < n_steps; ++it) {
         const double t = t_first + (double)it;
+        int64_t n_deleted = 0;
         /* :497-498 (no concentrated loads in the reader) */
         for (int64_t i = 0; i < fn; ++i) s->external_force[i] = 0.0;
+        /* :500-560 contact force into external_force */
+        if (ct) hko_contact_force(ct, s->position, s->velo, diag_M, s->element_flag, s->external_force);
         /* :562-567, diag_C = 0 (:217-218) */
         for (int64_t i = 0; i < fn; ++i) {
             const double dC = 0.0 * diag_M[i]; /* diag_C .= diag_M * C with C = 0 */
@@ -571,6 +581,7 @@ int hko_run(const hko_model* m, hko_state* s, const double* diag_M, double t_fir
             }
             if (v_e >= fr_e && s->element_flag[e] == 1) {
                 s->element_flag[e] = 0;
+                if (deleted) deleted[n_deleted++] = e + 1;
                 if (del_n) {
                     if (*del_n < del_cap) {
                         del_log[2 * *del_n + 0] = (int64_t)t;
@@ -585,7 +596,10 @@ int hko_run(const hko_model* m, hko_state* s, const double* diag_M, double t_fir
                     }
             }
         }
+        /* :766-804 surface update */
+        for (int64_t q = 0; q < n_deleted; ++q) hko_contact_element_deleted(ct, element_instance, deleted[q]);
     }
+    free(deleted);
     return 0;
 }
 

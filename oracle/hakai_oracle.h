@@ -103,6 +103,38 @@ void hko_eigvals_sym3(const double s[6], double out[3]);
 int hko_run(const hko_model* m, hko_state* s, const double* diag_M, double t_first, int64_t n_steps,
             int nthreads, int64_t* del_log, int64_t del_cap, int64_t* del_n);
 
+/* ---- contact (hakai_oracle_contact.c): all-exterior instance-vs-instance contact ---------- */
+typedef struct {
+    int64_t nN, nE;
+    const double* coordmat;          /* 3 x nN, kept by reference: must outlive the contact object */
+    const int64_t* elementmat;       /* 8 x nE, 1-based */
+    const int64_t* element_material; /* nE, 1-based */
+} hko_model_view;
+typedef struct hko_contact hko_contact;
+/* Setup v2/HAKAI_j.jl:244-421 for contact_flag >= 1 (no *Contact Pair: all exterior).
+ * element_instance: nE, 1-based, contiguous blocks; mat_young[mat] = Young's modulus. */
+hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
+                                const double* mat_young);
+void hko_contact_destroy(hko_contact* c);
+/* The constants of cal_contact_force (v2/HAKAI_j.jl:2255-2259); defaults 0.25, 1, 1, 0, 0. */
+void hko_contact_set_params(hko_contact* c, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s);
+/* external_force += contact force (Float128 accumulation, one rounding). Returns #contact events. */
+int64_t hko_contact_force(const hko_contact* c, const double* position, const double* velo, const double* diag_M,
+                          const int64_t* element_flag, double* external_force);
+/* Surface update after element e (1-based) was deleted (v2/HAKAI_j.jl:766-804). */
+void hko_contact_element_deleted(hko_contact* c, const int64_t* element_instance, int64_t e);
+double hko_contact_min_size(const hko_contact* c);
+double hko_contact_max_size(const hko_contact* c);
+int hko_contact_n_pairs(const hko_contact* c);
+/* out4 = (i_instance, j_instance, #nodes_i, #triangles); returns #nodes_j. */
+int64_t hko_contact_pair_info(const hko_contact* c, int pair, int64_t* out4);
+
+/* hko_run with contact (c may be NULL): contact force at the top of each step (:500-560) and the
+ * surface update after deletions (:766-804). element_instance is needed only with contact. */
+int hko_run_contact(const hko_model* m, hko_state* s, const double* diag_M, double t_first, int64_t n_steps,
+                    int nthreads, int64_t* del_log, int64_t del_cap, int64_t* del_n, hko_contact* c,
+                    const int64_t* element_instance);
+
 /* cal_node_stress_strain (v2/HAKAI_j.jl:3408-3486). node_stress/strain are nN x 6 row-major
  * like the reference's (nNode,6) Julia arrays read row-wise. */
 void hko_node_stress_strain(int64_t nN, int64_t nE, const int64_t* elementmat,

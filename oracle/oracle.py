@@ -26,6 +26,11 @@ class BC(ctypes.Structure):
                 ("amp_value", PD), ("entry_off", PI64), ("entry_value", PD), ("dof_off", PI64), ("dofs", PI64)]
 
 
+class View(ctypes.Structure):
+    _fields_ = [("nN", c_int64), ("nE", c_int64), ("coordmat", PD), ("elementmat", PI64),
+                ("element_material", PI64)]
+
+
 class St(ctypes.Structure):
     _fields_ = [(n, PD) for n in ("disp", "disp_pre", "disp_new", "d_disp", "velo", "position", "Q", "Qe",
                                   "external_force", "integ_stress", "integ_strain", "integ_yield_stress",
@@ -54,6 +59,23 @@ def lib():
         L.hko_run.argtypes = [c_void_p, POINTER(St), PD, c_double, c_int64, c_int, PI64, c_int64, PI64]
         L.hko_node_stress_strain.argtypes = [c_int64, c_int64, PI64, PD, PD, PD, PD, PD, PD, PD, PD, PD]
         L.hko_pusai.argtypes = [PD]
+        L.hko_contact_create.restype = c_void_p
+        L.hko_contact_create.argtypes = [POINTER(View), c_int, PI64, PD]
+        L.hko_contact_destroy.argtypes = [c_void_p]
+        L.hko_contact_set_params.argtypes = [c_void_p, c_double, c_double, c_double, c_double, c_double]
+        L.hko_contact_force.restype = c_int64
+        L.hko_contact_force.argtypes = [c_void_p, PD, PD, PD, PI64, PD]
+        L.hko_contact_element_deleted.argtypes = [c_void_p, PI64, c_int64]
+        L.hko_contact_min_size.restype = c_double
+        L.hko_contact_min_size.argtypes = [c_void_p]
+        L.hko_contact_max_size.restype = c_double
+        L.hko_contact_max_size.argtypes = [c_void_p]
+        L.hko_contact_n_pairs.restype = c_int
+        L.hko_contact_n_pairs.argtypes = [c_void_p]
+        L.hko_contact_pair_info.restype = c_int64
+        L.hko_contact_pair_info.argtypes = [c_void_p, c_int, PI64]
+        L.hko_run_contact.argtypes = [c_void_p, POINTER(St), PD, c_double, c_int64, c_int, PI64, c_int64, PI64,
+                                      c_void_p, PI64]
         _L = L
     return _L
 
@@ -105,6 +127,34 @@ class Oracle:
             self.s["disp_pre"][d - 1] = -v * dt
             self.s["velo"][d - 1] = v
         self.deletions = []
+        self.ct = None
+        if getattr(model, "contact_flag", 0) >= 1:
+            inst = getattr(model, "element_instance", None)
+            self._inst = np.ascontiguousarray(inst if inst is not None else np.ones(nE, np.int64), np.int64)
+            self._young = np.array([mt.young for mt in model.materials], np.float64)
+            self._view = View(nN, nE, _p(model.coordmat), _p(model.elementmat, c_int64),
+                              _p(model.element_material, c_int64))
+            self.ct = self.L.hko_contact_create(ctypes.byref(self._view), int(model.contact_flag), _p(self._inst, c_int64),
+                                                _p(self._young))
+            cp = getattr(model, "contact_params", None)
+            if cp is not None:
+                self.L.hko_contact_set_params(self.ct, *[float(x) for x in cp])
+
+    def contact_force(self):
+        """cal_contact_force at the current state (position, velo, flags) -> 3nN force (standalone)."""
+        f = np.zeros(3 * self.m.nNode)
+        n = self.L.hko_contact_force(self.ct, _p(self.s["position"]), _p(self.s["velo"]), _p(self.diag_M),
+                                     _p(self.s["element_flag"], c_int64), _p(f))
+        return f, n
+
+    def contact_pairs(self):
+        out = []
+        for c in range(self.L.hko_contact_n_pairs(self.ct)):
+            o = np.zeros(4, np.int64)
+            nj = self.L.hko_contact_pair_info(self.ct, c, _p(o, c_int64))
+            out.append(dict(i_instance=int(o[0]), j_instance=int(o[1]), n_nodes_i=int(o[2]), n_triangles=int(o[3]),
+                            n_nodes_j=int(nj)))
+        return out
 
     def _st(self):
         f = {}
@@ -118,8 +168,9 @@ class Oracle:
         cap = 1 << 16
         log = np.zeros(2 * cap, np.int64)
         n = c_int64(0)
-        self.L.hko_run(self.h, ctypes.byref(st), _p(self.diag_M), float(t_first), int(n_steps), self.nthreads,
-                       _p(log, c_int64), cap, ctypes.byref(n))
+        self.L.hko_run_contact(self.h, ctypes.byref(st), _p(self.diag_M), float(t_first), int(n_steps),
+                               self.nthreads, _p(log, c_int64), cap, ctypes.byref(n), self.ct,
+                               _p(self._inst, c_int64) if self.ct else None)
         k = min(n.value, cap)
         self.deletions += [tuple(x) for x in log[:2 * k].reshape(k, 2)]
 
@@ -137,6 +188,8 @@ class Oracle:
 
     def __del__(self):
         try:
+            if self.ct:
+                self.L.hko_contact_destroy(self.ct)
             self.L.hko_model_destroy(self.h)
         except Exception:
             pass

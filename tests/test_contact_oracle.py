@@ -1,0 +1,79 @@
+"""The oracle's contact (oracle/hakai_oracle_contact.c) against an independent literal Python
+restatement (tests/contact_ref.py), on CPU: surface extraction, pair lists, the surface update after
+deletions and the contact force bit for bit (Float128 ~ exact rational sum rounded once).
+The reference itself cannot run here (no Julia) and ships no contact fixtures: parity of this path
+to HAKAI is pinned only by these restatements ("parity unpinned" against the Julia run)."""
+import numpy as np
+import pytest
+
+from hakai import mesh
+import oracle as O
+from contact_ref import ContactRef
+
+
+def _counts_ref(ref):
+    return [dict(i_instance=c["i"] + 1, j_instance=c["j"] + 1, n_nodes_i=len(c["nodes_i"]), n_triangles=len(c["tri_e"]),
+                 n_nodes_j=len(c["nodes_j"])) for c in ref.ct]
+
+
+def _ref_force(ref, o):
+    return ref.force(o.s["position"].reshape(-1, 3), o.s["velo"], o.diag_M, o.s["element_flag"])
+
+
+@pytest.mark.parametrize("flag", [1, 2])
+def test_pairs_and_sizes(flag):
+    m = mesh.two_body_model(plate=(5, 4, 2), impactor=(3, 2, 2), contact_flag=flag, perturb=0.05, seed=2)
+    o = O.Oracle(m)
+    ref = ContactRef(m)
+    assert o.contact_pairs() == _counts_ref(ref)
+    assert O.lib().hko_contact_min_size(o.ct) == ref.min_size
+    assert O.lib().hko_contact_max_size(o.ct) == ref.max_size
+    want = [(1, 2), (2, 1)] if flag == 1 else [(1, 1), (1, 2), (2, 1), (2, 2)]
+    assert [(p["i_instance"], p["j_instance"]) for p in o.contact_pairs()] == want
+
+
+def test_single_instance_gets_self_pair():
+    """one instance with *Contact -> a self pair (1,1)."""
+    m = mesh.bar_model(2, 2, 3, mesh.steel_ductile(), 0.0)
+    m.contact_flag = 1
+    o = O.Oracle(m)
+    assert [(p["i_instance"], p["j_instance"]) for p in o.contact_pairs()] == [(1, 1)]
+    assert o.contact_pairs() == _counts_ref(ContactRef(m))
+
+
+@pytest.mark.parametrize("myu", [None, 0.0])
+def test_contact_force_matches_restatement(myu):
+    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.03, seed=4, myu=myu)
+    o = O.Oracle(m)
+    ref = ContactRef(m)
+    total = 0
+    for t in range(1, 40):
+        o.run(t, 1)
+        f, n = o.contact_force()
+        fr, nr = _ref_force(ref, o)
+        assert n == nr
+        assert np.array_equal(f, fr), f"step {t}: max diff {np.max(np.abs(f - fr))}"
+        total += n
+    assert total > 20, "the impactor must be in contact for several steps"
+
+
+def test_surface_update_after_deletion():
+    """Deleted impactor elements expose neighbour faces: node/triangle lists and forces follow."""
+    m = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    o = O.Oracle(m)
+    ref = ContactRef(m)
+    seen = 0
+    checked = 0
+    for t in range(1, 400):
+        o.run(t, 1)
+        for (_, e) in o.deletions[seen:]:
+            ref.element_deleted(int(e))
+        seen = len(o.deletions)
+        if seen and t % 10 == 0:
+            assert o.contact_pairs() == _counts_ref(ref)
+            f, n = o.contact_force()
+            fr, nr = _ref_force(ref, o)
+            assert n == nr and np.array_equal(f, fr)
+            checked += n
+    assert seen >= 4, "elements must be deleted during contact"
+    assert checked > 0

@@ -1,0 +1,116 @@
+"""GPU contact (hakai_contact.hip) against the oracle, through the C ABI.
+
+* setup: pairs, exterior node / triangle counts and element sizes equal the oracle's;
+* the contact force of one step, probed at oracle states, is bit-identical (both are the correctly
+  rounded sum of the same FP64 terms: Float128 in the reference/oracle, double-double here);
+* whole runs with contact, with friction (reference myu 0.25) and frictionless (BASELINE C4),
+  self-contact, and contact-driven element deletion with the surface update: same deletions,
+  displacement within the north star's 1e-6.
+"""
+import numpy as np
+import pytest
+
+from hakai import mesh
+from hakai.solver import Solver, State
+import oracle as O
+from util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _upload_oracle_state(o, sv):
+    s = o.s
+    st = State(s["disp"].copy(), s["disp_pre"].copy(), s["velo"].copy(), s["Q"].copy(), s["integ_stress"].copy(),
+               s["integ_strain"].copy(), s["integ_yield_stress"].copy(), s["integ_eq_plastic_strain"].copy(),
+               s["integ_triax_stress"].copy(), s["element_flag"].copy(), s["Qe"].copy())
+    sv.upload(st)
+
+
+@pytest.mark.parametrize("flag", [1, 2])
+def test_contact_setup_matches_oracle(flag):
+    m = mesh.two_body_model(plate=(5, 4, 2), impactor=(3, 2, 2), contact_flag=flag, perturb=0.05, seed=2)
+    o = O.Oracle(m)
+    with Solver(m) as sv:
+        pairs, sizes = sv.contact_info()
+    want = [(p["i_instance"], p["j_instance"], p["n_nodes_i"], p["n_triangles"], p["n_nodes_j"])
+            for p in o.contact_pairs()]
+    assert pairs == want
+    assert sizes == (O.lib().hko_contact_min_size(o.ct), O.lib().hko_contact_max_size(o.ct))
+
+
+def test_single_instance_self_pair():
+    m = mesh.bar_model(2, 2, 3, mesh.steel_ductile(), 0.0)
+    m.contact_flag = 1
+    o = O.Oracle(m)
+    with Solver(m) as sv:
+        pairs, _ = sv.contact_info()
+    p = o.contact_pairs()[0]
+    assert pairs == [(1, 1, p["n_nodes_i"], p["n_triangles"], p["n_nodes_j"])]
+
+
+@pytest.mark.parametrize("myu", [None, 0.0])
+def test_contact_force_probe_bitexact(myu):
+    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.03, seed=4, myu=myu)
+    o = O.Oracle(m)
+    total = 0
+    with Solver(m) as sv:
+        for t in range(1, 30):
+            o.run(t, 1)
+            _upload_oracle_state(o, sv)
+            f = sv.contact_force(t + 1)
+            fo, n = o.contact_force()
+            assert np.array_equal(f, fo), f"step {t + 1}: max |diff| {np.max(np.abs(f - fo))}"
+            total += n
+    assert total > 20
+
+
+@pytest.mark.parametrize("myu,flag", [(None, 1), (0.0, 1), (None, 2)])
+def test_two_body_run_parity(myu, flag):
+    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 3), v=-1e5, perturb=0.02, seed=1, myu=myu,
+                            contact_flag=flag, n_steps=300)
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    with Solver(m) as sv:
+        sv.step(1, 100)
+        sv.step(101, m.n_steps - 100)
+        g = sv.download()
+    assert rel_err(g.disp, o.s["disp"]) < 1e-9
+    assert rel_err(g.velo, o.s["velo"]) < 1e-8
+    assert rel_err(g.integ_stress, o.s["integ_stress"]) < 1e-8
+    # the impactor was stopped / bounced by contact (it moved up at some point)
+    assert np.max(g.disp[2::3]) > 0 or np.min(g.velo[2::3]) > -1e5
+
+
+def test_contact_with_deletion_surface_update():
+    m = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    assert len(o.deletions) >= 4
+    with Solver(m) as sv:
+        sv.step(1, m.n_steps)
+        g = sv.download()
+        dels = [tuple(x) for x in sv.deleted()]
+    assert dels == sorted(o.deletions)
+    assert np.array_equal(g.element_flag, o.s["element_flag"])
+    assert rel_err(g.disp, o.s["disp"]) < 1e-6
+
+
+def test_driver_runs_contact_deck(tmp_path):
+    """HAKAI(fname) on a *Contact deck written from code: contact on the device path, 101 VTK files,
+    final displacement equal to the oracle's to the VTK's %1.6e."""
+    import os
+    import hakai
+    from inp_writer import write_inp
+    m = mesh.two_body_model(plate=(5, 5, 2), impactor=(3, 3, 2), v=-1e5, n_steps=300)
+    deck = write_inp(str(tmp_path / "impact.inp"), m)
+    out = tmp_path / "out"
+    hakai.hakai(deck, str(out), verbose=False)
+    files = sorted(os.listdir(out))
+    assert len(files) == 101 and files[-1] == "file100.vtk"
+    txt = open(out / "file100.vtk").read().split("\n")
+    i = txt.index("VECTORS DISPLACEMENT float")
+    disp = np.array([[float(x) for x in l.split()] for l in txt[i + 1:i + 1 + m.nNode]])
+    o = O.Oracle(hakai.read_inp(deck))
+    o.run(1, m.n_steps)
+    ref = o.s["disp"].reshape(-1, 3)
+    assert np.allclose(disp, ref, rtol=2e-6, atol=1e-9)

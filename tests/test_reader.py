@@ -9,10 +9,11 @@ import hakai
 from hakai import mesh
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-TENSILE = os.path.join(HERE, "golden", "Tensile5e.inp")
+TENSILE = "/root/reference/HAKAI-v0.0.0/input/Tensile5e.inp"   # read in place, never copied
 REF_DIR = "/root/reference/HAKAI-v0.0.2/input"
 
 
+@pytest.mark.skipif(not os.path.exists(TENSILE), reason="reference decks not present")
 def test_tensile5e_reader_matches_code_model():
     a = hakai.read_inp(TENSILE)
     b = mesh.tensile5e_model()
@@ -91,3 +92,36 @@ def test_multi_instance_decks(deck):
     assert len(m.ic_dofs) > 0 and np.all(m.ic_dofs >= 1)
     diag, vol = m.lumped_mass()
     assert np.all(diag > 0)
+
+
+def _dof_map(groups):
+    out = {}
+    for g in groups:
+        for d, v in g.entries:
+            for x in np.asarray(d):
+                out[int(x)] = float(v)
+    return out
+
+
+@pytest.mark.parametrize("which", ["tensile5e", "two_body", "two_body_self", "bar_ic"])
+def test_written_decks_round_trip(tmp_path, which):
+    """Decks written from code (tests/inp_writer.py) read back by the C++ reader to the same model:
+    the path the GPU-box driver tests use, since the box has no reference decks."""
+    from inp_writer import write_inp
+    m = {"tensile5e": mesh.tensile5e_model,
+         "two_body": lambda: mesh.two_body_model(perturb=0.05, seed=3),
+         "two_body_self": lambda: mesh.two_body_model(contact_flag=2),
+         "bar_ic": lambda: mesh.bar_model(2, 3, 4, mesh.steel_ductile(), lambda z, L: 1e4 * z / L, perturb=0.02)}[which]()
+    path = write_inp(str(tmp_path / "deck.inp"), m)
+    a = hakai.read_inp(path)
+    assert np.array_equal(a.coordmat, m.coordmat) and np.array_equal(a.elementmat, m.elementmat)
+    assert np.array_equal(a.element_material, m.element_material)
+    assert (a.d_time, a.end_time, a.mass_scaling, a.contact_flag) == (m.d_time, m.end_time, m.mass_scaling,
+                                                                      m.contact_flag)
+    assert _dof_map(a.bc) == _dof_map(m.bc)
+    assert dict(zip(a.ic_dofs.tolist(), a.ic_values.tolist())) == dict(zip(m.ic_dofs.tolist(), m.ic_values.tolist()))
+    if m.element_instance is not None:
+        assert np.array_equal(a.element_instance, m.element_instance)
+    for x, y in zip(a.materials, m.materials):
+        assert (x.density, x.young, x.poisson) == (y.density, y.young, y.poisson)
+        assert np.array_equal(x.plastic, np.asarray(y.plastic).reshape(-1, 2))
