@@ -58,6 +58,8 @@ struct Contact {
     int n_ni = 0, n_nj = 0;
     int *d_ni_pair = nullptr, *d_ni_node = nullptr, *d_ni_orig = nullptr, *d_ni_aptr = nullptr, *d_ni_add = nullptr;
     int *d_nj_pair = nullptr, *d_nj_node = nullptr, *d_nj_orig = nullptr, *d_nj_aptr = nullptr, *d_nj_add = nullptr;
+    int nseg = 0;
+    int* d_seg = nullptr;  // [nseg][4] (start, end, pair, side) node-entry segments
     // triangles
     int n_tri = 0;
     int *d_tri_pair = nullptr, *d_tri_nodes = nullptr, *d_tri_ele = nullptr, *d_tri_adder = nullptr;
@@ -171,31 +173,64 @@ __device__ __forceinline__ void pos(const StepIn& s, int n, double p[3]) {
 }
 
 // live flags + bounding boxes of the live node lists per pair (:2281-2299)
-__global__ void k_ct_bbox(StepIn s, int n_ni, const int* ni_pair, const int* ni_node, const int* ni_orig,
-                          const int* ni_aptr, const int* ni_add, int n_nj, const int* nj_pair, const int* nj_node,
-                          const int* nj_orig, const int* nj_aptr, const int* nj_add, unsigned long long* bbox,
-                          int* ni_bucket) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n_ni) {
-        const bool on = live(ni_orig[k], ni_aptr, ni_add, k, s.del_step, s.t);
-        ni_bucket[k] = on ? 0 : -1;
-        if (!on) return;
+// Segment = the node entries of one pair side (entries are stored pair by pair). kSegBlocks blocks
+// per segment reduce in registers, then across the block (DPP-free shuffles + LDS), then issue ONE
+// atomic per bound: per-entry atomics on 12 shared addresses serialised the whole step.
+constexpr int kSegBlocks = 64;
+
+struct Seg {
+    int start, end, pair, side;  // side 0: i-nodes, 1: j-nodes
+};
+
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+
+__global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* ni_node, const int* ni_orig,
+                                                const int* ni_aptr, const int* ni_add, const int* nj_node,
+                                                const int* nj_orig, const int* nj_aptr, const int* nj_add,
+                                                unsigned long long* bbox, int* ni_bucket) {
+    const Seg sg = segs[blockIdx.x / kSegBlocks];
+    const int sub = blockIdx.x % kSegBlocks;
+    const bool side_i = sg.side == 0;
+    const int* node = side_i ? ni_node : nj_node;
+    const int* orig = side_i ? ni_orig : nj_orig;
+    const int* aptr = side_i ? ni_aptr : nj_aptr;
+    const int* add = side_i ? ni_add : nj_add;
+    unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
+    for (int k = sg.start + sub * kB + (int)threadIdx.x; k < sg.end; k += kSegBlocks * kB) {
+        const bool on = live(orig[k], aptr, add, k, s.del_step, s.t);
+        if (side_i) ni_bucket[k] = on ? 0 : -1;
+        if (!on) continue;
         double p[3];
-        pos(s, ni_node[k], p);
-        unsigned long long* bb = bbox + 12 * ni_pair[k];
+        pos(s, node[k], p);
         for (int d = 0; d < 3; ++d) {
-            atomicMin(&bb[d], enc(p[d]));
-            atomicMax(&bb[3 + d], enc(p[d]));
+            const unsigned long long e = enc(p[d]);
+            mn[d] = umin64(mn[d], e);
+            mx[d] = umax64(mx[d], e);
         }
-    } else if (k < n_ni + n_nj) {
-        const int j = k - n_ni;
-        if (!live(nj_orig[j], nj_aptr, nj_add, j, s.del_step, s.t)) return;
-        double p[3];
-        pos(s, nj_node[j], p);
-        unsigned long long* bb = bbox + 12 * nj_pair[j];
+    }
+    for (int off = 32; off > 0; off >>= 1)
         for (int d = 0; d < 3; ++d) {
-            atomicMin(&bb[6 + d], enc(p[d]));
-            atomicMax(&bb[9 + d], enc(p[d]));
+            mn[d] = umin64(mn[d], __shfl_xor(mn[d], off));
+            mx[d] = umax64(mx[d], __shfl_xor(mx[d], off));
+        }
+    __shared__ unsigned long long red[kB / 64][6];
+    const int w = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0)
+        for (int d = 0; d < 3; ++d) {
+            red[w][d] = mn[d];
+            red[w][3 + d] = mx[d];
+        }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int q = threadIdx.x;
+        unsigned long long v = red[0][q];
+        for (int ww = 1; ww < kB / 64; ++ww) v = q < 3 ? umin64(v, red[ww][q]) : umax64(v, red[ww][q]);
+        unsigned long long* bb = bbox + 12 * sg.pair + (side_i ? 0 : 6);
+        if (q < 3) {
+            if (v != ~0ULL) atomicMin(&bb[q], v);
+        } else if (v != 0ULL) {
+            atomicMax(&bb[q], v);
         }
     }
 }
@@ -493,10 +528,32 @@ void build_instance(Inst& I, const std::vector<double>& X, const std::vector<int
             f.ele = e;
         }
     }
+    // faces ordered by (key, index): counting sort on the smallest node, then a stable insertion
+    // sort inside each (tiny) bucket -- linear time at millions of faces
     I.order.resize(F);
-    for (int i = 0; i < F; ++i) I.order[i] = i;
-    std::stable_sort(I.order.begin(), I.order.end(),
-                     [&](int a, int b) { return key_less(I.faces[a], I.faces[b]); });
+    {
+        int kmin = INT32_MAX, kmax = -1;
+        for (const Face& f : I.faces) {
+            kmin = std::min(kmin, f.key[0]);
+            kmax = std::max(kmax, f.key[0]);
+        }
+        const int nb = F ? kmax - kmin + 1 : 0;
+        std::vector<int> start((size_t)nb + 1, 0);
+        for (const Face& f : I.faces) start[f.key[0] - kmin + 1]++;
+        for (int b = 0; b < nb; ++b) start[b + 1] += start[b];
+        std::vector<int> fill(start.begin(), start.end() - 1);
+        for (int i = 0; i < F; ++i) I.order[fill[I.faces[i].key[0] - kmin]++] = i;  // ascending index per bucket
+        for (int b = 0; b < nb; ++b)
+            for (int q = start[b] + 1; q < start[b + 1]; ++q) {
+                const int v = I.order[q];
+                int r = q - 1;
+                while (r >= start[b] && key_less(I.faces[v], I.faces[I.order[r]])) {
+                    I.order[r + 1] = I.order[r];
+                    --r;
+                }
+                I.order[r + 1] = v;
+            }
+    }
     // get_surface_triangle's scan (:2040-2084): in each run of equal keys o1<o2<..<om the scan
     // pairs (o1,o2), (o3,o4), ...; an odd run keeps its LAST face, unless that is the very last
     // face of the instance (the loop stops at nE*6-1) -- SURVEY §9 Q13.
@@ -542,6 +599,7 @@ void contact_destroy(hakai_ctx* c) {
     if (!C) return;
     (void)hipStreamSynchronize(c->stream);
     dfree(C->d_par);
+    dfree(C->d_seg);
     dfree(C->d_ni_pair); dfree(C->d_ni_node); dfree(C->d_ni_orig); dfree(C->d_ni_aptr); dfree(C->d_ni_add);
     dfree(C->d_nj_pair); dfree(C->d_nj_node); dfree(C->d_nj_orig); dfree(C->d_nj_aptr); dfree(C->d_nj_add);
     dfree(C->d_tri_pair); dfree(C->d_tri_nodes); dfree(C->d_tri_ele); dfree(C->d_tri_adder);
@@ -580,11 +638,10 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     in.t = (int)t;
     const int g12 = (12 * C->npairs + kB - 1) / kB;
     hipLaunchKernelGGL(k_ct_reset, dim3(std::max(g12, 1)), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_evn);
-    const int nb = C->n_ni + C->n_nj;
-    if (nb > 0)
-        hipLaunchKernelGGL(k_ct_bbox, dim3((nb + kB - 1) / kB), dim3(kB), 0, s, in, C->n_ni, C->d_ni_pair,
-                           C->d_ni_node, C->d_ni_orig, C->d_ni_aptr, C->d_ni_add, C->n_nj, C->d_nj_pair, C->d_nj_node,
-                           C->d_nj_orig, C->d_nj_aptr, C->d_nj_add, C->d_bbox, C->d_ni_bucket);
+    if (C->nseg > 0)
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, (const Seg*)C->d_seg, C->d_ni_node,
+                           C->d_ni_orig, C->d_ni_aptr, C->d_ni_add, C->d_nj_node, C->d_nj_orig, C->d_nj_aptr,
+                           C->d_nj_add, C->d_bbox, C->d_ni_bucket);
     if (C->n_ni > 0) {
         hipLaunchKernelGGL(k_ct_bin, dim3((C->n_ni + kB - 1) / kB), dim3(kB), 0, s, in, C->n_ni, C->d_ni_pair,
                            C->d_ni_node, C->d_par, C->d_bbox, C->d_ni_bucket, C->d_ni_map, C->d_bcnt);
@@ -692,39 +749,48 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
     }
     std::vector<int> ni_pair, ni_node, ni_orig, ni_aptr{0}, ni_add;
     std::vector<int> nj_pair, nj_node, nj_orig, nj_aptr{0}, nj_add;
-    std::vector<int> tri_pair, tri_nodes, tri_ele, tri_adder;
+    std::vector<int> tri_pair, tri_nodes, tri_ele, tri_adder, seg;
     // node list of a pair side: initial exterior nodes + nodes exposed by each element's deletion
     auto node_list = [&](int pr, const Inst& I, bool with_adds, std::vector<int>& vp, std::vector<int>& vn,
                          std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd) {
-        std::vector<std::pair<int, int>> ent;  // (node, adder or -1)
+        // per node: initial (exterior) or the ascending list of elements whose deletion exposes it;
+        // bucketed by node id in linear time (adders arrive in ascending element order)
+        const int nN = (int)c->nN;
+        std::vector<char> orig((size_t)nN, 0), seen((size_t)nN, 0);
         for (int f : I.exterior)
-            for (int q = 0; q < 4; ++q) ent.push_back({I.faces[f].n[q], -1});
-        if (with_adds)
+            for (int q = 0; q < 4; ++q) orig[I.faces[f].n[q]] = seen[I.faces[f].n[q]] = 1;
+        std::vector<int> cnt((size_t)nN + 1, 0), adders;
+        if (with_adds) {
             for (int j = 0; j < I.nE; ++j)
                 for (int f : I.added[j])
-                    for (int q = 0; q < 4; ++q) ent.push_back({I.faces[f].n[q], I.e0 + j});
-        std::sort(ent.begin(), ent.end());
+                    for (int q = 0; q < 4; ++q) {
+                        const int n = I.faces[f].n[q];
+                        seen[n] = 1;
+                        if (!orig[n]) cnt[n + 1]++;
+                    }
+            for (int n = 0; n < nN; ++n) cnt[n + 1] += cnt[n];
+            adders.resize((size_t)cnt[nN]);
+            std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+            for (int j = 0; j < I.nE; ++j)
+                for (int f : I.added[j])
+                    for (int q = 0; q < 4; ++q) {
+                        const int n = I.faces[f].n[q];
+                        if (!orig[n]) adders[fill[n]++] = I.e0 + j;
+                    }
+        }
         long long count = 0;
-        for (size_t a = 0; a < ent.size();) {
-            size_t b = a;
-            bool orig = false;
-            std::vector<int> adders;
-            while (b < ent.size() && ent[b].first == ent[a].first) {
-                if (ent[b].second < 0) orig = true;
-                else adders.push_back(ent[b].second);
-                ++b;
-            }
+        for (int n = 0; n < nN; ++n) {
+            if (!seen[n]) continue;
             vp.push_back(pr);
-            vn.push_back(ent[a].first);
-            vo.push_back(orig ? 1 : 0);
-            if (!orig) {
-                std::sort(adders.begin(), adders.end());
-                adders.erase(std::unique(adders.begin(), adders.end()), adders.end());
-                vadd.insert(vadd.end(), adders.begin(), adders.end());
+            vn.push_back(n);
+            vo.push_back(orig[n]);
+            if (!orig[n] && with_adds) {
+                int last = -1;
+                for (int a = cnt[n]; a < cnt[n + 1]; ++a)
+                    if (adders[a] != last) vadd.push_back(last = adders[a]);  // duplicates are adjacent
             }
             va.push_back((int)vadd.size());
-            count += orig;
-            a = b;
+            count += orig[n];
         }
         return count;
     };
@@ -738,7 +804,7 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
         pp.kc = self ? C->kc_s : C->kc_o;
         pp.Cr = self ? C->Cr_s : C->Cr_o;
         pp.ddiv = self ? C->max_size * 0.6 : C->max_size * 1.1;  // :2322-2325
-        const size_t ni0 = ni_node.size();
+        const size_t ni0 = ni_node.size(), nj0 = nj_node.size();
         // surface update (:766-804): c_nodes_i grows for every pair whose point instance lost an
         // element; triangles and c_nodes_j grow only when the triangle instance differs
         const long long c_i = node_list(pr, inst[a], true, ni_pair, ni_node, ni_orig, ni_aptr, ni_add);
@@ -767,6 +833,8 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
                         tri_adder.push_back(inst[b].e0 + j);
                     }
                 }
+        if (ni_node.size() > ni0) seg.insert(seg.end(), {(int)ni0, (int)ni_node.size(), pr, 0});
+        if (nj_node.size() > nj0) seg.insert(seg.end(), {(int)nj0, (int)nj_node.size(), pr, 1});
         int hs = 64;
         while (hs < 2 * (int)(ni_node.size() - ni0)) hs <<= 1;
         pp.hash_off = hoff;
@@ -783,6 +851,7 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
     C->n_ni = (int)ni_node.size();
     C->n_nj = (int)nj_node.size();
     C->n_tri = (int)tri_ele.size();
+    C->nseg = (int)seg.size() / 4;
     C->cap = std::max<long long>(1 << 16, 8LL * C->n_ni);
     hipStream_t s = c->stream;
     int rc = 0;
@@ -792,6 +861,7 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
         if (_e != hipSuccess) rc = hip_fail(_e, #dst);      \
     } while (0)
     UP(d_par, C->h_par);
+    UP(d_seg, seg);
     UP(d_ni_pair, ni_pair); UP(d_ni_node, ni_node); UP(d_ni_orig, ni_orig); UP(d_ni_aptr, ni_aptr); UP(d_ni_add, ni_add);
     UP(d_nj_pair, nj_pair); UP(d_nj_node, nj_node); UP(d_nj_orig, nj_orig); UP(d_nj_aptr, nj_aptr); UP(d_nj_add, nj_add);
     UP(d_tri_pair, tri_pair); UP(d_tri_nodes, tri_nodes); UP(d_tri_ele, tri_ele); UP(d_tri_adder, tri_adder);

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""C4 contact workload (BASELINE configs[3]): plate 200x200x50 + impactor 100x100x200 (4 M hex),
+gap 0.1 mm, impactor v = -1e5 mm/s, elastoplastic steel, all-exterior contact, frictionless.
+
+Prints one JSON line: element-updates/s over the timed steps (contact search + force included) and
+the per-kernel split from the library's HIP-event timers. --scale divides every edge count.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hakai-fem_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=1)
+    ap.add_argument("--preload", type=int, default=30, help="steps before timing (contact starts at ~10)")
+    ap.add_argument("--steps", type=int, default=50)
+    a = ap.parse_args()
+    import numpy as np
+    from hakai import mesh
+    from hakai._abi import K_BC, K_CONTACT, K_ELEMENT, K_NODAL
+    from hakai.solver import Solver
+    t0 = time.time()
+    m = mesh.config_c4(a.scale)
+    t1 = time.time()
+    sv = Solver(m)
+    t2 = time.time()
+    pairs, sizes = sv.contact_info()
+    sv.step(1, a.preload)
+    sv.sync()
+    sv.profile(True)
+    ts = time.perf_counter()
+    sv.step(1 + a.preload, a.steps)
+    sv.sync()
+    el = time.perf_counter() - ts
+    k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
+                                            (K_CONTACT, "contact"))}
+    f = sv.contact_force(1 + a.preload + a.steps)
+    st = sv.download(element_flag=True)
+    n_active = int(st.element_flag.sum())
+    out = {
+        "workload": f"C4 two-body impact, scale 1/{a.scale}", "elements": m.nElement, "nodes": m.nNode,
+        "pairs": pairs, "element_size": sizes, "steps": a.steps, "preload": a.preload,
+        "value_M_element_updates_per_s": round(n_active * a.steps / el / 1e6, 3),
+        "ms_per_step": round(el / a.steps * 1e3, 4),
+        "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
+        "contact_nodes_with_force": int(np.count_nonzero(np.abs(f.reshape(-1, 3)).sum(1))),
+        "setup_s": {"mesh": round(t1 - t0, 2), "upload_contact_setup": round(t2 - t1, 2)},
+    }
+    sv.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
