@@ -85,6 +85,7 @@ static void free_model(hakai_ctx* c) {
     dfree(c->d_fe);
     dfree(c->d_inc_ptr);
     dfree(c->d_inc);
+    dfree(c->d_inc_row);
     dfree(c->d_inc8);
     dfree(c->d_del_step);
     dfree(c->d_qbuf);
@@ -216,8 +217,78 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.any_plastic = c->any_plastic ? 1 : 0;
     ea.variant = c->elem_variant;
     ea.pipe_blocks = c->pipe_blocks;
+    ea.pipe_map = c->pipe_map;
+    ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
     ea.nmat = c->nmat;
     return ea;
+}
+
+// Base offset and component stride of (element e, local node k) in a force layout.
+static inline long long fe_base(const hakai_ctx* c, int layout, long long e, int k) {
+    return layout == 1 ? 3LL * k * c->nEp + e : 24 * e + 3 * k;
+}
+static inline long long fe_cs(const hakai_ctx* c, int layout) { return layout == 1 ? c->nEp : 1; }
+
+// Element forces <-> the reference's Qe (24 x nE) whatever the device layout.
+static int fe_download_qe(hakai_ctx* c, double* Qe) {
+    if (c->fe_layout == 0) {
+        HIPCHK(hipMemcpyAsync(Qe, c->d_fe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    std::vector<double> fe((size_t)c->fe_len);
+    HIPCHK(hipMemcpyAsync(fe.data(), c->d_fe, fe.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const long long cs = fe_cs(c, c->fe_layout);
+    for (long long e = 0; e < c->nE; ++e)
+        for (int k = 0; k < 8; ++k)
+            for (int q = 0; q < 3; ++q) Qe[24 * e + 3 * k + q] = fe[fe_base(c, c->fe_layout, e, k) + q * cs];
+    return 0;
+}
+
+static int fe_upload_qe(hakai_ctx* c, const double* Qe) {
+    if (c->fe_layout == 0) {
+        HIPCHK(hipMemcpyAsync(c->d_fe, Qe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    std::vector<double> fe((size_t)c->fe_len, 0.0);
+    const long long cs = fe_cs(c, c->fe_layout);
+    for (long long e = 0; e < c->nE; ++e)
+        for (int k = 0; k < 8; ++k)
+            for (int q = 0; q < 3; ++q) fe[fe_base(c, c->fe_layout, e, k) + q * cs] = Qe[24 * e + 3 * k + q];
+    HIPCHK(hipMemcpyAsync(c->d_fe, fe.data(), fe.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Incidence tables (CSR and padded) as bases of `layout`; padding -> the zero base 24nEp.
+static int fe_upload_incidence(hakai_ctx* c, int layout) {
+    std::vector<int> inc(c->h_inc0.size());
+    for (size_t j = 0; j < inc.size(); ++j) inc[j] = (int)fe_base(c, layout, c->h_inc0[j] >> 3, c->h_inc0[j] & 7);
+    if (!inc.empty())
+        HIPCHK(hipMemcpyAsync(c->d_inc, inc.data(), inc.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (c->d_inc8) {
+        std::vector<int> inc8(8 * (size_t)c->nN, (int)(24 * c->nEp));
+        for (long long n = 0; n < c->nN; ++n)
+            for (int j = c->h_ptr[n]; j < c->h_ptr[n + 1]; ++j) inc8[8 * n + (j - c->h_ptr[n])] = inc[j];
+        HIPCHK(hipMemcpyAsync(c->d_inc8, inc8.data(), inc8.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Switch the element-force layout, converting the current forces (the next step's Q).
+static int fe_set_layout(hakai_ctx* c, int layout) {
+    if (layout == c->fe_layout) return 0;
+    std::vector<double> qe(24 * (size_t)c->nE);
+    int r = c->state_ok ? fe_download_qe(c, qe.data()) : 0;
+    if (r) return r;
+    if ((r = fe_upload_incidence(c, layout))) return r;
+    HIPCHK(hipMemsetAsync(c->d_fe, 0, (size_t)c->fe_len * sizeof(double), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->fe_layout = layout;
+    return c->state_ok ? fe_upload_qe(c, qe.data()) : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -286,7 +357,7 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     if (nNode <= 0 || nElement < 0 || !coordmat || (nElement > 0 && (!elementmat || !element_material)) || nMat <= 0 ||
         !mats || !diag_M)
         return fail(HAKAI_ERR_ARG, "upload_model: bad arguments");
-    if (8 * nElement >= (int64_t)INT32_MAX || nNode >= (int64_t)INT32_MAX)
+    if (26 * (nElement + 32) + 8 >= (int64_t)INT32_MAX || nNode >= (int64_t)INT32_MAX)
         return fail(HAKAI_ERR_ARG, "upload_model: mesh too large for int32 indexing on one rank");
     HIPCHK(hipSetDevice(c->device));
     (void)hipStreamSynchronize(c->stream);
@@ -334,12 +405,6 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     }
     int maxinc = 0;
     for (long long n = 0; n < nN; ++n) maxinc = std::max(maxinc, ptr[n + 1] - ptr[n]);
-    std::vector<int> inc8;
-    if (maxinc <= 8) {  // padded table for the unrolled gather; pad -> zero row 8nE of fe
-        inc8.assign(8 * (size_t)nN, (int)(8 * nEp));
-        for (long long n = 0; n < nN; ++n)
-            for (int j = ptr[n]; j < ptr[n + 1]; ++j) inc8[8 * n + (j - ptr[n])] = inc[j];
-    }
     c->nN = nN;
     c->nE = nE;
     c->nEp = nEp;
@@ -359,9 +424,13 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     HIPCHK(dalloc(&c->d_eqps, ld));
     HIPCHK(dalloc(&c->d_yield, ld));
     HIPCHK(dalloc(&c->d_triax, ld));
-    HIPCHK(dalloc(&c->d_fe, 24 * (size_t)nEp + 3));  // + zero row for padded gathers
+    // forces: 24nEp doubles in either layout, then zeros up to 26nEp (padding base 24nEp with
+    // component stride up to nEp)
+    c->fe_len = 26 * nEp + 8;
+    HIPCHK(dalloc(&c->d_fe, (size_t)c->fe_len));
     HIPCHK(dalloc(&c->d_inc_ptr, (size_t)nN + 1));
     HIPCHK(dalloc(&c->d_inc, 8 * (size_t)nE));
+    HIPCHK(dalloc(&c->d_inc_row, 8 * (size_t)nE));
     HIPCHK(dalloc(&c->d_qbuf, 3 * (size_t)nN));
     hipStream_t s = c->stream;
     HIPCHK(hipMemcpyAsync(c->d_coord, coordmat, 3 * nN * sizeof(double), hipMemcpyHostToDevice, s));
@@ -369,15 +438,20 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     if (nE) {
         HIPCHK(hipMemcpyAsync(c->d_conn, conn.data(), 8 * nEp * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_mat, mat.data(), nEp * sizeof(int), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(c->d_inc, inc.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_inc_row, inc.data(), 8 * nE * sizeof(int), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(c->d_mats, c->h_mats.data(), nMat * sizeof(DevMat), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_inc_ptr, ptr.data(), (nN + 1) * sizeof(int), hipMemcpyHostToDevice, s));
-    if (!inc8.empty()) {
-        HIPCHK(dalloc(&c->d_inc8, inc8.size()));
-        HIPCHK(hipMemcpyAsync(c->d_inc8, inc8.data(), inc8.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    }
+    if (maxinc <= 8) HIPCHK(dalloc(&c->d_inc8, 8 * (size_t)nN));  // padded table for the unrolled gather
     HIPCHK(hipStreamSynchronize(s));  // host vectors go out of scope
+    c->fe_layout = 0;
+    c->max_inc = maxinc;
+    c->h_ptr = ptr;
+    c->h_inc0 = inc;
+    {
+        int r = fe_upload_incidence(c, 0);
+        if (r) return r;
+    }
     c->h_coord.assign(coordmat, coordmat + 3 * nN);
     c->h_conn.assign(conn.begin(), conn.begin() + 8 * nE);
     c->h_mat.assign(mat.begin(), mat.begin() + nE);
@@ -455,7 +529,7 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     c->cur = 0;
     HIPCHK(hipMemsetAsync(c->d_u[0], 0, fn * sizeof(double), s));
     HIPCHK(hipMemsetAsync(c->d_u[1], 0, fn * sizeof(double), s));
-    HIPCHK(hipMemsetAsync(c->d_fe, 0, (24 * (size_t)c->nEp + 3) * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(c->d_fe, 0, (size_t)c->fe_len * sizeof(double), s));
     HIPCHK(hipMemsetAsync(c->d_del_step, 0, ((size_t)c->nEp + 1) * sizeof(int), s));
     HIPCHK(hk::launch_reset_gp(c->d_stress, c->d_strain, c->d_eqps, c->d_yield, c->d_triax, c->d_flag, c->d_mat,
                                c->d_mats, c->nE, c->nEp, c->ld, s));
@@ -526,14 +600,21 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
         HIPCHK(hipMemcpyAsync(c->d_del_step, ds.data(), c->nE * sizeof(int), hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
         // fe of elements uploaded as deleted must not contribute
-        std::vector<double> z;
-        for (long long e = 0; e < c->nE; ++e)
-            if (!f[e]) {
-                if (z.empty()) z.assign(24, 0.0);
-                HIPCHK(hipMemcpyAsync(c->d_fe + 24 * e, z.data(), 24 * sizeof(double), hipMemcpyHostToDevice, s));
-            }
+        bool any = false;
+        for (long long e = 0; e < c->nE; ++e) any |= !f[e];
+        if (any && !st->Qe) {
+            std::vector<double> qe(24 * (size_t)c->nE);
+            int r = fe_download_qe(c, qe.data());
+            if (r) return r;
+            for (long long e = 0; e < c->nE; ++e)
+                if (!f[e]) std::fill(qe.begin() + 24 * e, qe.begin() + 24 * (e + 1), 0.0);
+            if ((r = fe_upload_qe(c, qe.data()))) return r;
+        }
     }
-    if (st->Qe) HIPCHK(hipMemcpyAsync(c->d_fe, st->Qe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyHostToDevice, s));
+    if (st->Qe) {
+        int r = fe_upload_qe(c, st->Qe);
+        if (r) return r;
+    }
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
     hkc::comm_reset(c);
@@ -575,7 +656,7 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
         } else {
             double* tmp = nullptr;
             HIPCHK(dalloc(&tmp, fn));
-            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, tmp, c->nN, s));
+            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, c->fe_layout == 1 ? c->nEp : 1, tmp, c->nN, s));
             HIPCHK(hipMemcpyAsync(st->Q, tmp, fn * sizeof(double), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             dfree(tmp);
@@ -608,7 +689,10 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
         HIPCHK(hipStreamSynchronize(s));
         for (long long e = 0; e < c->nE; ++e) st->element_flag[e] = (f[e] == 1) ? 1 : 0;
     }
-    if (st->Qe) HIPCHK(hipMemcpyAsync(st->Qe, c->d_fe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (st->Qe) {
+        int r = fe_download_qe(c, st->Qe);
+        if (r) return r;
+    }
     HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
@@ -631,7 +715,8 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.mass = c->d_mass;
         na.inc_ptr = c->d_inc_ptr;
         na.inc = c->d_inc;
-        na.inc8 = c->d_inc8;
+        na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
+        na.cstride = c->fe_layout == 1 ? c->nEp : 1;
         na.fe = c->d_fe;
         na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
         na.fext = nullptr;
@@ -726,6 +811,16 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         c->pipe_blocks = (int)value;
         return 0;
     }
+    if (!std::strcmp(key, "fe_layout")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fe_layout must be 0 or 1");
+        HIPCHK(hipSetDevice(c->device));
+        return fe_set_layout(c, (int)value);
+    }
+    if (!std::strcmp(key, "elem_map")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_map must be 0 or 1");
+        c->pipe_map = (int)value;
+        return 0;
+    }
     if (!std::strcmp(key, "nodal_padded")) {
         if (!value) {
             dfree(c->d_inc8);
@@ -768,7 +863,7 @@ int hakai_node_stress_strain(hakai_ctx* c, double* node_stress, double* node_str
     HIPCHK(dalloc(&ne, nN));
     HIPCHK(dalloc(&nm, nN));
     HIPCHK(dalloc(&nt, nN));
-    HIPCHK(hk::launch_node_average(c->d_inc_ptr, c->d_inc, c->d_stress, c->d_strain, c->d_eqps, c->d_triax, c->ld,
+    HIPCHK(hk::launch_node_average(c->d_inc_ptr, c->d_inc_row, c->d_stress, c->d_strain, c->d_eqps, c->d_triax, c->ld,
                                    c->nN, ns, nn, ne, nm, nt, s));
     if (node_stress) HIPCHK(hipMemcpyAsync(node_stress, ns, 6 * nN * sizeof(double), hipMemcpyDeviceToHost, s));
     if (node_strain) HIPCHK(hipMemcpyAsync(node_strain, nn, 6 * nN * sizeof(double), hipMemcpyDeviceToHost, s));

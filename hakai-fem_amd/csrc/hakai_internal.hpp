@@ -42,10 +42,21 @@ struct hakai_ctx {
     double* d_triax = nullptr;
     double* d_fe = nullptr;
     int* d_inc_ptr = nullptr;
-    int* d_inc = nullptr;
+    int* d_inc = nullptr;        // CSR incidences as force base offsets of the active layout
+    int* d_inc_row = nullptr;    // the same incidences as (8e+k), for element-indexed data
     int* d_inc8 = nullptr;       // padded incidence table, null if a node has > 8 incidences
+    // Element-force layout: component c of (element e, local node k) lives at fe[base + c*cs].
+    //   layout 0 (AoS rows, = the reference's Qe column order): base = 24e + 3k, cs = 1;
+    //   layout 1 (component SoA): base = 3k*nEp + e, cs = nEp -- a wave of neighbouring nodes
+    //   gathers neighbouring elements' same slot, i.e. contiguous doubles.
+    // d_inc / d_inc8 hold bases of the active layout; base 24nEp is all-zero in both (padding).
+    int fe_layout = 0;
+    long long fe_len = 0;        // doubles allocated for fe
+    int max_inc = 0;
+    std::vector<int> h_ptr, h_inc0;  // CSR node -> (8e+k), ascending element order
     int elem_variant = 2;        // k_element occupancy variant (HAKAI_ELEM_MINW)
     int pipe_blocks = 512;       // persistent pipelined element kernel grid (0 = simple kernel)
+    int pipe_map = 1;            // batch schedule of the persistent kernel (0 per block, 1 per XCD)
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
     // bc

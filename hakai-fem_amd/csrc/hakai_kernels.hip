@@ -40,7 +40,7 @@ __device__ constexpr double kSz[8] = {-1., -1., -1., -1., 1., 1., 1., 1.};
 
 // Everything one lane needs from HBM for one element, gathered ahead of the compute.
 struct ElemIn {
-    int n, fl, mt;       // stage A: local node, element flag, material
+    int n, fl, mt, fb;   // stage A: local node, element flag, material, force base offset
     double x[3], du[3];  // stage B: this lane's node: position = coord + u, d_disp = u - u_pre
     double sig[6], eps[6], eqp, ys;
 };
@@ -53,6 +53,7 @@ __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int
     in.fl = a.flag[e];
     in.n = a.conn[8 * e + k];
     in.mt = a.mat[e];
+    in.fb = a.cstride == 1 ? (int)(24 * e + 3 * k) : (int)(3 * k * a.nEp + e);
 }
 
 template <bool ANY_PLASTIC>
@@ -273,10 +274,10 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     const double S = allreduce8(det * (3.0 * mean));
 
     // ---- unconditional write-back (selects, no branches)
-    double* fo = a.fe + 24 * e + 3 * k;
+    double* fo = a.fe + in.fb;
     fo[0] = active ? fk[0] + S * bb0 : 0.0;
-    fo[1] = active ? fk[1] + S * bb1 : 0.0;
-    fo[2] = active ? fk[2] + S * bb2 : 0.0;
+    fo[a.cstride] = active ? fk[1] + S * bb1 : 0.0;
+    fo[2 * a.cstride] = active ? fk[2] + S * bb2 : 0.0;
     if (WITH_VOL) a.vol[e] = V;
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
@@ -329,21 +330,37 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     const DevMat* mats = LDS_MATS ? s_mats : a.mats;
     double* nd8 = s_nd + grp * kLdsStride;
     const long long nb = a.nEp / kEPB;
-    const long long lb = xcd_remap(blockIdx.x, gridDim.x);
-    const long long b0 = lb * nb / gridDim.x, b1 = (lb + 1) * nb / gridDim.x;
-    if (b0 >= b1) return;  // block-uniform
-    // batches past the end are clamped to the last one (loaded, never computed)
-    auto elem_of = [&](long long b) { return (b < b1 ? b : b1 - 1) * kEPB + grp; };
+    // Batch schedule, as (first, stride, count):
+    //  map 0: each block walks a contiguous run of batches;
+    //  map 1: each XCD owns a contiguous run and its blocks stride through it together, so the
+    //         batches that share a node layer (one element layer apart) are processed close in
+    //         time on the same L2 (blocks are dealt round-robin over the 8 XCDs).
+    long long first, stride, count;
+    if (a.pipe_map == 1 && gridDim.x % 8 == 0) {
+        const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, per = gridDim.x >> 3;
+        const long long r0 = x * nb / 8, r1 = (x + 1) * nb / 8;
+        first = r0 + j;
+        stride = per;
+        count = first < r1 ? (r1 - first + per - 1) / per : 0;
+    } else {
+        const long long lb = xcd_remap(blockIdx.x, gridDim.x);
+        first = lb * nb / gridDim.x;
+        stride = 1;
+        count = (lb + 1) * nb / gridDim.x - first;
+    }
+    if (count <= 0) return;  // block-uniform
+    // iterations past the end are clamped to the last batch (loaded, never computed)
+    auto elem_of = [&](long long i) { return (first + (i < count ? i : count - 1) * stride) * kEPB + grp; };
 
     ElemIn cur, nxt;
-    load_stage_a(a, elem_of(b0), k, cur);
-    load_stage_a(a, elem_of(b0 + 1), k, nxt);
-    load_stage_b<ANY_PLASTIC>(a, elem_of(b0), k, cur);
-    for (long long b = b0; b < b1; ++b) {
+    load_stage_a(a, elem_of(0), k, cur);
+    load_stage_a(a, elem_of(1), k, nxt);
+    load_stage_b<ANY_PLASTIC>(a, elem_of(0), k, cur);
+    for (long long i = 0; i < count; ++i) {
         ElemIn nn;
-        load_stage_a(a, elem_of(b + 2), k, nn);
-        load_stage_b<ANY_PLASTIC>(a, elem_of(b + 1), k, nxt);
-        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false>(a, mats, elem_of(b), k, nd8, cur);
+        load_stage_a(a, elem_of(i + 2), k, nn);
+        load_stage_b<ANY_PLASTIC>(a, elem_of(i + 1), k, nxt);
+        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false>(a, mats, elem_of(i), k, nd8, cur);
         cur = nxt;
         nxt = nn;
     }
@@ -472,6 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
     const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
     if (n >= a.nN) return;
+    const long long cs = a.cstride;
     double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0;
     if (a.qbuf) {
         Q0 = a.qbuf[3 * n + 0];
@@ -484,10 +502,10 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
         double f[8][3];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const double* p = a.fe + 3 * (long long)idx[j];
+            const double* p = a.fe + idx[j];
             f[j][0] = p[0];
-            f[j][1] = p[1];
-            f[j][2] = p[2];
+            f[j][1] = p[cs];
+            f[j][2] = p[2 * cs];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -498,10 +516,10 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
     } else {
         const int j0 = a.inc_ptr[n], j1 = a.inc_ptr[n + 1];
         for (int j = j0; j < j1; ++j) {
-            const double* f = a.fe + 3 * (long long)a.inc[j];
+            const double* f = a.fe + a.inc[j];
             Q0 += f[0];
-            Q1 += f[1];
-            Q2 += f[2];
+            Q1 += f[cs];
+            Q2 += f[2 * cs];
         }
     }
     nodal_update(a, n, Q0, Q1, Q2);
@@ -551,26 +569,27 @@ hipError_t launch_bc(const BCArgs& a, hipStream_t s) {
 // node averages for output.
 // ---------------------------------------------------------------------------------------------
 __global__ void k_gather_q(const int* __restrict__ ptr, const int* __restrict__ inc, const double* __restrict__ fe,
-                           double* Q, long long nN) {
+                           long long cs, double* Q, long long nN) {
 #pragma clang fp contract(off)
     const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= nN) return;
     double q0 = 0.0, q1 = 0.0, q2 = 0.0;
     for (int j = ptr[n]; j < ptr[n + 1]; ++j) {
-        const double* f = fe + 3 * (long long)inc[j];
+        const double* f = fe + inc[j];
         q0 += f[0];
-        q1 += f[1];
-        q2 += f[2];
+        q1 += f[cs];
+        q2 += f[2 * cs];
     }
     Q[3 * n + 0] = q0;
     Q[3 * n + 1] = q1;
     Q[3 * n + 2] = q2;
 }
 
-hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
-                           hipStream_t s) {
+hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, long long cstride, double* Q,
+                           long long nN, hipStream_t s) {
     if (nN <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, inc_ptr, inc, fe, Q, nN);
+    hipLaunchKernelGGL(k_gather_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, inc_ptr, inc, fe, cstride,
+                       Q, nN);
     return hipGetLastError();
 }
 

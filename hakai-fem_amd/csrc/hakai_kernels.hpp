@@ -20,7 +20,8 @@ struct ElemArgs {
     double* eqps;          // [ld]
     double* yield;         // [ld]
     double* triax;         // [ld]
-    double* fe;            // element nodal forces [nE][8][3] (= Qe column of the reference)
+    double* fe;            // element nodal forces: component c of (e, k) at fe[base + c*cstride],
+    long long cstride;     // base = 24e+3k (cstride 1, Qe order) or 3k*nEp+e (cstride nEp)
     double* vol;           // optional current volume per element (elementVolume, :1169)
     long long nE;          // elements
     long long nEp;         // elements padded to whole 32-element batches (padding: flag 0)
@@ -30,6 +31,7 @@ struct ElemArgs {
     int any_plastic;       // some material has a *Plastic table (eqps/yield are live)
     int variant;           // occupancy variant of the simple kernel: min waves per SIMD (2, 3, 4)
     int pipe_blocks;        // > 0: persistent pipelined kernel with this many blocks
+    int pipe_map;           // batch schedule: 0 contiguous per block, 1 contiguous per XCD, strided
     int nmat;               // materials (staged in LDS when <= kMaxLdsMats)
 };
 
@@ -37,12 +39,13 @@ struct NodalArgs {
     const double* u;       // disp
     double* u_pre_out;     // in: disp_pre, out: disp_new (ping-pong buffers, no copies)
     const double* mass;    // per node lumped mass (diag_M of each dof)
-    const int* inc_ptr;    // CSR node -> incidences (8e+i), ascending element order
+    const int* inc_ptr;    // CSR node -> incidences (fe base offsets), ascending element order
     const int* inc;
-    const int* inc8;       // padded [nN][8] table (pad -> zero row 8nEp) or null (use CSR)
+    const int* inc8;       // padded [nN][8] table of bases (pad -> zero base 24nEp) or null (CSR)
     const double* fe;
     const double* qbuf;    // if non-null: Q taken from this 3nN buffer (uploaded state), not from fe
     const double* fext;    // external force 3nN or null (= 0)
+    long long cstride;     // component stride of fe (inc / inc8 hold base offsets)
     long long nN;
     double dt;
 };
@@ -66,7 +69,8 @@ hipError_t launch_nodal(const NodalArgs& a, hipStream_t s);
 hipError_t launch_bc(const BCArgs& a, hipStream_t s);
 
 // Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
-hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
+hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, long long cstride, double* Q,
+                           long long nN,
                            hipStream_t s);
 // AoS [gp][6] <-> SoA [6][ld] conversions used at upload/download.
 hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, long long ld, hipStream_t s);

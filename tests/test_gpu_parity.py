@@ -193,3 +193,30 @@ def test_hakai_driver_writes_vtk(tmp_path):
     assert np.allclose(disp, ref, rtol=2e-6, atol=1e-12)
     cells = txt[txt.index(next(l for l in txt if l.startswith("CELLS"))) ]
     assert cells == "CELLS 4 36"
+
+
+@pytest.mark.parametrize("tuning", [{"fe_layout": 1}, {"elem_map": 1}, {"fe_layout": 1, "elem_map": 1},
+                                    {"elem_pipe_blocks": 0, "fe_layout": 1}, {"elem_map": 0},
+                                    {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1}])
+def test_tuning_variants_bitexact(tuning):
+    """Force layouts (AoS rows / component SoA) and batch schedules change only where bytes
+    live and which block computes what: the trajectory is bit-identical to the default."""
+    m = fast_deletion_bar(3, 3, 10)
+    n = 1200
+    with Solver(m) as sv:
+        sv.step(1, n)
+        ref = sv.download()
+        rdel = [tuple(x) for x in sv.deleted()]
+    with Solver(m) as sv:
+        for k, v in tuning.items():
+            sv.set_tuning(k, v)
+        sv.step(1, 500)
+        if "fe_layout" in tuning:   # switching mid-run converts the live forces
+            sv.set_tuning("fe_layout", 0)
+            sv.set_tuning("fe_layout", tuning["fe_layout"])
+        sv.step(501, n - 500)
+        g = sv.download()
+        dels = [tuple(x) for x in sv.deleted()]
+    assert dels == rdel and len(rdel) > 0
+    for name in ("disp", "disp_pre", "Q", "Qe", "integ_stress", "integ_eq_plastic_strain", "element_flag"):
+        assert np.array_equal(getattr(g, name), getattr(ref, name)), name
