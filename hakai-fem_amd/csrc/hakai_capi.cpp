@@ -717,6 +717,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.inc = c->d_inc;
         na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
         na.cstride = c->fe_layout == 1 ? c->nEp : 1;
+        na.early = c->nodal_early;
         na.fe = c->d_fe;
         na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
         na.fext = nullptr;
@@ -815,6 +816,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fe_layout must be 0 or 1");
         HIPCHK(hipSetDevice(c->device));
         return fe_set_layout(c, (int)value);
+    }
+    if (!std::strcmp(key, "nodal_early")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_early must be 0 or 1");
+        c->nodal_early = (int)value;
+        return 0;
     }
     if (!std::strcmp(key, "elem_map")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_map must be 0 or 1");

@@ -57,6 +57,7 @@ struct hakai_ctx {
     int elem_variant = 2;        // k_element occupancy variant (HAKAI_ELEM_MINW)
     int pipe_blocks = 512;       // persistent pipelined element kernel grid (0 = simple kernel)
     int pipe_map = 1;            // batch schedule of the persistent kernel (0 per block, 1 per XCD)
+    int nodal_early = 1;         // nodal kernel loads its node operands before the gather
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
     // bc

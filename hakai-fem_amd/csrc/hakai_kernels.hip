@@ -468,9 +468,28 @@ hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream
 // points at a zero row of fe, and x + 0.0 == x leaves the sum unchanged). Nodes with more than 8
 // incidences (unstructured meshes) use the CSR path.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, double Q0, double Q1, double Q2) {
+// The node's own operands are loaded FIRST, so they are in flight together with the incidence
+// indices; loaded after the gather they add a third dependent memory round trip (measured with
+// tools/nodal_probe.hip: 0.174 -> 0.141 ms on the C3 node count).
+struct NodeIn {
+    double m, uc[3], up[3], f[3];
+};
+
+template <bool FEXT>
+__device__ __forceinline__ void nodal_load(const NodalArgs& a, long long n, NodeIn& in) {
+    in.m = a.mass[n];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        in.uc[c] = a.u[3 * n + c];
+        in.up[c] = a.u_pre_out[3 * n + c];
+        in.f[c] = FEXT ? a.fext[3 * n + c] : 0.0;
+    }
+}
+
+__device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, const NodeIn& in, double Q0, double Q1,
+                                             double Q2) {
 #pragma clang fp contract(off)
-    const double m = a.mass[n];
+    const double m = in.m;
     const double dt = a.dt;
     const double dC = 0.0 * m;  // diag_C .= diag_M * C, C = 0
     const double mdt2 = m / (dt * dt);
@@ -478,24 +497,28 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, do
     const double Q[3] = {Q0, Q1, Q2};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const double f = a.fext ? a.fext[3 * n + c] : 0.0;
-        const double uc = a.u[3 * n + c];
-        const double up = a.u_pre_out[3 * n + c];
-        a.u_pre_out[3 * n + c] = inv * (f - Q[c] + mdt2 * (2.0 * uc - up) + dC / 2.0 / dt * up);
+        const double up = in.up[c];
+        a.u_pre_out[3 * n + c] = inv * (in.f[c] - Q[c] + mdt2 * (2.0 * in.uc[c] - up) + dC / 2.0 / dt * up);
     }
 }
 
+// MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer. Compile-time modes keep the
+// kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
+// which serialises the early node loads with the gather again.
+template <int MODE, bool FEXT, bool AOS, bool EARLY>
 __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
     const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
     if (n >= a.nN) return;
-    const long long cs = a.cstride;
+    NodeIn in;
+    if (EARLY) nodal_load<FEXT>(a, n, in);
+    const long long cs = AOS ? 1 : a.cstride;  // compile-time 1: a row's 3 loads merge into 2
     double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0;
-    if (a.qbuf) {
+    if (MODE == 2) {
         Q0 = a.qbuf[3 * n + 0];
         Q1 = a.qbuf[3 * n + 1];
         Q2 = a.qbuf[3 * n + 2];
-    } else if (a.inc8) {
+    } else if (MODE == 0) {
         const int4 lo = reinterpret_cast<const int4*>(a.inc8)[2 * n];
         const int4 hi = reinterpret_cast<const int4*>(a.inc8)[2 * n + 1];
         const int idx[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -522,13 +545,43 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
             Q2 += f[2 * cs];
         }
     }
-    nodal_update(a, n, Q0, Q1, Q2);
+    if (!EARLY) nodal_load<FEXT>(a, n, in);
+    nodal_update(a, n, in, Q0, Q1, Q2);
+}
+
+template <bool FEXT, bool AOS, bool EARLY>
+static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
+    if (a.qbuf)
+        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (a.inc8)
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <bool FEXT, bool AOS>
+static void launch_nodal_f(const NodalArgs& a, unsigned grid, hipStream_t s) {
+    if (a.early)
+        launch_nodal_e<FEXT, AOS, true>(a, grid, s);
+    else
+        launch_nodal_e<FEXT, AOS, false>(a, grid, s);
+}
+
+template <bool FEXT>
+static void launch_nodal_a(const NodalArgs& a, unsigned grid, hipStream_t s) {
+    if (a.cstride == 1)
+        launch_nodal_f<FEXT, true>(a, grid, s);
+    else
+        launch_nodal_f<FEXT, false>(a, grid, s);
 }
 
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
     if (a.nN <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((a.nN + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_nodal, dim3(grid), dim3(kBlock), 0, s, a);
+    if (a.fext)
+        launch_nodal_a<true>(a, grid, s);
+    else
+        launch_nodal_a<false>(a, grid, s);
     return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@ struct NodalArgs {
     const double* qbuf;    // if non-null: Q taken from this 3nN buffer (uploaded state), not from fe
     const double* fext;    // external force 3nN or null (= 0)
     long long cstride;     // component stride of fe (inc / inc8 hold base offsets)
+    int early;             // 1: node operands loaded before the gather (in flight with the indices)
     long long nN;
     double dt;
 };
