@@ -177,14 +177,15 @@ static hipEvent_t prof_event(hakai_ctx* c) {
 
 namespace hkc {
 void prof_begin(hakai_ctx* c, int kernel, EventPair* p) {
-    if (!c->prof) return;
+    p->kernel = -1;
+    if (!c->prof || !((c->prof_mask >> kernel) & 1u)) return;
     p->kernel = kernel;
     p->a = prof_event(c);
     p->b = prof_event(c);
     (void)hipEventRecord(p->a, c->stream);
 }
 void prof_end(hakai_ctx* c, EventPair* p) {
-    if (!c->prof) return;
+    if (!c->prof || p->kernel < 0) return;
     (void)hipEventRecord(p->b, c->stream);
     c->ev_pending.push_back(*p);
 }
@@ -885,10 +886,13 @@ int hakai_node_stress_strain(hakai_ctx* c, double* node_stress, double* node_str
     return 0;
 }
 
-int hakai_profile_enable(hakai_ctx* c, int on) {
+int hakai_profile_enable(hakai_ctx* c, int on) { return hakai_profile_mask(c, on ? (1u << HAKAI_K_COUNT) - 1 : 0u); }
+
+int hakai_profile_mask(hakai_ctx* c, uint32_t mask) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
-    if (!on) prof_harvest(c);
-    c->prof = on != 0;
+    if (!mask) prof_harvest(c);
+    c->prof = mask != 0;
+    c->prof_mask = mask;
     for (int k = 0; k < HAKAI_K_COUNT; ++k) {
         c->k_ms[k] = 0;
         c->k_n[k] = 0;

@@ -685,7 +685,14 @@ int contact_check(hakai_ctx* c) {
 extern "C" {
 
 int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance) {
+    return hakai_set_contact_cp(c, contact_flag, element_instance, 0, nullptr, nullptr, nullptr);
+}
+
+int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
+                         const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
+        return fail(HAKAI_ERR_ARG, "set_contact_cp: bad contact-pair arrays");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_contact before upload_model");
     HIPCHK(hipSetDevice(c->device));
     hkc::contact_destroy(c);
@@ -712,18 +719,55 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
     const int ni = (int)inst.size();
     if (ni == 0) return 0;
     for (auto& I : inst) build_instance(I, c->h_coord, c->h_conn);
-    // pairs (:273-311) and CT entries (:332-396)
+    // pairs (:273-311) and CT entries (:332-396). With *Contact Pair surfaces the exterior faces of
+    // each side are restricted to the surface's elements (get_surface_triangle's "pick up only
+    // contact element", :2087-2112 -- applied only when the list is not the whole instance).
+    struct CtDef {
+        int a, b;                                  // a: points (i side), b: triangles (j side)
+        const std::vector<char>* fa = nullptr;     // element filters (instance-local), null = all
+        const std::vector<char>* fb = nullptr;
+    };
+    std::vector<std::vector<char>> filters;
+    filters.reserve(2 * (size_t)n_cp);
     std::vector<std::pair<int, int>> cp;
-    if (ni > 1) {
+    std::vector<std::pair<const std::vector<char>*, const std::vector<char>*>> cpf;
+    if (n_cp > 0) {
+        for (int k = 0; k < n_cp; ++k) {
+            const std::vector<char>* f[2] = {nullptr, nullptr};
+            int id[2];
+            for (int s = 0; s < 2; ++s) {
+                id[s] = cp_instance[2 * k + s] - 1;
+                if (id[s] < 0 || id[s] >= ni) return fail(HAKAI_ERR_ARG, "contact pair %d: instance %d", k + 1, id[s] + 1);
+                const long long b0 = cp_elem_off[2 * k + s], b1 = cp_elem_off[2 * k + s + 1];
+                std::vector<char> bm((size_t)inst[id[s]].nE, 0);
+                for (long long q = b0; q < b1; ++q) {
+                    const long long el = cp_elems[q];
+                    if (el < 1 || el > inst[id[s]].nE)
+                        return fail(HAKAI_ERR_ARG, "contact pair %d: element %lld not in instance %d", k + 1, el, id[s] + 1);
+                    bm[el - 1] = 1;
+                }
+                if (b1 - b0 != inst[id[s]].nE) {  // the reference compares the list length only (:2087)
+                    filters.push_back(std::move(bm));
+                    f[s] = &filters.back();
+                }
+            }
+            cp.push_back({id[0], id[1]});
+            cpf.push_back({f[0], f[1]});
+        }
+    } else if (ni > 1) {
         for (int i = 0; i < ni; ++i)
-            for (int j = (contact_flag == 2 ? i : i + 1); j < ni; ++j) cp.push_back({i, j});
+            for (int j = (contact_flag == 2 ? i : i + 1); j < ni; ++j) {
+                cp.push_back({i, j});
+                cpf.push_back({nullptr, nullptr});
+            }
     } else {
         cp.push_back({0, 0});
+        cpf.push_back({nullptr, nullptr});
     }
-    std::vector<std::pair<int, int>> ct;
-    for (auto& p : cp) {
-        ct.push_back(p);
-        if (p.first != p.second) ct.push_back({p.second, p.first});
+    std::vector<CtDef> ct;
+    for (size_t k = 0; k < cp.size(); ++k) {
+        ct.push_back({cp[k].first, cp[k].second, cpf[k].first, cpf[k].second});
+        if (cp[k].first != cp[k].second) ct.push_back({cp[k].second, cp[k].first, cpf[k].second, cpf[k].first});
     }
     auto* C = new hkc::Contact();
     C->npairs = (int)ct.size();
@@ -751,14 +795,18 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
     std::vector<int> nj_pair, nj_node, nj_orig, nj_aptr{0}, nj_add;
     std::vector<int> tri_pair, tri_nodes, tri_ele, tri_adder, seg;
     // node list of a pair side: initial exterior nodes + nodes exposed by each element's deletion
-    auto node_list = [&](int pr, const Inst& I, bool with_adds, std::vector<int>& vp, std::vector<int>& vn,
-                         std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd) {
+    auto keep = [](const Inst& I, const std::vector<char>* filt, int f) {
+        return !filt || (*filt)[I.faces[f].ele - I.e0];
+    };
+    auto node_list = [&](int pr, const Inst& I, const std::vector<char>* filt, bool with_adds, std::vector<int>& vp,
+                         std::vector<int>& vn, std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd) {
         // per node: initial (exterior) or the ascending list of elements whose deletion exposes it;
         // bucketed by node id in linear time (adders arrive in ascending element order)
         const int nN = (int)c->nN;
         std::vector<char> orig((size_t)nN, 0), seen((size_t)nN, 0);
         for (int f : I.exterior)
-            for (int q = 0; q < 4; ++q) orig[I.faces[f].n[q]] = seen[I.faces[f].n[q]] = 1;
+            if (keep(I, filt, f))
+                for (int q = 0; q < 4; ++q) orig[I.faces[f].n[q]] = seen[I.faces[f].n[q]] = 1;
         std::vector<int> cnt((size_t)nN + 1, 0), adders;
         if (with_adds) {
             for (int j = 0; j < I.nE; ++j)
@@ -796,7 +844,7 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
     };
     int hoff = 0;
     for (int pr = 0; pr < C->npairs; ++pr) {
-        const int a = ct[pr].first, b = ct[pr].second;  // a: points (i), b: triangles (j)
+        const int a = ct[pr].a, b = ct[pr].b;  // a: points (i), b: triangles (j)
         const bool self = a == b;
         PairParam pp;
         pp.young = inst[b].young;  // :367
@@ -807,10 +855,11 @@ int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element
         const size_t ni0 = ni_node.size(), nj0 = nj_node.size();
         // surface update (:766-804): c_nodes_i grows for every pair whose point instance lost an
         // element; triangles and c_nodes_j grow only when the triangle instance differs
-        const long long c_i = node_list(pr, inst[a], true, ni_pair, ni_node, ni_orig, ni_aptr, ni_add);
-        const long long c_j = node_list(pr, inst[b], !self, nj_pair, nj_node, nj_orig, nj_aptr, nj_add);
+        const long long c_i = node_list(pr, inst[a], ct[pr].fa, true, ni_pair, ni_node, ni_orig, ni_aptr, ni_add);
+        const long long c_j = node_list(pr, inst[b], ct[pr].fb, !self, nj_pair, nj_node, nj_orig, nj_aptr, nj_add);
         long long c_t = 0;
         for (int f : inst[b].exterior) {
+            if (!keep(inst[b], ct[pr].fb, f)) continue;
             const int* n = inst[b].faces[f].n;
             const int tv[6] = {n[0], n[1], n[2], n[2], n[3], n[0]};  // :2140-2145
             for (int h = 0; h < 2; ++h) {

@@ -90,6 +90,7 @@ struct hakai_ctx {
     hkc::Contact* contact = nullptr;
     // profiling
     bool prof = false;
+    uint32_t prof_mask = 0;      // bit k: time kernel k (HAKAI_K_*)
     std::vector<hipEvent_t> ev_pool;
     std::vector<EventPair> ev_pending;
     double k_ms[HAKAI_K_COUNT] = {0, 0, 0, 0};

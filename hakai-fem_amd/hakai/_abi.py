@@ -56,7 +56,8 @@ class InpModelT(ctypes.Structure):
                 ("mass_scaling", c_double), ("contact_flag", c_int32), ("bc", BCT),
                 ("n_ic_dofs", c_int64), ("ic_dofs", PI64), ("ic_values", PD), ("n_instance", c_int32),
                 ("instance_node_offset", PI64), ("instance_element_offset", PI64),
-                ("instance_nElement", PI64), ("n_contact_pairs", c_int32)]
+                ("instance_nElement", PI64), ("n_cp", c_int32), ("cp_instance", PI32), ("cp_elem_off", PI64),
+                ("cp_elems", PI64)]
 
 
 class HakaiError(RuntimeError):
@@ -100,8 +101,10 @@ def lib() -> ctypes.CDLL:
                                       c_double, PD, PD]),
         "hakai_profile_enable": (c_int, [c_void_p, c_int]),
         "hakai_profile_read": (c_int, [c_void_p, c_int, PD, PI64]),
+        "hakai_profile_mask": (c_int, [c_void_p, ctypes.c_uint32]),
         "hakai_set_tuning": (c_int, [c_void_p, c_char_p, c_int64]),
         "hakai_set_contact": (c_int, [c_void_p, c_int32, PI64]),
+        "hakai_set_contact_cp": (c_int, [c_void_p, c_int32, PI64, c_int32, PI32, PI64, PI64]),
         "hakai_set_contact_params": (c_int, [c_void_p, c_double, c_double, c_double, c_double, c_double]),
         "hakai_contact_info": (c_int, [c_void_p, POINTER(c_int32), PI64, c_int32, PD]),
         "hakai_contact_force": (c_int, [c_void_p, c_double, c_double, PD]),
@@ -131,8 +134,8 @@ def exported_symbols() -> list[str]:
         "hakai_upload_model", "hakai_set_bc", "hakai_reset_state", "hakai_upload_state",
         "hakai_download_state", "hakai_step", "hakai_sync", "hakai_deleted", "hakai_negative_jacobians",
         "hakai_node_stress_strain", "hakai_stress_hexa", "hakai_triax_stress", "hakai_lumped_mass",
-        "hakai_profile_enable", "hakai_profile_read", "hakai_set_tuning", "hakai_set_contact",
-        "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",
+        "hakai_profile_enable", "hakai_profile_mask", "hakai_profile_read", "hakai_set_tuning", "hakai_set_contact",
+        "hakai_set_contact_cp", "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",
         "hakai_comm_init_local", "hakai_set_interface", "hakai_set_element_offset", "hakai_inp_read", "hakai_inp_free", "hakai_write_vtk", "hakai_run_inp",
     ]
 

@@ -93,7 +93,7 @@ def config_c5(layers: int = 1600, n: int = 100) -> Model:
 
 
 def two_body_model(plate=(8, 8, 2), impactor=(4, 4, 4), gap=0.1, v=-1e5, material: Material | None = None,
-                   perturb=0.0, seed=0, d_time=1e-7, n_steps=1000, contact_flag=1, myu=None,
+                   perturb=0.0, seed=0, d_time=1e-7, n_steps=1000, contact_flag=1, myu=None, surfaces=False,
                    name="two_body") -> Model:
     """Two instances: a plate (instance 1) clamped on its bottom face and an impactor block
     (instance 2) above it, centred in x/y, `gap` mm away, with initial velocity v along z.
@@ -112,10 +112,15 @@ def two_body_model(plate=(8, 8, 2), impactor=(4, 4, 4), gap=0.1, v=-1e5, materia
     inst = np.concatenate([np.ones(e1.shape[0], np.int64), np.full(e2.shape[0], 2, np.int64)])
     imp_nodes = np.arange(n1 + 1, coord.shape[0] + 1, dtype=np.int64)
     params = None if myu is None else (float(myu), 1.0, 1.0, 0.0, 0.0)
+    cps = None
+    if surfaces:  # *Contact Pair: plate top element layer vs impactor bottom element layer
+        top = np.arange((pz - 1) * px * py + 1, pz * px * py + 1, dtype=np.int64)
+        bottom = np.arange(1, ix * iy + 1, dtype=np.int64)
+        cps = [((1, top), (2, bottom))]
     return Model(coord, elem, np.ones(elem.shape[0], np.int64), [mat], bc=[encastre(plane_nodes(px, py, 0))],
                  ic_dofs=imp_nodes * 3, ic_values=np.full(imp_nodes.shape[0], float(v)), d_time=d_time,
                  end_time=d_time * n_steps, contact_flag=contact_flag, element_instance=inst, name=name,
-                 contact_params=params)
+                 contact_params=params, contact_pairs=cps)
 
 
 def config_c4(scale: int = 1) -> Model:

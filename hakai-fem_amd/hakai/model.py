@@ -54,6 +54,18 @@ class Model:
     # cal_contact_force constants (myu, kc_o, kc_s, Cr_o, Cr_s); None = the reference's
     # hard-coded (0.25, 1, 1, 0, 0) (v2/HAKAI_j.jl:2255-2259)
     contact_params: tuple | None = None
+    # *Contact Pair surfaces: [((instance, elements), (instance, elements)), ...] with 1-based
+    # instances and instance-local 1-based element ids; None = all-exterior contact
+    contact_pairs: list | None = None
+
+    def c_contact_pairs(self):
+        """(n_cp, cp_instance int32[2n], cp_elem_off int64[2n+1], cp_elems int64[]) for the C ABI."""
+        cps = self.contact_pairs or []
+        inst = np.array([s[0] for cp in cps for s in cp], np.int32)
+        lists = [np.asarray(s[1], np.int64) for cp in cps for s in cp]
+        off = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+        els = np.concatenate(lists).astype(np.int64) if lists else np.zeros(0, np.int64)
+        return len(cps), np.ascontiguousarray(inst), np.ascontiguousarray(off), np.ascontiguousarray(els)
 
     def __post_init__(self):
         self.coordmat = np.ascontiguousarray(self.coordmat, dtype=np.float64)
@@ -194,7 +206,14 @@ def read_inp(path: str) -> Model:
                     bc.append(BCGroup(ents))
         ic_d = _arr(m.ic_dofs, m.n_ic_dofs, np.int64)
         ic_v = _arr(m.ic_values, m.n_ic_dofs, np.float64)
+        cps = None
+        if m.n_cp > 0:
+            inst = _arr(m.cp_instance, 2 * m.n_cp, np.int64)
+            off = _arr(m.cp_elem_off, 2 * m.n_cp + 1, np.int64)
+            els = _arr(m.cp_elems, int(off[-1]), np.int64)
+            cps = [tuple((int(inst[2 * k + s]), els[off[2 * k + s]:off[2 * k + s + 1]].copy()) for s in range(2))
+                   for k in range(m.n_cp)]
         return Model(coord, elem, emat, mats, bc, ic_d, ic_v, m.d_time, m.end_time, m.mass_scaling,
-                     m.contact_flag, einst, name=str(path))
+                     m.contact_flag, einst, name=str(path), contact_pairs=cps)
     finally:
         L.hakai_inp_free(out)

@@ -73,7 +73,9 @@ class Solver:
         if getattr(model, "contact_flag", 0) >= 1:
             inst = model.element_instance
             inst = np.ones(model.nElement, np.int64) if inst is None else np.ascontiguousarray(inst, np.int64)
-            check(self.L.hakai_set_contact(self.ctx, int(model.contact_flag), ptr(inst, I64)))
+            ncp, cpi, cpo, cpe = model.c_contact_pairs()
+            check(self.L.hakai_set_contact_cp(self.ctx, int(model.contact_flag), ptr(inst, I64), ncp,
+                                              ptr(cpi, ctypes.c_int32), ptr(cpo, I64), ptr(cpe, I64)))
             if getattr(model, "contact_params", None) is not None:
                 check(self.L.hakai_set_contact_params(self.ctx, *[float(x) for x in model.contact_params]))
         self.reset()
@@ -165,8 +167,12 @@ class Solver:
         return f
 
     # -- profiling (HIP events on the context's own stream) ------------------------------------
-    def profile(self, on: bool = True):
-        check(self.L.hakai_profile_enable(self.ctx, int(on)))
+    def profile(self, on: bool = True, kernels=None):
+        """Time kernels with HIP events on the context's stream (all, or the HAKAI_K_* ids given)."""
+        if kernels is None:
+            check(self.L.hakai_profile_enable(self.ctx, int(on)))
+        else:
+            check(self.L.hakai_profile_mask(self.ctx, sum(1 << k for k in kernels) if on else 0))
 
     def profile_read(self, kernel: int) -> tuple[float, int]:
         ms, n = ctypes.c_double(0), I64(0)

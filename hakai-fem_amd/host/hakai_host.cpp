@@ -7,6 +7,7 @@
 // (SURVEY.md §9): a multi-line *Amplitude keeps only its last line; assembly *Nset lookups for
 // *Boundary append every match while *Initial Conditions take the first; ENCASTRE fixes the 3 dofs;
 // directions > 3 are ignored; a BC block ends at "**" or the next "*Boundary".
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -151,6 +152,8 @@ struct Owned {
     std::vector<int64_t> amp_off, entry_off, dof_off, dofs, ic_dofs;
     std::vector<double> amp_t, amp_v, entry_val, ic_val;
     std::vector<int64_t> inst_noff, inst_eoff, inst_ne;
+    std::vector<int32_t> cp_inst;           // *Contact Pair: 2 instances per pair
+    std::vector<int64_t> cp_off, cp_elems;  // surface element lists (instance-local, 1-based)
 };
 
 void read_lines(const char* path, std::vector<std::string>& lines) {
@@ -583,9 +586,48 @@ void parse(const char* path, Owned& o) {
             contact_flag = 2;
             break;
         }
-    int n_contact_pairs = 0;  // explicit *Contact Pair blocks (:1063-1102)
-    for (long long i = 1; i <= n; ++i)
-        if (has(line(i), "*Contact Pair,")) ++n_contact_pairs;
+    // ---- *Surface (:517-564): element sets (face ids ignored), instance of the last listed elset
+    struct Surf {
+        std::string name;
+        int instance_id = 0;
+        std::vector<long long> elements;
+    };
+    std::vector<Surf> SURF;
+    for (long long i = 1; i <= n; ++i) {
+        if (!has(line(i), "*Surface,")) continue;
+        Surf sf;
+        sf.name = after(at(split(nospace(line(i)), ',', false), 3), "name=");
+        for (long long r = i + 1; r <= n; ++r) {
+            if (has(line(r), "*")) break;
+            const std::string es = at(split(nospace(line(r)), ',', false), 1);
+            for (auto& E : ELSET)
+                if (E.name == es) {
+                    sf.instance_id = E.instance_id;
+                    sf.elements.insert(sf.elements.end(), E.elements.begin(), E.elements.end());
+                }
+        }
+        std::sort(sf.elements.begin(), sf.elements.end());
+        sf.elements.erase(std::unique(sf.elements.begin(), sf.elements.end()), sf.elements.end());
+        SURF.push_back(sf);
+    }
+    // ---- *Contact Pair (:1063-1102): the two surfaces on the line after the keyword
+    o.cp_inst.clear();
+    o.cp_off.assign(1, 0);
+    o.cp_elems.clear();
+    for (long long i = 1; i <= n; ++i) {
+        if (!has(line(i), "*Contact Pair,")) continue;
+        const auto names = split(nospace(line(i + 1)), ',', false);
+        for (int s = 0; s < 2; ++s) {
+            const std::string& nm = at(names, s + 1);
+            const Surf* hit = nullptr;
+            for (auto& sf : SURF)
+                if (sf.name == nm) hit = &sf;
+            if (!hit || hit->instance_id == 0) throw ParseError{"*Contact Pair: unknown surface " + nm};
+            o.cp_inst.push_back(hit->instance_id);
+            o.cp_elems.insert(o.cp_elems.end(), hit->elements.begin(), hit->elements.end());
+            o.cp_off.push_back((int64_t)o.cp_elems.size());
+        }
+    }
 
     // ---- flatten into the C view
     o.coord = coordmat;
@@ -650,7 +692,10 @@ void parse(const char* path, Owned& o) {
     p.end_time = end_time;
     p.mass_scaling = mass_scaling;
     p.contact_flag = contact_flag;
-    p.n_contact_pairs = n_contact_pairs;
+    p.n_cp = (int32_t)o.cp_inst.size() / 2;
+    p.cp_instance = o.cp_inst.data();
+    p.cp_elem_off = o.cp_off.data();
+    p.cp_elems = o.cp_elems.data();
     p.bc.n_groups = (int32_t)BCS.size();
     p.bc.amp_n = o.amp_n.data();
     p.bc.amp_off = o.amp_off.data();
@@ -825,9 +870,6 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
         std::printf("nNode:%lld\nnElement:%lld\ncontact_flag:%d\n", (long long)M->nNode, (long long)M->nElement,
                     M->contact_flag);
     }
-    if (M->contact_flag >= 1 && M->n_contact_pairs > 0)
-        return fail(HAKAI_ERR_MODEL, "%s: *Contact Pair surfaces are not supported yet (all-exterior contact is)",
-                    fname);
     const long long nN = M->nNode, nE = M->nElement;
     const double d_time = M->d_time * std::sqrt(M->mass_scaling);  // v2/HAKAI_j.jl:114
     const double time_num = M->end_time / d_time;
@@ -847,7 +889,9 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
                                 diag_M.data())))
         return r;
     if ((r = hakai_set_bc(c, &M->bc))) return r;
-    if (M->contact_flag >= 1 && (r = hakai_set_contact(c, M->contact_flag, M->element_instance))) return r;
+    if (M->contact_flag >= 1 && (r = hakai_set_contact_cp(c, M->contact_flag, M->element_instance, M->n_cp,
+                                                          M->cp_instance, M->cp_elem_off, M->cp_elems)))
+        return r;
     if ((r = hakai_reset_state(c, M->n_ic_dofs, M->ic_dofs, M->ic_values, d_time))) return r;
     const long long n_steps = time_num >= 1.0 ? (long long)std::floor(time_num) : 0;
     const long long d_out = (long long)std::floor(time_num / 100);  // output_num = 100 (:471-472)

@@ -148,7 +148,9 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
 /* ---- profiling: per-kernel device time measured with HIP events on the context's stream ---- */
 enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_CONTACT = 4,
        HAKAI_K_COUNT = 5 };
-int hakai_profile_enable(hakai_ctx* ctx, int on);
+int hakai_profile_enable(hakai_ctx* ctx, int on);  /* all kernels on / off; resets the totals */
+/* Time only the kernels whose bit (1 << HAKAI_K_*) is set (fewer events in a timed loop). */
+int hakai_profile_mask(hakai_ctx* ctx, uint32_t mask);
 int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
 /* Tuning knobs for A/B measurements: "elem_pipe_blocks" (>0: persistent software-pipelined
  * element kernel on that many blocks, default 512; 0: one-batch-per-block kernel), "elem_minw"
@@ -163,6 +165,12 @@ int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
  * (:2167-2245, :766-804). *Contact Pair decks are not supported yet. Then every hakai_step
  * computes cal_contact_force (:2248-2706) into the external force before the nodal update. */
 int hakai_set_contact(hakai_ctx* ctx, int32_t contact_flag, const int64_t* element_instance);
+/* Same with explicit *Contact Pair surfaces (v2/readInpFile_j.jl:517-564, :1063-1102; pairs
+ * v2/HAKAI_j.jl:273-345): pair k couples instances cp_instance[2k], cp_instance[2k+1] (1-based);
+ * side s of pair k holds the surface's elements cp_elems[cp_elem_off[2k+s] .. cp_elem_off[2k+s+1])
+ * (instance-local, 1-based). n_cp = 0 is the all-exterior case of hakai_set_contact. */
+int hakai_set_contact_cp(hakai_ctx* ctx, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
+                         const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems);
 /* The constants hard-coded at v2/HAKAI_j.jl:2255-2259 (defaults myu 0.25, kc_o 1, kc_s 1,
  * Cr_o 0, Cr_s 0). BASELINE's C4 runs frictionless: myu = 0. */
 int hakai_set_contact_params(hakai_ctx* ctx, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s);
@@ -211,7 +219,10 @@ typedef struct {
     const int64_t* instance_node_offset;    /* [n_instance] */
     const int64_t* instance_element_offset; /* [n_instance] */
     const int64_t* instance_nElement;       /* [n_instance] */
-    int32_t n_contact_pairs;                /* *Contact Pair blocks (explicit surfaces; not supported yet) */
+    int32_t n_cp;                           /* *Contact Pair blocks (0: all-exterior contact) */
+    const int32_t* cp_instance;             /* [2 n_cp] instances (1-based) of the two surfaces */
+    const int64_t* cp_elem_off;             /* [2 n_cp + 1] into cp_elems */
+    const int64_t* cp_elems;                /* surface elements, instance-local 1-based */
 } hakai_inp_model_t;
 
 int hakai_inp_read(const char* path, hakai_inp_model_t** out);

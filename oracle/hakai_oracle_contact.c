@@ -116,8 +116,13 @@ static int same4(const int64_t* a, const int64_t* b) {
     return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
 }
 
-/* get_surface_triangle (all elements of the instance), v2/HAKAI_j.jl:1996-2164 */
-static void surface_triangles(const inst_t* I, ivec* tri, ivec* tri_ele, ivec* nodes) {
+/* get_surface_triangle, v2/HAKAI_j.jl:1996-2164. contact: instance-local 1-based element list of a
+ * *Contact Pair surface (n_contact < 0: all elements); like the reference the exterior faces are
+ * filtered only when the list length differs from the instance's element count (:2087). */
+static void surface_triangles_of(const inst_t* I, ivec* tri, ivec* tri_ele, ivec* nodes, const int64_t* contact,
+                                 int64_t n_contact);
+static void surface_triangles_of(const inst_t* I, ivec* tri, ivec* tri_ele, ivec* nodes, const int64_t* contact,
+                                 int64_t n_contact) {
     const int64_t F = 6 * I->nE;
     char* dp = (char*)calloc((size_t)F + 1, 1);
     for (int64_t j = 0; j < F - 1; ++j) { /* j = 1 : nE*6-1 */
@@ -129,6 +134,12 @@ static void surface_triangles(const inst_t* I, ivec* tri, ivec* tri_ele, ivec* n
                 dp[k] = 1;
                 break;
             }
+        if (u && n_contact >= 0 && n_contact != I->nE) { /* "pick up only contact element" */
+            const int64_t local = I->face_ele[j] - I->e0;  /* 1-based instance-local */
+            int in = 0;
+            for (int64_t q = 0; q < n_contact; ++q) in |= (contact[q] == local);
+            u = in;
+        }
         if (u) {
             const int64_t* f = I->faces + 4 * j;
             iv_push(tri, f[0]); iv_push(tri, f[1]); iv_push(tri, f[2]);
@@ -150,6 +161,12 @@ static void surface_triangles(const inst_t* I, ivec* tri, ivec* tri_ele, ivec* n
 
 hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
                                 const double* mat_young) {
+    return hko_contact_create_cp(mv, contact_flag, element_instance, mat_young, 0, NULL, NULL, NULL);
+}
+
+hko_contact* hko_contact_create_cp(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
+                                   const double* mat_young, int32_t n_cp, const int32_t* cp_instance,
+                                   const int64_t* cp_off, const int64_t* cp_elems) {
     if (contact_flag < 1) return NULL;
     hko_contact* C = (hko_contact*)calloc(1, sizeof(hko_contact));
     C->view = *mv;
@@ -171,10 +188,16 @@ hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, cons
         I->nE++;
     }
     for (int i = 0; i < n_inst; ++i) element_faces(mv, &C->inst[i]);
-    /* pairs, :273-311 (all exterior: no *Contact Pair) */
+    /* pairs, :273-311 (all exterior) or the *Contact Pair list (:1063-1102) */
     int np = 0;
-    int (*pi)[2] = (int (*)[2])malloc(sizeof(int[2]) * (size_t)(n_inst * (n_inst + 1) / 2 + 1));
-    if (n_inst > 1) {
+    int (*pi)[2] = (int (*)[2])malloc(sizeof(int[2]) * (size_t)(n_inst * (n_inst + 1) / 2 + 1 + n_cp));
+    if (n_cp > 0) {
+        for (int k = 0; k < n_cp; ++k) {
+            pi[np][0] = cp_instance[2 * k] - 1;
+            pi[np][1] = cp_instance[2 * k + 1] - 1;
+            ++np;
+        }
+    } else if (n_inst > 1) {
         for (int i = 0; i < n_inst; ++i)
             for (int j = (contact_flag == 2 ? i : i + 1); j < n_inst; ++j) {
                 pi[np][0] = i; pi[np][1] = j; ++np;
@@ -191,10 +214,16 @@ hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, cons
             ct_t* T = &C->ct[C->n_ct++];
             T->i_inst = prs[r][0];
             T->j_inst = prs[r][1];
+            /* surface lists of this CT entry (:347-365): side 1 of the CP when i is its instance_1 */
+            const int si = (r == 0) ? 0 : 1, sj = (r == 0) ? 1 : 0;
+            const int64_t* li = n_cp ? cp_elems + cp_off[2 * cc + si] : NULL;
+            const int64_t ni = n_cp ? cp_off[2 * cc + si + 1] - cp_off[2 * cc + si] : -1;
+            const int64_t* lj = n_cp ? cp_elems + cp_off[2 * cc + sj] : NULL;
+            const int64_t nj = n_cp ? cp_off[2 * cc + sj + 1] - cp_off[2 * cc + sj] : -1;
             ivec tri = {0}, te = {0};
-            surface_triangles(&C->inst[T->i_inst], &tri, &te, &T->nodes_i);
+            surface_triangles_of(&C->inst[T->i_inst], &tri, &te, &T->nodes_i, li, ni);
             free(tri.v); free(te.v);
-            surface_triangles(&C->inst[T->j_inst], &T->tri, &T->tri_ele, &T->nodes_j);
+            surface_triangles_of(&C->inst[T->j_inst], &T->tri, &T->tri_ele, &T->nodes_j, lj, nj);
             T->young = C->inst[T->j_inst].young;  /* :367 */
         }
     }

@@ -61,6 +61,8 @@ def lib():
         L.hko_pusai.argtypes = [PD]
         L.hko_contact_create.restype = c_void_p
         L.hko_contact_create.argtypes = [POINTER(View), c_int, PI64, PD]
+        L.hko_contact_create_cp.restype = c_void_p
+        L.hko_contact_create_cp.argtypes = [POINTER(View), c_int, PI64, PD, c_int32, POINTER(c_int32), PI64, PI64]
         L.hko_contact_destroy.argtypes = [c_void_p]
         L.hko_contact_set_params.argtypes = [c_void_p, c_double, c_double, c_double, c_double, c_double]
         L.hko_contact_force.restype = c_int64
@@ -134,8 +136,11 @@ class Oracle:
             self._young = np.array([mt.young for mt in model.materials], np.float64)
             self._view = View(nN, nE, _p(model.coordmat), _p(model.elementmat, c_int64),
                               _p(model.element_material, c_int64))
-            self.ct = self.L.hko_contact_create(ctypes.byref(self._view), int(model.contact_flag), _p(self._inst, c_int64),
-                                                _p(self._young))
+            ncp, cpi, cpo, cpe = model.c_contact_pairs()
+            self._cp = (cpi, cpo, cpe)
+            self.ct = self.L.hko_contact_create_cp(ctypes.byref(self._view), int(model.contact_flag),
+                                                   _p(self._inst, c_int64), _p(self._young), ncp, _p(cpi, c_int32),
+                                                   _p(cpo, c_int64), _p(cpe, c_int64))
             cp = getattr(model, "contact_params", None)
             if cp is not None:
                 self.L.hko_contact_set_params(self.ct, *[float(x) for x in cp])

@@ -40,7 +40,9 @@ def element_faces(coord, elem, e_ids):
     return faces, keys, owner
 
 
-def surface_triangle(faces, keys, owner):
+def surface_triangle(faces, keys, owner, contact=None, e0=0, nE=None):
+    """contact: instance-local 1-based element list of a *Contact Pair surface (None = all);
+    filtering applies only when its length differs from nE (v2/HAKAI_j.jl:2087)."""
     F = len(faces)
     dp = []
     surf = []
@@ -55,6 +57,9 @@ def surface_triangle(faces, keys, owner):
                 break
         if u:
             surf.append((faces[j], owner[j]))
+    if contact is not None and len(contact) != nE:
+        cs = set(int(x) for x in contact)
+        surf = [(f, e) for f, e in surf if e - e0 in cs]
     tri, tri_e = [], []
     for f, e in surf:
         tri += [[f[0], f[1], f[2]], [f[2], f[3], f[0]]]
@@ -73,15 +78,19 @@ class ContactRef:
         for i in range(ni):
             self.inst.append(element_faces(coord, elem, self.inst_elems[i]))
         young = [model.materials[model.element_material[es[0] - 1] - 1].young for es in self.inst_elems]
-        if ni > 1:
-            cp = [(i, j) for i in range(ni) for j in range(i if model.contact_flag == 2 else i + 1, ni)]
+        cps = getattr(model, "contact_pairs", None)
+        if cps:
+            cp = [(c[0][0] - 1, c[1][0] - 1, list(c[0][1]), list(c[1][1])) for c in cps]
+        elif ni > 1:
+            cp = [(i, j, None, None) for i in range(ni) for j in range(i if model.contact_flag == 2 else i + 1, ni)]
         else:
-            cp = [(0, 0)]
+            cp = [(0, 0, None, None)]
         self.ct = []
-        for a, b in cp:
-            for (pi, pj) in ([(a, b)] if a == b else [(a, b), (b, a)]):
-                _, _, ni_nodes = surface_triangle(*self.inst[pi])
-                tri, tri_e, nj_nodes = surface_triangle(*self.inst[pj])
+        for a, b, la, lb in cp:
+            for (pi, pj, li, lj) in ([(a, b, la, lb)] if a == b else [(a, b, la, lb), (b, a, lb, la)]):
+                e0i, e0j = self.inst_elems[pi][0] - 1, self.inst_elems[pj][0] - 1
+                _, _, ni_nodes = surface_triangle(*self.inst[pi], li, e0i, len(self.inst_elems[pi]))
+                tri, tri_e, nj_nodes = surface_triangle(*self.inst[pj], lj, e0j, len(self.inst_elems[pj]))
                 self.ct.append(dict(i=pi, j=pj, nodes_i=list(ni_nodes), nodes_j=list(nj_nodes), tri=tri,
                                     tri_e=tri_e, young=young[pj]))
         sizes = []

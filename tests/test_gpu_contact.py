@@ -95,13 +95,14 @@ def test_contact_with_deletion_surface_update():
     assert rel_err(g.disp, o.s["disp"]) < 1e-6
 
 
-def test_driver_runs_contact_deck(tmp_path):
-    """HAKAI(fname) on a *Contact deck written from code: contact on the device path, 101 VTK files,
-    final displacement equal to the oracle's to the VTK's %1.6e."""
+@pytest.mark.parametrize("surfaces", [False, True])
+def test_driver_runs_contact_deck(tmp_path, surfaces):
+    """HAKAI(fname) on a *Contact (all exterior) or *Contact Pair deck written from code: contact on
+    the device path, 101 VTK files, final displacement equal to the oracle's to the VTK's %1.6e."""
     import os
     import hakai
     from inp_writer import write_inp
-    m = mesh.two_body_model(plate=(5, 5, 2), impactor=(3, 3, 2), v=-1e5, n_steps=300)
+    m = mesh.two_body_model(plate=(5, 5, 2), impactor=(3, 3, 2), v=-1e5, n_steps=300, surfaces=surfaces)
     deck = write_inp(str(tmp_path / "impact.inp"), m)
     out = tmp_path / "out"
     hakai.hakai(deck, str(out), verbose=False)
@@ -114,3 +115,20 @@ def test_driver_runs_contact_deck(tmp_path):
     o.run(1, m.n_steps)
     ref = o.s["disp"].reshape(-1, 3)
     assert np.allclose(disp, ref, rtol=2e-6, atol=1e-9)
+
+
+def test_contact_pair_surfaces_parity():
+    """*Contact Pair surfaces (plate top layer vs impactor bottom layer): same pair lists as the
+    oracle, same trajectory."""
+    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.02, seed=1, surfaces=True,
+                            n_steps=300)
+    o = O.Oracle(m)
+    want = [(p["i_instance"], p["j_instance"], p["n_nodes_i"], p["n_triangles"], p["n_nodes_j"])
+            for p in o.contact_pairs()]
+    o.run(1, m.n_steps)
+    with Solver(m) as sv:
+        pairs, _ = sv.contact_info()
+        sv.step(1, m.n_steps)
+        g = sv.download()
+    assert pairs == want
+    assert rel_err(g.disp, o.s["disp"]) < 1e-9

@@ -103,7 +103,7 @@ def _dof_map(groups):
     return out
 
 
-@pytest.mark.parametrize("which", ["tensile5e", "two_body", "two_body_self", "bar_ic"])
+@pytest.mark.parametrize("which", ["tensile5e", "two_body", "two_body_self", "two_body_cp", "bar_ic"])
 def test_written_decks_round_trip(tmp_path, which):
     """Decks written from code (tests/inp_writer.py) read back by the C++ reader to the same model:
     the path the GPU-box driver tests use, since the box has no reference decks."""
@@ -111,6 +111,7 @@ def test_written_decks_round_trip(tmp_path, which):
     m = {"tensile5e": mesh.tensile5e_model,
          "two_body": lambda: mesh.two_body_model(perturb=0.05, seed=3),
          "two_body_self": lambda: mesh.two_body_model(contact_flag=2),
+         "two_body_cp": lambda: mesh.two_body_model(surfaces=True),
          "bar_ic": lambda: mesh.bar_model(2, 3, 4, mesh.steel_ductile(), lambda z, L: 1e4 * z / L, perturb=0.02)}[which]()
     path = write_inp(str(tmp_path / "deck.inp"), m)
     a = hakai.read_inp(path)
@@ -125,3 +126,7 @@ def test_written_decks_round_trip(tmp_path, which):
     for x, y in zip(a.materials, m.materials):
         assert (x.density, x.young, x.poisson) == (y.density, y.young, y.poisson)
         assert np.array_equal(x.plastic, np.asarray(y.plastic).reshape(-1, 2))
+    assert (a.contact_pairs is None) == (m.contact_pairs is None)
+    for p, q in zip(a.contact_pairs or [], m.contact_pairs or []):
+        for (ia, ea), (ib, eb) in zip(p, q):
+            assert ia == ib and np.array_equal(ea, eb)
