@@ -418,7 +418,7 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     HIPCHK(dalloc(&c->d_conn, 8 * (size_t)nEp));
     HIPCHK(dalloc(&c->d_flag, (size_t)nEp));
     HIPCHK(dalloc(&c->d_mat, (size_t)nEp));
-    HIPCHK(dalloc(&c->d_del_step, (size_t)nEp + 1));
+    HIPCHK(dalloc(&c->d_del_step, (size_t)nEp + 2));
     HIPCHK(dalloc(&c->d_mats, (size_t)nMat));
     HIPCHK(dalloc(&c->d_stress, 6 * ld));
     HIPCHK(dalloc(&c->d_strain, 6 * ld));
@@ -531,7 +531,7 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     HIPCHK(hipMemsetAsync(c->d_u[0], 0, fn * sizeof(double), s));
     HIPCHK(hipMemsetAsync(c->d_u[1], 0, fn * sizeof(double), s));
     HIPCHK(hipMemsetAsync(c->d_fe, 0, (size_t)c->fe_len * sizeof(double), s));
-    HIPCHK(hipMemsetAsync(c->d_del_step, 0, ((size_t)c->nEp + 1) * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(c->d_del_step, 0, ((size_t)c->nEp + 2) * sizeof(int), s));
     HIPCHK(hk::launch_reset_gp(c->d_stress, c->d_strain, c->d_eqps, c->d_yield, c->d_triax, c->d_flag, c->d_mat,
                                c->d_mats, c->nE, c->nEp, c->ld, s));
     c->h_velo0.assign(fn, 0.0);
@@ -599,6 +599,7 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
         std::vector<int> ds((size_t)c->nE);
         for (long long e = 0; e < c->nE; ++e) ds[e] = f[e] ? 0 : -1;
         HIPCHK(hipMemcpyAsync(c->d_del_step, ds.data(), c->nE * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(c->d_del_step + c->nEp, 0, 2 * sizeof(int), s));  // dump + last-deletion slots
         HIPCHK(hipStreamSynchronize(s));
         // fe of elements uploaded as deleted must not contribute
         bool any = false;
@@ -834,6 +835,10 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
             return 0;
         }
         return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
+    }
+    if (!std::strncmp(key, "contact_", 8)) {
+        HIPCHK(hipSetDevice(c->device));
+        return hkc::contact_tuning(c, key, value);
     }
     return fail(HAKAI_ERR_ARG, "unknown tuning key '%s'", key);
 }

@@ -59,21 +59,44 @@ struct Contact {
     int *d_ni_pair = nullptr, *d_ni_node = nullptr, *d_ni_orig = nullptr, *d_ni_aptr = nullptr, *d_ni_add = nullptr;
     int *d_nj_pair = nullptr, *d_nj_node = nullptr, *d_nj_orig = nullptr, *d_nj_aptr = nullptr, *d_nj_add = nullptr;
     int nseg = 0;
-    int* d_seg = nullptr;  // [nseg][4] (start, end, pair, side) node-entry segments
+    int* d_seg = nullptr;  // [nseg] Seg: node-entry segment (start, end, pair, side, region)
     // triangles
     int n_tri = 0;
     int *d_tri_pair = nullptr, *d_tri_nodes = nullptr, *d_tri_ele = nullptr, *d_tri_adder = nullptr;
+    // live lists (rebuilt on steps where the surface may have changed)
+    int ntile = 0, nreg = 0;
+    void* d_tiles = nullptr;        // [ntile] Tile
+    int *d_tile_cnt = nullptr, *d_tile_off = nullptr;            // [ntile], [ntile+1]
+    int* d_reg_first = nullptr;     // [nreg+1] first tile of each region
+    int* d_reg = nullptr;           // [nreg][2] (base, live count)
+    int* d_pair_reg = nullptr;      // [npairs][2] region of (pair, side)
+    int tri_reg = 0;
+    std::vector<int> reg_list_h;    // [nreg] list of each region (0 i-nodes, 1 j-nodes, 2 triangles)
+    // element -> entries its deletion exposes (CSR), and the deleted-element list of a step
+    int *d_el_tri_ptr = nullptr, *d_el_tri = nullptr, *d_el_ni_ptr = nullptr, *d_el_ni = nullptr;
+    int *d_el_nj_ptr = nullptr, *d_el_nj = nullptr, *d_dlist = nullptr;
+    int *d_ni_live = nullptr, *d_nj_live = nullptr, *d_tri_live = nullptr;
+    bool force_rebuild = true;
+    long long last_t = -1;
     // hash grid over i-nodes
     int htot = 0;
-    int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_ni_bucket = nullptr;
+    int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
     long long* d_ni_map = nullptr;
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
-    // events and per-node gather
+    // events and per-node gather over the touched nodes
     long long cap = 0;
-    unsigned int* d_evn = nullptr;  // [0] events this step, [1] max seen (overflow check)
+    unsigned int* d_ctl = nullptr;  // kCtl control words (events, max events, dirty, touched counts)
     int* d_ev_nodes = nullptr;      // [cap][4]
     double* d_ev_f = nullptr;       // [cap][3]
-    int *d_cnt = nullptr, *d_off = nullptr;
+    int* d_cnt = nullptr;           // [nN] terms per node (zero between steps)
+    int* d_tpos = nullptr;          // [nN] position of a touched node in its list
+    int* d_touched[2] = {nullptr, nullptr};  // ping-pong lists of nodes with contact force
+    int tsel = 0;
+    long long tcap = 0;
+    int* d_toff = nullptr;          // [tcap] start of each touched node's term range
+    int* d_tcnt = nullptr;          // [tcap] its length
+    int* d_cand = nullptr;          // [n_tri] triangles passing the prefilter
+    int tri_lanes = 32;             // lanes per candidate triangle (32: one per cell; 1: a loop over cells)
     double* d_terms = nullptr;      // [4 cap][3]
     void* d_tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -148,10 +171,36 @@ __device__ __forceinline__ Range pair_range(const unsigned long long* bb) {
     return r;
 }
 
-__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* evn) {
+// Control words (device): events this step, max events seen, full rebuild of the live lists,
+// incremental update (an element was deleted in the previous step), deleted elements found, and
+// the number of nodes with contact force in each of the two ping-pong "touched" lists.
+enum { kEv = 0, kEvMax = 1, kDirty = 2, kDel = 3, kNdel = 4, kTouched = 5 /* [5], [6] */, kNcand = 7, kTerms = 8,
+       kCtl = 16 };
+
+// Step prologue: pair boxes to (+inf, -inf), event counter to 0, full rebuild if the host forces
+// it, incremental update if an element was deleted in the previous step (del_any == t-1), and
+// the contact forces of the previous step's touched nodes back to 0 (external_force is otherwise
+// never rewritten).
+__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, int force, const int* del_any,
+                           int t, const int* touched_prev, int tsel, double* fext) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 12 * npairs) bbox[i] = ((i % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
-    if (i == 0) evn[0] = 0;
+    if (i == 0) {
+        ctl[kEv] = 0;
+        ctl[kDirty] = force ? 1u : 0u;
+        ctl[kDel] = (!force && *del_any == t - 1) ? 1u : 0u;
+        ctl[kNdel] = 0;
+        ctl[kNcand] = 0;
+        ctl[kTerms] = 0;
+        ctl[kTouched + tsel] = 0;
+    }
+    const int np = (int)ctl[kTouched + 1 - tsel];
+    for (int q = i; q < np; q += gridDim.x * blockDim.x) {
+        const int n = touched_prev[q];
+        fext[3 * (long long)n] = 0.0;
+        fext[3 * (long long)n + 1] = 0.0;
+        fext[3 * (long long)n + 2] = 0.0;
+    }
 }
 
 struct StepIn {
@@ -172,37 +221,221 @@ __device__ __forceinline__ void pos(const StepIn& s, int n, double p[3]) {
     for (int c = 0; c < 3; ++c) p[c] = s.coord[3 * n + c] + s.u[3 * n + c];  // position, :653-655
 }
 
-// live flags + bounding boxes of the live node lists per pair (:2281-2299)
-// Segment = the node entries of one pair side (entries are stored pair by pair). kSegBlocks blocks
-// per segment reduce in registers, then across the block (DPP-free shuffles + LDS), then issue ONE
-// atomic per bound: per-entry atomics on 12 shared addresses serialised the whole step.
-constexpr int kSegBlocks = 64;
+// ---- live lists -----------------------------------------------------------------------------
+// Every node entry / triangle that can ever appear is enumerated at setup (most of them are
+// interior and only become live if elements are deleted). The live ones are kept in index lists,
+// one region per pair side's node segment (at the segment's own offset, capacity = segment size)
+// and one for all triangles; reg[2r] = region base, reg[2r+1] = live count. Like the reference's
+// c_nodes / c_triangles they only grow (:766-804): a deletion appends the entries it exposes
+// (k_ct_append); triangles of deleted elements stay listed and are skipped at use (:2374-2377).
+// A full rebuild (setup, state upload/reset, a probe, a non-consecutive step) scans everything
+// in tiles of kTile entries that never straddle a region. Lists: 0 i-nodes, 1 j-nodes, 2 triangles.
+constexpr int kTilePer = 8;
+constexpr int kTile = kB * kTilePer;
+
+struct LiveIn {
+    const int *ni_orig, *ni_aptr, *ni_add, *nj_orig, *nj_aptr, *nj_add, *tri_ele, *tri_adder, *flag, *del_step;
+    int t;
+};
+
+__device__ __forceinline__ bool is_live(const LiveIn& L, int list, int k) {
+    if (list == 0) return live(L.ni_orig[k], L.ni_aptr, L.ni_add, k, L.del_step, L.t);
+    if (list == 1) return live(L.nj_orig[k], L.nj_aptr, L.nj_add, k, L.del_step, L.t);
+    const int ad = L.tri_adder[k];
+    if (ad < 0) return true;
+    const int st = L.del_step[ad];
+    return st != 0 && st < L.t;  // face exposed by a deletion in an earlier step
+}
+
+// block-wide exclusive scan of one int per thread (blockDim.x <= 1024 threads, s_w[blockDim.x/64]);
+// returns this thread's exclusive prefix, total = the block's sum
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+    const int nw = (int)blockDim.x >> 6;
+    for (int q = 0; q < nw; ++q) {
+        base += q < w ? s_w[q] : 0;
+        tot += s_w[q];
+    }
+    __syncthreads();
+    total = tot;
+    return base + x - v;
+}
+
+struct Tile {
+    int list, start, end, region;
+};
+
+__global__ __launch_bounds__(kB) void k_ct_live_count(const unsigned int* ctl, LiveIn L, const Tile* tiles,
+                                                      int ntile, int* tile_cnt) {
+    if (ctl[kDirty] == 0) return;
+    __shared__ int s_w[kB / 64];
+    for (int b = blockIdx.x; b < ntile; b += gridDim.x) {
+        const Tile tl = tiles[b];
+        int n = 0;
+        for (int q = 0; q < kTilePer; ++q) {
+            const int k = tl.start + (int)threadIdx.x + kB * q;
+            if (k < tl.end && is_live(L, tl.list, k)) ++n;
+        }
+        int tot;
+        block_excl_scan(n, s_w, tot);
+        if (threadIdx.x == 0) tile_cnt[b] = tot;
+    }
+}
+
+// one block: exclusive scan of the tile counts (tile_off[0..ntile]); region r = tiles
+// [reg_first[r], reg_first[r+1]) -> reg[2r+1] = its live count
+__global__ __launch_bounds__(kB) void k_ct_live_scan(const unsigned int* ctl, int ntile, const int* tile_cnt,
+                                                     int* tile_off, int nreg, const int* reg_first, int* reg) {
+    if (ctl[kDirty] == 0) return;
+    __shared__ int s_w[kB / 64];
+    int carry = 0;
+    constexpr int PER = 16;
+    for (int c0 = 0; c0 < ntile; c0 += kB * PER) {
+        const int b = c0 + (int)threadIdx.x * PER;
+        int v[PER], sum = 0;
+        for (int q = 0; q < PER; ++q) {
+            v[q] = b + q < ntile ? tile_cnt[b + q] : 0;
+            sum += v[q];
+        }
+        int tot;
+        int run = carry + block_excl_scan(sum, s_w, tot);
+        for (int q = 0; q < PER; ++q) {
+            if (b + q < ntile) tile_off[b + q] = run;
+            run += v[q];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) tile_off[ntile] = carry;
+    __syncthreads();  // this block's global stores are visible to its own threads after the barrier
+    for (int r = threadIdx.x; r < nreg; r += kB) reg[2 * r + 1] = tile_off[reg_first[r + 1]] - tile_off[reg_first[r]];
+}
+
+__global__ __launch_bounds__(kB) void k_ct_live_write(const unsigned int* ctl, LiveIn L, const Tile* tiles,
+                                                      int ntile, const int* tile_off, const int* reg_first,
+                                                      const int* reg, int* out_ni, int* out_nj, int* out_tri) {
+    if (ctl[kDirty] == 0) return;
+    __shared__ int s_w[kB / 64];
+    for (int b = blockIdx.x; b < ntile; b += gridDim.x) {
+        const Tile tl = tiles[b];
+        const int k0 = tl.start + (int)threadIdx.x * kTilePer;
+        unsigned m = 0;
+        int n = 0;
+        for (int q = 0; q < kTilePer; ++q) {
+            const int k = k0 + q;
+            if (k < tl.end && is_live(L, tl.list, k)) {
+                m |= 1u << q;
+                ++n;
+            }
+        }
+        int tot;
+        int o = block_excl_scan(n, s_w, tot) + reg[2 * tl.region] + tile_off[b] - tile_off[reg_first[tl.region]];
+        int* out = tl.list == 0 ? out_ni : (tl.list == 1 ? out_nj : out_tri);
+        for (int q = 0; q < kTilePer; ++q)
+            if (m >> q & 1) out[o++] = k0 + q;
+    }
+}
+
+// incremental update, part 1: the elements deleted in the previous step (int4 sweep of del_step)
+__global__ void k_ct_find_del(unsigned int* ctl, const int* del_step, int nE, int t, int* dlist) {
+    if (ctl[kDel] == 0) return;
+    const int n4 = nE >> 2;
+    const int4* d4 = reinterpret_cast<const int4*>(del_step);
+    for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += gridDim.x * blockDim.x) {
+        const int4 d = d4[v];
+        if (d.x == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v;
+        if (d.y == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 1;
+        if (d.z == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 2;
+        if (d.w == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 3;
+    }
+    if (blockIdx.x == 0 && (int)threadIdx.x < nE - 4 * n4) {
+        const int e = 4 * n4 + (int)threadIdx.x;
+        if (del_step[e] == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = e;
+    }
+}
+
+// a node entry becomes live with the first deletion among its adders; of several adders deleted in
+// the same step, the lowest element id appends it
+__device__ __forceinline__ bool newly_live(const int* orig, const int* aptr, const int* add, int k, int e,
+                                           const int* del_step, int t) {
+    if (orig[k]) return false;
+    for (int a = aptr[k]; a < aptr[k + 1]; ++a) {
+        const int ad = add[a], st = del_step[ad];
+        if (st != 0 && st < t - 1) return false;  // live before (st = -1: deleted before an upload)
+        if (st == t - 1 && ad < e) return false;
+    }
+    return true;
+}
+
+struct AppendIn {
+    const int *el_tri_ptr, *el_tri, *el_ni_ptr, *el_ni, *el_nj_ptr, *el_nj;
+    const int *ni_orig, *ni_aptr, *ni_add, *ni_pair, *nj_orig, *nj_aptr, *nj_add, *nj_pair;
+    const int* pair_reg;  // [npairs][2] region of (pair, side), -1 if none
+    int tri_reg;
+};
+
+// incremental update, part 2: one block per deleted element, one thread per entry its deletion
+// exposes (triangles, then i-node entries, then j-node entries)
+__global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t, int* reg,
+                            int* ni_live, int* nj_live, int* tri_live) {
+    if (ctl[kDel] == 0) return;
+    const int nd = (int)ctl[kNdel];
+    for (int q = blockIdx.x; q < nd; q += gridDim.x) {
+        const int e = dlist[q];
+        const int t0 = A.el_tri_ptr[e], nt = A.el_tri_ptr[e + 1] - t0;
+        const int i0 = A.el_ni_ptr[e], ni = A.el_ni_ptr[e + 1] - i0;
+        const int j0 = A.el_nj_ptr[e], nj = A.el_nj_ptr[e + 1] - j0;
+        for (int x = threadIdx.x; x < nt + ni + nj; x += blockDim.x) {
+            if (x < nt) {  // unique adder per triangle
+                tri_live[atomicAdd(&reg[2 * A.tri_reg + 1], 1)] = A.el_tri[t0 + x];
+            } else if (x < nt + ni) {
+                const int k = A.el_ni[i0 + x - nt];
+                if (!newly_live(A.ni_orig, A.ni_aptr, A.ni_add, k, e, del_step, t)) continue;
+                const int r = A.pair_reg[2 * A.ni_pair[k]];
+                ni_live[reg[2 * r] + atomicAdd(&reg[2 * r + 1], 1)] = k;
+            } else {
+                const int k = A.el_nj[j0 + x - nt - ni];
+                if (!newly_live(A.nj_orig, A.nj_aptr, A.nj_add, k, e, del_step, t)) continue;
+                const int r = A.pair_reg[2 * A.nj_pair[k] + 1];
+                nj_live[reg[2 * r] + atomicAdd(&reg[2 * r + 1], 1)] = k;
+            }
+        }
+    }
+}
+
+// bounding boxes of the live node lists per pair (:2281-2299). Segment = the live node entries of
+// one pair side. kSegBlocks blocks per segment reduce in registers, then across the block
+// (shuffles + LDS), then issue ONE atomic per bound.
+constexpr int kSegBlocks = 256;
 
 struct Seg {
     int start, end, pair, side;  // side 0: i-nodes, 1: j-nodes
+    int region, pad[3];
 };
 
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
-__global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* ni_node, const int* ni_orig,
-                                                const int* ni_aptr, const int* ni_add, const int* nj_node,
-                                                const int* nj_orig, const int* nj_aptr, const int* nj_add,
-                                                unsigned long long* bbox, int* ni_bucket) {
+__global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                                const int* nj_live, const int* ni_node, const int* nj_node,
+                                                unsigned long long* bbox) {
     const Seg sg = segs[blockIdx.x / kSegBlocks];
     const int sub = blockIdx.x % kSegBlocks;
     const bool side_i = sg.side == 0;
     const int* node = side_i ? ni_node : nj_node;
-    const int* orig = side_i ? ni_orig : nj_orig;
-    const int* aptr = side_i ? ni_aptr : nj_aptr;
-    const int* add = side_i ? ni_add : nj_add;
+    const int* lst = (side_i ? ni_live : nj_live) + reg[2 * sg.region];
+    const int cnt = reg[2 * sg.region + 1];
     unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
-    for (int k = sg.start + sub * kB + (int)threadIdx.x; k < sg.end; k += kSegBlocks * kB) {
-        const bool on = live(orig[k], aptr, add, k, s.del_step, s.t);
-        if (side_i) ni_bucket[k] = on ? 0 : -1;
-        if (!on) continue;
+    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += kSegBlocks * kB) {
         double p[3];
-        pos(s, node[k], p);
+        pos(s, node[lst[q]], p);
         for (int d = 0; d < 3; ++d) {
             const unsigned long long e = enc(p[d]);
             mn[d] = umin64(mn[d], e);
@@ -235,69 +468,152 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
     }
 }
 
-// cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts
-__global__ void k_ct_bin(StepIn s, int n_ni, const int* ni_pair, const int* ni_node, const PairParam* par,
-                         const unsigned long long* bbox, int* ni_bucket, long long* ni_map, int* bcnt) {
+// cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts.
+// kSegBlocks blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
+__global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                               const int* ni_pair, const int* ni_node, const PairParam* par,
+                                               const unsigned long long* bbox, int* qbucket, long long* ni_map,
+                                               int* bcnt) {
 #pragma clang fp contract(off)
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_ni || ni_bucket[k] < 0) return;
-    const int pr = ni_pair[k];
-    const Range r = pair_range(bbox + 12 * pr);
-    double p[3];
-    pos(s, ni_node[k], p);
-    if (r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] || p[1] > r.mx[1] ||
-        p[2] > r.mx[2]) {  // the candidate test of :2514-2519, applied before binning
-        ni_bucket[k] = -1;
-        return;
+    const Seg sg = segs[blockIdx.x / kSegBlocks];
+    if (sg.side != 0) return;
+    const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
+    for (int q = (blockIdx.x % kSegBlocks) * kB + (int)threadIdx.x; q < n; q += kSegBlocks * kB) {
+        const int k = ni_live[base + q];
+        const int pr = ni_pair[k];
+        const Range r = pair_range(bbox + 12 * pr);
+        double p[3];
+        pos(s, ni_node[k], p);
+        if (r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] || p[1] > r.mx[1] ||
+            p[2] > r.mx[2]) {  // the candidate test of :2514-2519, applied before binning
+            qbucket[base + q] = -1;
+            continue;
+        }
+        const PairParam pp = par[pr];
+        long long m[3];
+        for (int d = 0; d < 3; ++d) {
+            m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
+            ni_map[3 * (long long)k + d] = m[d];
+        }
+        const int b = pp.hash_off + (int)(hash3(m[0], m[1], m[2]) & (unsigned)(pp.hash_size - 1));
+        qbucket[base + q] = b;
+        atomicAdd(&bcnt[b], 1);
     }
-    const PairParam pp = par[pr];
-    long long m[3];
-    for (int d = 0; d < 3; ++d) {
-        m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
-        ni_map[3 * (long long)k + d] = m[d];
-    }
-    const int b = pp.hash_off + (int)(hash3(m[0], m[1], m[2]) & (unsigned)(pp.hash_size - 1));
-    ni_bucket[k] = b;
-    atomicAdd(&bcnt[b], 1);
 }
 
-__global__ void k_ct_fill(int n_ni, const int* ni_bucket, const int* boff, int* bcnt, int* blist) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_ni) return;
-    const int b = ni_bucket[k];
-    if (b < 0) return;
-    const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-    blist[slot] = k;
+__global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
+                                                const int* qbucket, const int* boff, int* bcnt, int* blist) {
+    const Seg sg = segs[blockIdx.x / kSegBlocks];
+    if (sg.side != 0) return;
+    const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
+    for (int q = (blockIdx.x % kSegBlocks) * kB + (int)threadIdx.x; q < n; q += kSegBlocks * kB) {
+        const int b = qbucket[base + q];
+        if (b < 0) continue;
+        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
+        blist[slot] = ni_live[base + q];
+    }
 }
 
-// one thread per triangle: the body of the @floop at :2371-2698
-__global__ void k_ct_tri(StepIn s, int n_tri, const int* tri_pair, const int* tri_nodes, const int* tri_ele,
-                         const int* tri_adder, const PairParam* par, const unsigned long long* bbox, const int* boff,
-                         const int* blist, const int* ni_node, const long long* ni_map, double d_lim, double myu,
-                         unsigned int* evn, long long cap, int* ev_nodes, double* ev_f) {
+// wave-aggregated append: one atomic per wave; every lane of the wave must call it
+__device__ __forceinline__ unsigned wave_append(unsigned int* ctr, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = m ? __ffsll((long long)m) - 1 : 0;
+    unsigned base = 0;
+    if (m && lane == leader) base = atomicAdd(ctr, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
+}
+
+// triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
+// side of the range box along any axis -> candidate list
+__global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
+                                                      const int* tri_pair, const int* tri_nodes, const int* tri_ele,
+                                                      const unsigned long long* bbox, unsigned int* ctl, int* cand) {
+    const int n = *tri_cnt;
+    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {  // wave-uniform trip count
+        const int q = q0 + (int)threadIdx.x;
+        bool keep = false;
+        int j = 0;
+        if (q < n) {
+            j = tri_live[q];
+            keep = s.flag[tri_ele[j]] == 1;
+            if (keep) {
+                const Range r = pair_range(bbox + 12 * tri_pair[j]);
+                keep = !r.empty;
+                if (keep) {
+                    double p0[3], p1[3], p2[3];
+                    pos(s, tri_nodes[3 * j], p0);
+                    pos(s, tri_nodes[3 * j + 1], p1);
+                    pos(s, tri_nodes[3 * j + 2], p2);
+                    for (int d = 0; d < 3; ++d) {
+                        if (p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]) keep = false;
+                        if (p0[d] > r.mx[d] && p1[d] > r.mx[d] && p2[d] > r.mx[d]) keep = false;
+                    }
+                }
+            }
+        }
+        const unsigned slot = wave_append(&ctl[kNcand], keep);
+        if (keep) cand[slot] = j;
+    }
+}
+
+// events of one thread, kept in registers and appended with one atomic per wave (a same-address
+// atomic per event serialised the kernel); more than kEvLocal go out one by one
+constexpr int kEvLocal = 4;
+struct EvBuf {
+    int n, j0, j1, j2;
+    int i[kEvLocal];
+    double f[kEvLocal][3];
+};
+
+__device__ __forceinline__ void ev_write(int* ev_nodes, double* ev_f, long long e, int i, int j0, int j1, int j2,
+                                         double fx, double fy, double fz) {
+    int* en = ev_nodes + 4 * e;
+    en[0] = i;
+    en[1] = j0;
+    en[2] = j1;
+    en[3] = j2;
+    double* ef = ev_f + 3 * e;
+    ef[0] = fx;
+    ef[1] = fy;
+    ef[2] = fz;
+}
+
+// one (candidate triangle, neighbour cell) pair: the body of the @floop at :2371-2698 for the
+// i-nodes of one of the 27 cells around the triangle's first node. The lanes of a triangle each
+// compute its geometry (same expressions, same bits; the loads are shared); a cell whose hash
+// bucket an earlier cell of the same triangle already maps to is skipped, so every bucket is
+// visited once.
+__device__ __forceinline__ void tri_cell(const StepIn& s, int j, int cell, const int* tri_pair, const int* tri_nodes,
+                                         const int* tri_ele, const PairParam* par, const unsigned long long* bbox,
+                                         const int* boff, const int* blist, const int* ni_node,
+                                         const long long* ni_map, double d_lim, double myu, unsigned int* evn,
+                                         long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
 #pragma clang fp contract(off)
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_tri) return;
     const int eleid = tri_ele[j];
-    if (s.flag[eleid] != 1) return;  // :2374-2377
-    const int ad = tri_adder[j];
-    if (ad >= 0) {
-        const int st = s.del_step[ad];
-        if (!(st != 0 && st < s.t)) return;  // face not exposed yet
-    }
     const int pr = tri_pair[j];
     const Range r = pair_range(bbox + 12 * pr);
-    if (r.empty) return;
     const PairParam pp = par[pr];
+    long long mj[3];
+    {
+        double q0[3];
+        pos(s, tri_nodes[3 * j], q0);
+        for (int d = 0; d < 3; ++d) mj[d] = (long long)ceil((q0[d] - r.amn[d]) / pp.ddiv);
+    }
+    const unsigned hmask = (unsigned)(pp.hash_size - 1);
+    const int dz = cell / 9 - 1, dy = (cell / 3) % 3 - 1, dx = cell % 3 - 1;
+    const unsigned hb = hash3(mj[0] + dx, mj[1] + dy, mj[2] + dz) & hmask;
+    for (int c2 = 0; c2 < cell; ++c2)
+        if ((hash3(mj[0] + (c2 % 3 - 1), mj[1] + ((c2 / 3) % 3 - 1), mj[2] + (c2 / 9 - 1)) & hmask) == hb) return;
+    const int b = pp.hash_off + (int)hb;
+    const int sl0 = boff[b], sl1 = boff[b + 1];
+    if (sl0 == sl1) return;
     const int j0 = tri_nodes[3 * j], j1 = tri_nodes[3 * j + 1], j2 = tri_nodes[3 * j + 2];
     double q0[3], q1[3], q2[3];
     pos(s, j0, q0);
     pos(s, j1, q1);
     pos(s, j2, q2);
-    for (int d = 0; d < 3; ++d) {  // :2394-2411
-        if (q0[d] < r.mn[d] && q1[d] < r.mn[d] && q2[d] < r.mn[d]) return;
-        if (q0[d] > r.mx[d] && q1[d] > r.mx[d] && q2[d] > r.mx[d]) return;
-    }
     const double cx = (q0[0] + q1[0] + q2[0]) / 3.0, cy = (q0[1] + q1[1] + q2[1]) / 3.0,
                  cz = (q0[2] + q1[2] + q2[2]) / 3.0;
     const double R0 = my3norm(q0[0] - cx, q0[1] - cy, q0[2] - cz);
@@ -323,105 +639,199 @@ __global__ void k_ct_tri(StepIn s, int n_tri, const int* tri_pair, const int* tr
     const double im12 = A13 * A32 - A12 * A33, im22 = A11 * A33 - A13 * A31, im32 = A12 * A31 - A11 * A32;
     const double im13 = A12 * A23 - A13 * A22, im23 = A13 * A21 - A11 * A23, im33 = A11 * A22 - A12 * A21;
     const double kk = pp.young * S / Lmax * pp.kc;  // :2575
-    long long mj[3];
-    for (int d = 0; d < 3; ++d) mj[d] = (long long)ceil((q0[d] - r.amn[d]) / pp.ddiv);
     int el[8];
     if (pp.self)
         for (int a = 0; a < 8; ++a) el[a] = s.conn[8 * (long long)eleid + a];
-    int seen[27];
-    int ns = 0;
-    for (int dz = -1; dz <= 1; ++dz)
-        for (int dy = -1; dy <= 1; ++dy)
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int b =
-                    pp.hash_off + (int)(hash3(mj[0] + dx, mj[1] + dy, mj[2] + dz) & (unsigned)(pp.hash_size - 1));
-                bool dup = false;
-                for (int q = 0; q < ns; ++q) dup |= (seen[q] == b);
-                if (dup) continue;
-                seen[ns++] = b;
-                for (int sl = boff[b]; sl < boff[b + 1]; ++sl) {
-                    const int k = blist[sl];
-                    const long long* mk = ni_map + 3 * (long long)k;
-                    if (llabs(mj[0] - mk[0]) > 1 || llabs(mj[1] - mk[1]) > 1 || llabs(mj[2] - mk[2]) > 1) continue;
-                    const int i = ni_node[k];
-                    if (pp.self) {
-                        bool own = false;
-                        for (int a = 0; a < 8; ++a) own |= (i == el[a]);
-                        if (own) continue;
-                    }
-                    double p[3];
-                    pos(s, i, p);
-                    const double dpc = my3norm(p[0] - cx, p[1] - cy, p[2] - cz);
-                    if (dpc >= Rmax) continue;
-                    const double bx = p[0] - q0[0], by = p[1] - q0[1], bz = p[2] - q0[2];
-                    const double x1 = (im11 * bx + im12 * by + im13 * bz) / vdet;
-                    const double x2 = (im21 * bx + im22 * by + im23 * bz) / vdet;
-                    const double d = (im31 * bx + im32 * by + im33 * bz) / vdet;
-                    if (!(0.0 <= x1 && 0.0 <= x2 && x1 + x2 <= 1.0 && d > 0.0 && d <= d_lim)) continue;
-                    // velo = d_disp / d_time of the previous step (:628); the IC before step 1
-                    double vi[3], vj[3];
-                    for (int c = 0; c < 3; ++c) {
-                        if (s.velo0) {
-                            vi[c] = s.velo0[3 * i + c];
-                            vj[c] = s.velo0[3 * j0 + c];
-                        } else {
-                            vi[c] = (s.u[3 * i + c] - s.u_pre[3 * i + c]) / s.d_time;
-                            vj[c] = (s.u[3 * j0 + c] - s.u_pre[3 * j0 + c]) / s.d_time;
-                        }
-                    }
-                    const double vx = vi[0] - vj[0], vy = vi[1] - vj[1], vz = vi[2] - vj[2];
-                    const double mag_v = my3norm(vx, vy, vz);
-                    double vex = 0.0, vey = 0.0, vez = 0.0;
-                    if (mag_v > 0.0) {
-                        vex = vx / mag_v;
-                        vey = vy / mag_v;
-                        vez = vz / mag_v;
-                    }
-                    const double F = kk * d;
-                    double fx = F * nx, fy = F * ny, fz = F * nz;
-                    // damping: diag_M[i] indexes the dof vector with a node id (:2592)
-                    const double Cd = 2 * sqrt(s.mass[(i) / 3] * kk) * pp.Cr;
-                    const double fc_x = -Cd * vx, fc_y = -Cd * vy, fc_z = -Cd * vz;
-                    const double dot_ve_n = vex * nx + vey * ny + vez * nz;
-                    const double vsx = vex - dot_ve_n * nx, vsy = vey - dot_ve_n * ny, vsz = vez - dot_ve_n * nz;
-                    const double fric_x = -myu * F * vsx, fric_y = -myu * F * vsy, fric_z = -myu * F * vsz;
-                    fx += fric_x + fc_x;
-                    fy += fric_y + fc_y;
-                    fz += fric_z + fc_z;
-                    const unsigned e = atomicAdd(&evn[0], 1u);
-                    if ((long long)e < cap) {
-                        int* en = ev_nodes + 4 * (long long)e;
-                        en[0] = i;
-                        en[1] = j0;
-                        en[2] = j1;
-                        en[3] = j2;
-                        double* ef = ev_f + 3 * (long long)e;
-                        ef[0] = fx;
-                        ef[1] = fy;
-                        ef[2] = fz;
-                    }
-                }
+    for (int sl = sl0; sl < sl1; ++sl) {
+        const int k = blist[sl];
+        const long long* mk = ni_map + 3 * (long long)k;
+        if (llabs(mj[0] - mk[0]) > 1 || llabs(mj[1] - mk[1]) > 1 || llabs(mj[2] - mk[2]) > 1) continue;
+        const int i = ni_node[k];
+        if (pp.self) {
+            bool own = false;
+            for (int a = 0; a < 8; ++a) own |= (i == el[a]);
+            if (own) continue;
+        }
+        double p[3];
+        pos(s, i, p);
+        const double dpc = my3norm(p[0] - cx, p[1] - cy, p[2] - cz);
+        if (dpc >= Rmax) continue;
+        const double bx = p[0] - q0[0], by = p[1] - q0[1], bz = p[2] - q0[2];
+        const double x1 = (im11 * bx + im12 * by + im13 * bz) / vdet;
+        const double x2 = (im21 * bx + im22 * by + im23 * bz) / vdet;
+        const double d = (im31 * bx + im32 * by + im33 * bz) / vdet;
+        if (!(0.0 <= x1 && 0.0 <= x2 && x1 + x2 <= 1.0 && d > 0.0 && d <= d_lim)) continue;
+        // velo = d_disp / d_time of the previous step (:628); the IC before step 1
+        double vi[3], vj[3];
+        for (int c = 0; c < 3; ++c) {
+            if (s.velo0) {
+                vi[c] = s.velo0[3 * i + c];
+                vj[c] = s.velo0[3 * j0 + c];
+            } else {
+                vi[c] = (s.u[3 * i + c] - s.u_pre[3 * i + c]) / s.d_time;
+                vj[c] = (s.u[3 * j0 + c] - s.u_pre[3 * j0 + c]) / s.d_time;
             }
+        }
+        const double vx = vi[0] - vj[0], vy = vi[1] - vj[1], vz = vi[2] - vj[2];
+        const double mag_v = my3norm(vx, vy, vz);
+        double vex = 0.0, vey = 0.0, vez = 0.0;
+        if (mag_v > 0.0) {
+            vex = vx / mag_v;
+            vey = vy / mag_v;
+            vez = vz / mag_v;
+        }
+        const double F = kk * d;
+        double fx = F * nx, fy = F * ny, fz = F * nz;
+        // damping: diag_M[i] indexes the dof vector with a node id (:2592)
+        const double Cd = 2 * sqrt(s.mass[(i) / 3] * kk) * pp.Cr;
+        const double fc_x = -Cd * vx, fc_y = -Cd * vy, fc_z = -Cd * vz;
+        const double dot_ve_n = vex * nx + vey * ny + vez * nz;
+        const double vsx = vex - dot_ve_n * nx, vsy = vey - dot_ve_n * ny, vsz = vez - dot_ve_n * nz;
+        const double fric_x = -myu * F * vsx, fric_y = -myu * F * vsy, fric_z = -myu * F * vsz;
+        fx += fric_x + fc_x;
+        fy += fric_y + fc_y;
+        fz += fric_z + fc_z;
+        if (eb.n < kEvLocal) {
+            eb.j0 = j0;
+            eb.j1 = j1;
+            eb.j2 = j2;
+#pragma unroll
+            for (int u = 0; u < kEvLocal; ++u)
+                if (u == eb.n) {
+                    eb.i[u] = i;
+                    eb.f[u][0] = fx;
+                    eb.f[u][1] = fy;
+                    eb.f[u][2] = fz;
+                }
+            ++eb.n;
+        } else {
+            const unsigned e = atomicAdd(&evn[0], 1u);
+            if ((long long)e < cap) ev_write(ev_nodes, ev_f, e, i, j0, j1, j2, fx, fy, fz);
+        }
+    }
 }
 
-__global__ void k_ct_count(const unsigned int* evn, long long cap, const int* ev_nodes, int* cnt, unsigned int* evmax) {
-    const long long n = std::min<long long>((long long)evn[0], cap);
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(evmax, evn[0]);
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < 4 * n;
-         e += (long long)gridDim.x * blockDim.x)
-        atomicAdd(&cnt[ev_nodes[e]], 1);
+__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, const unsigned int* ncand, const int* cand,
+                                                const int* tri_pair, const int* tri_nodes, const int* tri_ele,
+                                                const PairParam* par, const unsigned long long* bbox, const int* boff,
+                                                const int* blist, const int* ni_node, const long long* ni_map,
+                                                double d_lim, double myu, unsigned int* evn, long long cap,
+                                                int* ev_nodes, double* ev_f) {
+    // 32 lanes per triangle (27 cells used): the triangle's data are wave-uniform loads, fetched once
+    const long long n = 32LL * (long long)*ncand;
+    const int lane = (int)(threadIdx.x & 63);
+    for (long long q0 = blockIdx.x * (long long)blockDim.x; q0 < n; q0 += (long long)gridDim.x * blockDim.x) {
+        const long long q = q0 + threadIdx.x;  // wave-uniform trip count (the append below is wave-wide)
+        EvBuf eb;
+        eb.n = 0;
+        eb.j0 = eb.j1 = eb.j2 = 0;
+        if (q < n && (q & 31) < 27)
+            tri_cell(s, cand[q >> 5], (int)(q & 31), tri_pair, tri_nodes, tri_ele, par, bbox, boff, blist, ni_node,
+                     ni_map, d_lim, myu, evn, cap, ev_nodes, ev_f, eb);
+        const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
+        int x = c;  // wave inclusive scan of the buffered counts
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        unsigned base = 0;
+        if (lane == 63 && x > 0) base = atomicAdd(&evn[0], (unsigned)x);
+        base = __shfl(base, 63) + (unsigned)(x - c);
+#pragma unroll
+        for (int u = 0; u < kEvLocal; ++u)
+            if (u < c && (long long)(base + u) < cap)
+                ev_write(ev_nodes, ev_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+    }
 }
 
-__global__ void k_ct_scatter(const unsigned int* evn, long long cap, const int* ev_nodes, const double* ev_f,
-                             const int* off, int* cnt, double* terms) {
+// one thread per candidate triangle, the 27 cells in a loop (the reference's loop structure)
+__global__ __launch_bounds__(128) void k_ct_tri1(StepIn s, const unsigned int* ncand, const int* cand,
+                                                 const int* tri_pair, const int* tri_nodes, const int* tri_ele,
+                                                 const PairParam* par, const unsigned long long* bbox,
+                                                 const int* boff, const int* blist, const int* ni_node,
+                                                 const long long* ni_map, double d_lim, double myu, unsigned int* evn,
+                                                 long long cap, int* ev_nodes, double* ev_f) {
+    const int n = (int)*ncand;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {
+        const int q = q0 + (int)threadIdx.x;
+        EvBuf eb;
+        eb.n = 0;
+        eb.j0 = eb.j1 = eb.j2 = 0;
+        if (q < n)
+            for (int cell = 0; cell < 27; ++cell)
+                tri_cell(s, cand[q], cell, tri_pair, tri_nodes, tri_ele, par, bbox, boff, blist, ni_node, ni_map,
+                         d_lim, myu, evn, cap, ev_nodes, ev_f, eb);
+        const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
+        int x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        unsigned base = 0;
+        if (lane == 63 && x > 0) base = atomicAdd(&evn[0], (unsigned)x);
+        base = __shfl(base, 63) + (unsigned)(x - c);
+#pragma unroll
+        for (int u = 0; u < kEvLocal; ++u)
+            if (u < c && (long long)(base + u) < cap)
+                ev_write(ev_nodes, ev_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+    }
+}
+
+// Per-node gather of the event terms over the nodes that received one ("touched", a compact list
+// instead of a pass over all nN nodes): count -> per-node term ranges by a wave-aggregated bump
+// allocator (ranges are disjoint; their order is irrelevant) -> scatter -> sum.
+__global__ void k_ct_count(unsigned int* ctl, long long cap, const int* ev_nodes, int* cnt, int* touched, int* tpos,
+                           int tsel) {
+    const long long n = 4 * std::min<long long>((long long)ctl[kEv], cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&ctl[kEvMax], ctl[kEv]);
+    for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
+        const long long e = e0 + threadIdx.x;
+        int node = -1;
+        bool first = false;
+        if (e < n) {
+            node = ev_nodes[e];
+            first = atomicAdd(&cnt[node], 1) == 0;
+        }
+        const unsigned q = wave_append(&ctl[kTouched + tsel], first);
+        if (first) {
+            touched[q] = node;
+            tpos[node] = (int)q;
+        }
+    }
+}
+
+__global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, const int* cnt, int* toff, int* tcnt) {
+    const int nt = (int)ctl[kTouched + tsel];
+    const int lane = (int)(threadIdx.x & 63);
+    for (int q0 = blockIdx.x * blockDim.x; q0 < nt; q0 += gridDim.x * blockDim.x) {
+        const int q = q0 + (int)threadIdx.x;
+        const int c = q < nt ? cnt[touched[q]] : 0;
+        int x = c;  // wave inclusive scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        unsigned base = 0;
+        if (lane == 63) base = atomicAdd(&ctl[kTerms], (unsigned)x);
+        base = __shfl(base, 63);
+        if (q < nt) {
+            toff[q] = (int)base + x - c;
+            tcnt[q] = c;
+        }
+    }
+}
+
+__global__ void k_ct_scatter(const unsigned int* ctl, long long cap, const int* ev_nodes, const double* ev_f,
+                             const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
-    const long long n = std::min<long long>((long long)evn[0], cap);
+    const long long n = std::min<long long>((long long)ctl[kEv], cap);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < 4 * n;
          e += (long long)gridDim.x * blockDim.x) {
         const int node = ev_nodes[e];
         const long long ev = e >> 2;
         const int role = (int)(e & 3);
-        const int slot = off[node] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
+        const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
         const double* f = ev_f + 3 * ev;
         double* o = terms + 3 * (long long)slot;
         if (role == 0) {  // c_force3[i] += f
@@ -437,22 +847,25 @@ __global__ void k_ct_scatter(const unsigned int* evn, long long cap, const int* 
 }
 
 // external_force = 0.0 + (sum of the node's terms), summed in double-double and rounded once
-__global__ void k_ct_sum(long long nN, const int* off, const double* terms, double* fext) {
+__global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
+                         const double* terms, double* fext) {
 #pragma clang fp contract(off)
-    const long long n = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (n >= nN) return;
-    const int a = off[n], b = off[n + 1];
-    for (int c = 0; c < 3; ++c) {
-        double s = 0.0, e = 0.0;
-        for (int q = a; q < b; ++q) {
-            const double x = terms[3 * (long long)q + c];
-            const double t = s + x;  // TwoSum
-            const double bp = t - s;
-            const double err = (s - (t - bp)) + (x - bp);
-            s = t;
-            e += err;
+    const int nt = (int)ctl[kTouched + tsel];
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
+        const long long n = touched[q];
+        const int a = toff[q], b = a + tcnt[q];
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0, e = 0.0;
+            for (int i = a; i < b; ++i) {
+                const double x = terms[3 * (long long)i + c];
+                const double t = s + x;  // TwoSum
+                const double bp = t - s;
+                const double err = (s - (t - bp)) + (x - bp);
+                s = t;
+                e += err;
+            }
+            fext[3 * n + c] = s + e;
         }
-        fext[3 * n + c] = s + e;
     }
 }
 
@@ -603,8 +1016,14 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_ni_pair); dfree(C->d_ni_node); dfree(C->d_ni_orig); dfree(C->d_ni_aptr); dfree(C->d_ni_add);
     dfree(C->d_nj_pair); dfree(C->d_nj_node); dfree(C->d_nj_orig); dfree(C->d_nj_aptr); dfree(C->d_nj_add);
     dfree(C->d_tri_pair); dfree(C->d_tri_nodes); dfree(C->d_tri_ele); dfree(C->d_tri_adder);
-    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_ni_bucket); dfree(C->d_ni_map);
-    dfree(C->d_bbox); dfree(C->d_evn); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_off);
+    if (C->d_tiles) (void)hipFree(C->d_tiles);
+    dfree(C->d_tile_cnt); dfree(C->d_tile_off); dfree(C->d_reg_first); dfree(C->d_reg); dfree(C->d_pair_reg);
+    dfree(C->d_el_tri_ptr); dfree(C->d_el_tri); dfree(C->d_el_ni_ptr); dfree(C->d_el_ni); dfree(C->d_el_nj_ptr);
+    dfree(C->d_el_nj); dfree(C->d_dlist);
+    dfree(C->d_ni_live); dfree(C->d_nj_live); dfree(C->d_tri_live);
+    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_ni_map);
+    dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
+    dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); dfree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0);
     if (C->d_tmp) (void)hipFree(C->d_tmp);
     delete C;
@@ -616,6 +1035,7 @@ void contact_state_reset(hakai_ctx* c, const double* velo0_host) {
     Contact* C = c->contact;
     if (!C) return;
     C->use_velo0 = true;
+    C->force_rebuild = true;
     if (velo0_host)
         (void)hipMemcpyAsync(C->d_velo0, velo0_host, 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice,
                              c->stream);
@@ -636,43 +1056,120 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     in.conn = c->d_conn;
     in.mass = c->d_mass;
     in.t = (int)t;
-    const int g12 = (12 * C->npairs + kB - 1) / kB;
-    hipLaunchKernelGGL(k_ct_reset, dim3(std::max(g12, 1)), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_evn);
-    if (C->nseg > 0)
-        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, (const Seg*)C->d_seg, C->d_ni_node,
-                           C->d_ni_orig, C->d_ni_aptr, C->d_ni_add, C->d_nj_node, C->d_nj_orig, C->d_nj_aptr,
-                           C->d_nj_add, C->d_bbox, C->d_ni_bucket);
-    if (C->n_ni > 0) {
-        hipLaunchKernelGGL(k_ct_bin, dim3((C->n_ni + kB - 1) / kB), dim3(kB), 0, s, in, C->n_ni, C->d_ni_pair,
-                           C->d_ni_node, C->d_par, C->d_bbox, C->d_ni_bucket, C->d_ni_map, C->d_bcnt);
+    if ((long long)in.t != C->last_t + 1) C->force_rebuild = true;
+    const int tsel = C->tsel = 1 - C->tsel;
+    hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl,
+                       C->force_rebuild ? 1 : 0, c->d_del_step + c->nEp + 1, in.t, C->d_touched[1 - tsel], tsel,
+                       c->d_fext);
+    C->force_rebuild = false;
+    C->last_t = in.t;
+    if (C->ntile > 0) {
+        LiveIn L;
+        L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
+        L.nj_orig = C->d_nj_orig; L.nj_aptr = C->d_nj_aptr; L.nj_add = C->d_nj_add;
+        L.tri_ele = C->d_tri_ele; L.tri_adder = C->d_tri_adder;
+        L.flag = c->d_flag; L.del_step = c->d_del_step; L.t = in.t;
+        const Tile* tl = (const Tile*)C->d_tiles;
+        const unsigned gt = (unsigned)std::min(C->ntile, 2048);
+        // full rebuild (forced steps only)
+        hipLaunchKernelGGL(k_ct_live_count, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_cnt);
+        hipLaunchKernelGGL(k_ct_live_scan, dim3(1), dim3(kB), 0, s, C->d_ctl, C->ntile, C->d_tile_cnt, C->d_tile_off,
+                           C->nreg, C->d_reg_first, C->d_reg);
+        hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
+                           C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+        // incremental update (steps after a deletion)
+        hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, c->d_del_step, (int)c->nE, in.t,
+                           C->d_dlist);
+        AppendIn A;
+        A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
+        A.el_ni_ptr = C->d_el_ni_ptr; A.el_ni = C->d_el_ni; A.el_nj_ptr = C->d_el_nj_ptr; A.el_nj = C->d_el_nj;
+        A.ni_orig = C->d_ni_orig; A.ni_aptr = C->d_ni_aptr; A.ni_add = C->d_ni_add; A.ni_pair = C->d_ni_pair;
+        A.nj_orig = C->d_nj_orig; A.nj_aptr = C->d_nj_aptr; A.nj_add = C->d_nj_add; A.nj_pair = C->d_nj_pair;
+        A.pair_reg = C->d_pair_reg;
+        A.tri_reg = C->tri_reg;
+        hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, c->d_del_step, in.t,
+                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+    }
+    if (C->nseg > 0) {
+        const Seg* sg = (const Seg*)C->d_seg;
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox);
+        hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt);
     }
     size_t tb = C->tmp_bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
-    if (C->n_ni > 0)
-        hipLaunchKernelGGL(k_ct_fill, dim3((C->n_ni + kB - 1) / kB), dim3(kB), 0, s, C->n_ni, C->d_ni_bucket,
-                           C->d_boff, C->d_bcnt, C->d_blist);
-    if (C->n_tri > 0)
-        hipLaunchKernelGGL(k_ct_tri, dim3((C->n_tri + 127) / 128), dim3(128), 0, s, in, C->n_tri, C->d_tri_pair,
-                           C->d_tri_nodes, C->d_tri_ele, C->d_tri_adder, C->d_par, C->d_bbox, C->d_boff, C->d_blist,
-                           C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evn, C->cap, C->d_ev_nodes, C->d_ev_f);
-    const unsigned ge = (unsigned)std::min<long long>((4 * C->cap + kB - 1) / kB, 2048);
-    hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_evn, C->cap, C->d_ev_nodes, C->d_cnt, C->d_evn + 1);
-    tb = C->tmp_bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_cnt, C->d_off, (int)c->nN + 1, s));
-    hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_evn, C->cap, C->d_ev_nodes, C->d_ev_f, C->d_off,
-                       C->d_cnt, C->d_terms);
-    hipLaunchKernelGGL(k_ct_sum, dim3((unsigned)((c->nN + kB - 1) / kB)), dim3(kB), 0, s, (long long)c->nN, C->d_off,
+    if (C->nseg > 0)
+        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
+                           C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist);
+    if (C->n_tri > 0) {
+        hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, 2048))),
+                           dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
+                           C->d_tri_nodes, C->d_tri_ele, C->d_bbox, C->d_ctl, C->d_cand);
+        if (C->tri_lanes == 32)
+            hipLaunchKernelGGL(k_ct_tri, dim3(4096), dim3(128), 0, s, in, C->d_ctl + kNcand, C->d_cand, C->d_tri_pair,
+                               C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_boff, C->d_blist, C->d_ni_node,
+                               C->d_ni_map, C->d_lim, C->myu, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f);
+        else
+            hipLaunchKernelGGL(k_ct_tri1, dim3(1024), dim3(128), 0, s, in, C->d_ctl + kNcand, C->d_cand,
+                               C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_boff, C->d_blist,
+                               C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f);
+    }
+    const unsigned ge = (unsigned)std::min<long long>((4 * C->cap + kB - 1) / kB, 1024);
+    hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->cap, C->d_ev_nodes, C->d_cnt,
+                       C->d_touched[tsel], C->d_tpos, tsel);
+    hipLaunchKernelGGL(k_ct_alloc, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
+                       C->d_tcnt);
+    hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f,
+                       C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
+    hipLaunchKernelGGL(k_ct_sum, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
                        C->d_terms, c->d_fext);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
 }
 
+int contact_tuning(hakai_ctx* c, const char* key, long long value) {
+    Contact* C = c->contact;
+    if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
+    if (!std::strcmp(key, "contact_tri_lanes")) {
+        if (value != 1 && value != 32) return fail(HAKAI_ERR_ARG, "contact_tri_lanes must be 1 or 32");
+        C->tri_lanes = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "contact_event_cap")) {
+        if (value < 1 || value > (1LL << 30)) return fail(HAKAI_ERR_ARG, "contact_event_cap out of range");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(C->d_ev_nodes);
+        dfree(C->d_ev_f);
+        dfree(C->d_terms);
+        dfree(C->d_touched[0]);
+        dfree(C->d_touched[1]);
+        dfree(C->d_toff);
+        dfree(C->d_tcnt);
+        C->cap = value;
+        C->tcap = std::min<long long>(c->nN, 4 * C->cap);
+        HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
+        HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
+        HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
+        HIPCHK(dalloc(&C->d_touched[0], (size_t)C->tcap));
+        HIPCHK(dalloc(&C->d_touched[1], (size_t)C->tcap));
+        HIPCHK(dalloc(&C->d_toff, (size_t)C->tcap));
+        HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
+        // the previous step's touched list is gone: clear external_force and its count
+        HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), c->stream));
+        HIPCHK(hipMemsetAsync(C->d_ctl + kTouched, 0, 2 * sizeof(unsigned int), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    return fail(HAKAI_ERR_ARG, "unknown tuning key '%s'", key);
+}
+
 int contact_check(hakai_ctx* c) {
     Contact* C = c->contact;
     if (!C) return 0;
     unsigned int mx = 0;
-    HIPCHK(hipMemcpyAsync(&mx, C->d_evn + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&mx, C->d_ctl + kEvMax, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if ((long long)mx > C->cap)
         return fail(HAKAI_ERR_STATE, "contact: %u events in one step exceed the buffer (%lld); raise "
@@ -882,10 +1379,11 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
                         tri_adder.push_back(inst[b].e0 + j);
                     }
                 }
-        if (ni_node.size() > ni0) seg.insert(seg.end(), {(int)ni0, (int)ni_node.size(), pr, 0});
-        if (nj_node.size() > nj0) seg.insert(seg.end(), {(int)nj0, (int)nj_node.size(), pr, 1});
+        if (ni_node.size() > ni0) seg.insert(seg.end(), {(int)ni0, (int)ni_node.size(), pr, 0, -1, 0, 0, 0});
+        if (nj_node.size() > nj0) seg.insert(seg.end(), {(int)nj0, (int)nj_node.size(), pr, 1, -1, 0, 0, 0});
+        // sized for the initial surface; nodes exposed later share buckets (slower, same result)
         int hs = 64;
-        while (hs < 2 * (int)(ni_node.size() - ni0)) hs <<= 1;
+        while (hs < 2 * c_i) hs <<= 1;
         pp.hash_off = hoff;
         pp.hash_size = hs;
         hoff += hs;
@@ -900,8 +1398,57 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     C->n_ni = (int)ni_node.size();
     C->n_nj = (int)nj_node.size();
     C->n_tri = (int)tri_ele.size();
-    C->nseg = (int)seg.size() / 4;
+    C->nseg = (int)seg.size() / 8;
     C->cap = std::max<long long>(1 << 16, 8LL * C->n_ni);
+    C->tcap = std::min<long long>(c->nN, 4 * C->cap);
+    // live-list regions: i-node segments, j-node segments, then the triangle list; tiles of
+    // kTile entries inside one region each (full rebuild)
+    std::vector<Tile> tiles;
+    std::vector<int> reg_first, reg;  // reg: [nreg][2] (base, count = 0)
+    std::vector<int> pair_reg(2 * (size_t)C->npairs, -1);
+    auto add_region = [&](int list, int a0, int a1) {
+        const int r = (int)reg_first.size();
+        reg_first.push_back((int)tiles.size());
+        C->reg_list_h.push_back(list);
+        reg.push_back(a0);
+        reg.push_back(0);
+        for (int k = a0; k < a1; k += kTile) tiles.push_back({list, k, std::min(a1, k + kTile), r});
+        return r;
+    };
+    for (int list = 0; list < 2; ++list)
+        for (int q = 0; q < C->nseg; ++q)
+            if (seg[8 * q + 3] == list) {
+                const int r = add_region(list, seg[8 * q], seg[8 * q + 1]);
+                seg[8 * q + 4] = r;
+                pair_reg[2 * (size_t)seg[8 * q + 2] + list] = r;
+            }
+    C->tri_reg = add_region(2, 0, C->n_tri);
+    C->nreg = (int)reg_first.size();
+    reg_first.push_back((int)tiles.size());
+    C->ntile = (int)tiles.size();
+    // element -> entries its deletion exposes (CSR over global element ids)
+    auto invert = [&](const std::vector<int>& aptr, const std::vector<int>& add, int n, std::vector<int>& ptr,
+                      std::vector<int>& idx) {
+        ptr.assign((size_t)nE + 1, 0);
+        for (int k = 0; k < n; ++k)
+            for (int a = aptr[k]; a < aptr[k + 1]; ++a) ptr[add[a] + 1]++;
+        for (int e = 0; e < nE; ++e) ptr[e + 1] += ptr[e];
+        idx.resize((size_t)ptr[nE]);
+        std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+        for (int k = 0; k < n; ++k)
+            for (int a = aptr[k]; a < aptr[k + 1]; ++a) idx[fill[add[a]]++] = k;
+    };
+    std::vector<int> el_ni_ptr, el_ni, el_nj_ptr, el_nj, el_tri_ptr, el_tri;
+    invert(ni_aptr, ni_add, C->n_ni, el_ni_ptr, el_ni);
+    invert(nj_aptr, nj_add, C->n_nj, el_nj_ptr, el_nj);
+    {
+        std::vector<int> taptr((size_t)C->n_tri + 1, 0), tadd;
+        for (int j = 0; j < C->n_tri; ++j) {
+            if (tri_adder[j] >= 0) tadd.push_back(tri_adder[j]);
+            taptr[j + 1] = (int)tadd.size();
+        }
+        invert(taptr, tadd, C->n_tri, el_tri_ptr, el_tri);
+    }
     hipStream_t s = c->stream;
     int rc = 0;
 #define UP(dst, v)                                          \
@@ -914,6 +1461,15 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     UP(d_ni_pair, ni_pair); UP(d_ni_node, ni_node); UP(d_ni_orig, ni_orig); UP(d_ni_aptr, ni_aptr); UP(d_ni_add, ni_add);
     UP(d_nj_pair, nj_pair); UP(d_nj_node, nj_node); UP(d_nj_orig, nj_orig); UP(d_nj_aptr, nj_aptr); UP(d_nj_add, nj_add);
     UP(d_tri_pair, tri_pair); UP(d_tri_nodes, tri_nodes); UP(d_tri_ele, tri_ele); UP(d_tri_adder, tri_adder);
+    UP(d_reg_first, reg_first); UP(d_reg, reg); UP(d_pair_reg, pair_reg);
+    UP(d_el_ni_ptr, el_ni_ptr); UP(d_el_ni, el_ni); UP(d_el_nj_ptr, el_nj_ptr); UP(d_el_nj, el_nj);
+    UP(d_el_tri_ptr, el_tri_ptr); UP(d_el_tri, el_tri);
+    {
+        Tile* dt = nullptr;
+        hipError_t e = upload(&dt, tiles, s);
+        C->d_tiles = dt;
+        if (e != hipSuccess) rc = hip_fail(e, "d_tiles");
+    }
 #undef UP
     c->contact = C;
     if (rc) {
@@ -923,31 +1479,42 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     HIPCHK(dalloc(&C->d_bcnt, (size_t)C->htot + 1));
     HIPCHK(dalloc(&C->d_boff, (size_t)C->htot + 1));
     HIPCHK(dalloc(&C->d_blist, (size_t)C->n_ni));
-    HIPCHK(dalloc(&C->d_ni_bucket, (size_t)C->n_ni));
+    HIPCHK(dalloc(&C->d_qbucket, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_ni_map, 3 * (size_t)C->n_ni));
+    HIPCHK(dalloc(&C->d_tile_cnt, (size_t)C->ntile));
+    HIPCHK(dalloc(&C->d_tile_off, (size_t)C->ntile + 1));
+    HIPCHK(dalloc(&C->d_dlist, (size_t)nE));
+    HIPCHK(dalloc(&C->d_ni_live, (size_t)C->n_ni));
+    HIPCHK(dalloc(&C->d_nj_live, (size_t)C->n_nj));
+    HIPCHK(dalloc(&C->d_tri_live, (size_t)C->n_tri));
     HIPCHK(dalloc(&C->d_bbox, 12 * (size_t)C->npairs));
-    HIPCHK(dalloc(&C->d_evn, 2));
+    HIPCHK(dalloc(&C->d_ctl, (size_t)kCtl));
     HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_cnt, (size_t)c->nN + 1));
-    HIPCHK(dalloc(&C->d_off, (size_t)c->nN + 1));
+    HIPCHK(dalloc(&C->d_tpos, (size_t)c->nN + 1));
+    HIPCHK(dalloc(&C->d_touched[0], (size_t)C->tcap));
+    HIPCHK(dalloc(&C->d_touched[1], (size_t)C->tcap));
+    HIPCHK(dalloc(&C->d_toff, (size_t)C->tcap));
+    HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
+    HIPCHK(dalloc(&C->d_cand, (size_t)C->n_tri));
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));
     HIPCHK(hipMemsetAsync(C->d_bcnt, 0, ((size_t)C->htot + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_cnt, 0, ((size_t)c->nN + 1) * sizeof(int), s));
-    HIPCHK(hipMemsetAsync(C->d_evn, 0, 2 * sizeof(unsigned int), s));
+    HIPCHK(hipMemsetAsync(C->d_ctl, 0, kCtl * sizeof(unsigned int), s));
     HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), s));
+    C->force_rebuild = true;
     // velocity before the first step: the state's (IC / uploaded) velocity
     if (!c->h_velo0.empty())
         HIPCHK(hipMemcpyAsync(C->d_velo0, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice, s));
     else
         HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)c->nN * sizeof(double), s));
     C->use_velo0 = c->steps_done == 0 || !c->h_velo0.empty();
-    size_t t1 = 0, t2 = 0;
+    size_t t1 = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, C->d_bcnt, C->d_boff, C->htot + 1, s));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, C->d_cnt, C->d_off, (int)c->nN + 1, s));
-    C->tmp_bytes = std::max(t1, t2);
+    C->tmp_bytes = t1;
     HIPCHK(hipMalloc(&C->d_tmp, std::max<size_t>(C->tmp_bytes, 1)));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
@@ -992,14 +1559,34 @@ int hakai_contact_info(hakai_ctx* c, int32_t* n_pairs, int64_t* info, int32_t ca
     return 0;
 }
 
+int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
+    if (!c || (!stats && cap > 0)) return fail(HAKAI_ERR_ARG, "null");
+    hkc::Contact* C = c->contact;
+    if (!C) return fail(HAKAI_ERR_STATE, "contact_stats before set_contact");
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<unsigned int> ctl(kCtl);
+    std::vector<int> reg(2 * (size_t)C->nreg);
+    HIPCHK(hipMemcpyAsync(ctl.data(), C->d_ctl, kCtl * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+    if (C->nreg)
+        HIPCHK(hipMemcpyAsync(reg.data(), C->d_reg, reg.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    long long live[3] = {0, 0, 0};
+    const int64_t v[7] = {ctl[kEv], ctl[kEvMax], ctl[kNcand], ctl[kTouched + C->tsel], 0, 0, 0};
+    for (int r = 0; r < C->nreg; ++r) live[C->reg_list_h[r]] += reg[2 * r + 1];
+    for (int k = 0; k < cap && k < 7; ++k) stats[k] = k < 4 ? v[k] : live[k == 4 ? 2 : k - 5];
+    return 0;
+}
+
 int hakai_contact_force(hakai_ctx* c, double t, double d_time, double* external_force) {
     if (!c || !external_force) return fail(HAKAI_ERR_ARG, "null");
     if (!c->contact) return fail(HAKAI_ERR_STATE, "contact_force before set_contact");
     if (!c->state_ok) return fail(HAKAI_ERR_STATE, "contact_force before reset/upload_state");
     HIPCHK(hipSetDevice(c->device));
     const bool keep = c->contact->use_velo0;
+    c->contact->force_rebuild = true;  // live lists for this t; and again for the next real step
     int rc = hkc::contact_step(c, t, d_time);
     c->contact->use_velo0 = keep;  // a probe, not a step
+    c->contact->force_rebuild = true;
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(external_force, c->d_fext, 3 * (size_t)c->nN * sizeof(double), hipMemcpyDeviceToHost,
                           c->stream));

@@ -75,7 +75,8 @@ struct hakai_ctx {
     std::vector<double> h_velo0;  // velo as uploaded / set by IC, valid until the first step
     long long steps_done = 0;
     double last_dt = 0.0;
-    int* d_del_step = nullptr;   // [nEp+1] deletion step per element (0 = never), [nEp] dump slot
+    int* d_del_step = nullptr;   // [nEp+2] deletion step per element (0 = never), [nEp] dump slot,
+                                 // [nEp+1] last step in which any element was deleted
     unsigned long long* d_negjac = nullptr;
     bool any_plastic = false;
     bool model_ok = false;
@@ -115,4 +116,5 @@ void contact_destroy(hakai_ctx* c);
 void contact_state_reset(hakai_ctx* c, const double* velo0_host);
 int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
 int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
+int contact_tuning(hakai_ctx* c, const char* key, long long value);  // "contact_*" tuning keys
 }  // namespace hkc

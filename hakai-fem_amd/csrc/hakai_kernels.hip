@@ -292,7 +292,9 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
     if (DO_DELETE) {
         a.flag[e] = kill ? 2 : (in.fl == 2 ? 0 : in.fl);        // 8 lanes, same value
-        int* ds = kill ? a.del_step + e : a.del_step + a.nEp;  // deletion step, or a dump slot
+        // lane 0: the element's deletion step; lanes 1-7 of a killed element: slot nEp+1, "last step
+        // with a deletion" (contact rebuilds its live surface lists from it); others: dump slot nEp
+        int* ds = kill ? a.del_step + (k == 0 ? e : a.nEp + 1) : a.del_step + a.nEp;
         *ds = a.step_i;
     }
 }

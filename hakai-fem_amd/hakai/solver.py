@@ -151,6 +151,14 @@ class Solver:
                     node_triax_stress=nt)
 
     # -- contact ----------------------------------------------------------------------------------
+    def contact_stats(self) -> dict:
+        """Counters of the last contact step (hakai_contact_stats)."""
+        st = np.zeros(8, np.int64)
+        check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 8))
+        keys = ("events", "max_events", "candidate_triangles", "touched_nodes", "live_triangles", "live_nodes_i",
+                "live_nodes_j")
+        return {k: int(v) for k, v in zip(keys, st)}
+
     def contact_info(self):
         """Pairs [(i_instance, j_instance, n_nodes_i, n_triangles, n_nodes_j)], (min, max) element size."""
         n = ctypes.c_int32(0)

@@ -162,7 +162,7 @@ int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
  * 2 = HAKAIoption=self-contact; v2/readInpFile_j.jl:1046-1060), element_instance = instance
  * (1-based, contiguous element blocks) of each element. Builds the exterior surfaces and pairs
  * (v2/HAKAI_j.jl:244-421, :1944-2164) and, once, every face an element deletion can expose
- * (:2167-2245, :766-804). *Contact Pair decks are not supported yet. Then every hakai_step
+ * (:2167-2245, :766-804). Then every hakai_step
  * computes cal_contact_force (:2248-2706) into the external force before the nodal update. */
 int hakai_set_contact(hakai_ctx* ctx, int32_t contact_flag, const int64_t* element_instance);
 /* Same with explicit *Contact Pair surfaces (v2/readInpFile_j.jl:517-564, :1063-1102; pairs
@@ -177,6 +177,11 @@ int hakai_set_contact_params(hakai_ctx* ctx, double myu, double kc_o, double kc_
 /* Pairs (CT entries): info[5p..5p+4] = (i_instance, j_instance, #nodes_i, #triangles, #nodes_j)
  * at setup; sizes = (elementMinSize, elementMaxSize). */
 int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t cap, double* sizes);
+/* Counters of the last contact step (diagnostics; syncs the stream): stats[0..cap) = events,
+ * max events in any step, prefiltered triangles, nodes with contact force, live triangles, live
+ * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
+ * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included). */
+int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);
 

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--preload", type=int, default=30, help="steps before timing (contact starts at ~10)")
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--tri-lanes", type=int, default=0, help="contact_tri_lanes tuning (0: library default)")
     a = ap.parse_args()
     import numpy as np
     from hakai import mesh
@@ -31,6 +32,8 @@ def main():
     sv = Solver(m)
     t2 = time.time()
     pairs, sizes = sv.contact_info()
+    if a.tri_lanes:
+        sv.set_tuning("contact_tri_lanes", a.tri_lanes)
     sv.step(1, a.preload)
     sv.sync()
     sv.profile(True)
@@ -40,6 +43,10 @@ def main():
     el = time.perf_counter() - ts
     k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
                                             (K_CONTACT, "contact"))}
+    cstats = sv.contact_stats()
+    dl = sv.deleted()
+    t_lo, t_hi = 1 + a.preload, a.preload + a.steps
+    del_steps = sorted(set(int(x) for x in dl[:, 0])) if len(dl) else []
     f = sv.contact_force(1 + a.preload + a.steps)
     st = sv.download(element_flag=True)
     n_active = int(st.element_flag.sum())
@@ -49,6 +56,10 @@ def main():
         "value_M_element_updates_per_s": round(n_active * a.steps / el / 1e6, 3),
         "ms_per_step": round(el / a.steps * 1e3, 4),
         "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
+        "deleted_elements": int(len(dl)),
+        "timed_steps_with_deletions": sum(1 for x in del_steps if t_lo <= x <= t_hi),
+        "first_deletion_step": del_steps[0] if del_steps else None,
+        "contact_stats_last_step": cstats,
         "contact_nodes_with_force": int(np.count_nonzero(np.abs(f.reshape(-1, 3)).sum(1))),
         "setup_s": {"mesh": round(t1 - t0, 2), "upload_contact_setup": round(t2 - t1, 2)},
     }
