@@ -219,6 +219,7 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.variant = c->elem_variant;
     ea.pipe_blocks = c->pipe_blocks;
     ea.pipe_map = c->pipe_map;
+    ea.gp_nt = c->gp_nt;
     ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
     ea.nmat = c->nmat;
     return ea;
@@ -720,6 +721,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
         na.cstride = c->fe_layout == 1 ? c->nEp : 1;
         na.early = c->nodal_early;
+        na.fe_nt = c->nodal_fe_nt;
         na.fe = c->d_fe;
         na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
         na.fext = nullptr;
@@ -822,6 +824,16 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "nodal_early")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_early must be 0 or 1");
         c->nodal_early = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "nodal_fe_nt")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_fe_nt must be 0 or 1");
+        c->nodal_fe_nt = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "elem_gp_nt")) {
+        if (value < 0 || value > 3) return fail(HAKAI_ERR_ARG, "elem_gp_nt must be 0..3 (bit 0 loads, bit 1 stores)");
+        c->gp_nt = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_map")) {

@@ -56,7 +56,23 @@ __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int
     in.fb = a.cstride == 1 ? (int)(24 * e + 3 * k) : (int)(3 * k * a.nEp + e);
 }
 
-template <bool ANY_PLASTIC>
+// Gauss-point state accesses: plain, or nontemporal (streamed once per step; keeps the caches for
+// the node data and the element forces the nodal kernel reads next)
+// (NT bit 0: loads, bit 1: stores)
+template <int NT>
+__device__ __forceinline__ double gp_ld(const double* p) {
+    if (NT & 1) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <int NT>
+__device__ __forceinline__ void gp_st(double* p, double v) {
+    if (NT & 2)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <bool ANY_PLASTIC, int NT = 0>
 __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int k, ElemIn& in) {
     const long long gp = 8 * e + k, ld = a.ld, n = in.n;
 #pragma unroll
@@ -66,14 +82,14 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
         in.du[c] = uc - a.u_pre[3 * n + c];
     }
 #pragma unroll
-    for (int c = 0; c < 6; ++c) in.sig[c] = a.stress[c * ld + gp];
+    for (int c = 0; c < 6; ++c) in.sig[c] = gp_ld<NT>(a.stress + c * ld + gp);
 #pragma unroll
-    for (int c = 0; c < 6; ++c) in.eps[c] = a.strain[c * ld + gp];
+    for (int c = 0; c < 6; ++c) in.eps[c] = gp_ld<NT>(a.strain + c * ld + gp);
     in.eqp = 0.0;
     in.ys = 0.0;
     if (ANY_PLASTIC) {
-        in.eqp = a.eqps[gp];
-        in.ys = a.yield[gp];
+        in.eqp = gp_ld<NT>(a.eqps + gp);
+        in.ys = gp_ld<NT>(a.yield + gp);
     }
 }
 
@@ -81,7 +97,7 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
 // is stored):  flag 1 -> full update;  flag 2 (deleted in the previous step) -> Qe and triaxiality
 // become 0 and the flag 0 (the reference skips deleted elements, :1116, and their stress is zero);
 // flag 0 -> state written back unchanged, Qe 0.
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0>
 __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __restrict__ mats, long long e, int k,
                                           double* nd8, const ElemIn& in) {
     const DevMat* M = mats + in.mt;
@@ -282,12 +298,12 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-        a.stress[c * ld + gp] = kill ? 0.0 : (active ? fin[c] : in.sig[c]);
-        a.strain[c * ld + gp] = kill ? 0.0 : (active ? eps[c] : in.eps[c]);
+        gp_st<NT>(a.stress + c * ld + gp, kill ? 0.0 : (active ? fin[c] : in.sig[c]));
+        gp_st<NT>(a.strain + c * ld + gp, kill ? 0.0 : (active ? eps[c] : in.eps[c]));
     }
     if (ANY_PLASTIC) {
-        a.eqps[gp] = active ? eqp : in.eqp;
-        a.yield[gp] = active ? ys : in.ys;
+        gp_st<NT>(a.eqps + gp, active ? eqp : in.eqp);
+        gp_st<NT>(a.yield + gp, active ? ys : in.ys);
     }
     if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
     if (DO_DELETE) {
@@ -316,7 +332,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT = 0>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
@@ -357,12 +373,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     ElemIn cur, nxt;
     load_stage_a(a, elem_of(0), k, cur);
     load_stage_a(a, elem_of(1), k, nxt);
-    load_stage_b<ANY_PLASTIC>(a, elem_of(0), k, cur);
+    load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a(a, elem_of(i + 2), k, nn);
-        load_stage_b<ANY_PLASTIC>(a, elem_of(i + 1), k, nxt);
-        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false>(a, mats, elem_of(i), k, nd8, cur);
+        load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
+        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, cur);
         cur = nxt;
         nxt = nn;
     }
@@ -386,8 +402,31 @@ static void launch_element_w(const ElemArgs& a, bool do_delete, bool store_triax
     }
 }
 
+template <int NT>
+static void launch_pipe_nt(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (do_delete) {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<true, true, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<true, false, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+    } else {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<false, true, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<false, false, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+    }
+}
+
 template <bool ANY_PLASTIC, bool LDS_MATS>
 static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (ANY_PLASTIC && LDS_MATS && a.gp_nt) {
+        switch (a.gp_nt) {
+            case 1: launch_pipe_nt<1>(a, do_delete, store_triax, grid, s); break;
+            case 2: launch_pipe_nt<2>(a, do_delete, store_triax, grid, s); break;
+            default: launch_pipe_nt<3>(a, do_delete, store_triax, grid, s); break;
+        }
+        return;
+    }
     if (do_delete) {
         if (store_triax)
             hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
@@ -507,7 +546,7 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
 // MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer. Compile-time modes keep the
 // kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
 // which serialises the early node loads with the gather again.
-template <int MODE, bool FEXT, bool AOS, bool EARLY>
+template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false>
 __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
     const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
@@ -528,9 +567,9 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const double* p = a.fe + idx[j];
-            f[j][0] = p[0];
-            f[j][1] = p[cs];
-            f[j][2] = p[2 * cs];
+            f[j][0] = gp_ld<FE_NT ? 1 : 0>(p);
+            f[j][1] = gp_ld<FE_NT ? 1 : 0>(p + cs);
+            f[j][2] = gp_ld<FE_NT ? 1 : 0>(p + 2 * cs);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -555,6 +594,8 @@ template <bool FEXT, bool AOS, bool EARLY>
 static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.qbuf)
         hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (a.inc8 && a.fe_nt)
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8)
         hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
     else

@@ -33,6 +33,7 @@ struct ElemArgs {
     int pipe_blocks;        // > 0: persistent pipelined kernel with this many blocks
     int pipe_map;           // batch schedule: 0 contiguous per block, 1 contiguous per XCD, strided
     int nmat;               // materials (staged in LDS when <= kMaxLdsMats)
+    int gp_nt;              // 1: Gauss-point state streamed with nontemporal loads/stores
 };
 
 struct NodalArgs {
@@ -47,6 +48,7 @@ struct NodalArgs {
     const double* fext;    // external force 3nN or null (= 0)
     long long cstride;     // component stride of fe (inc / inc8 hold base offsets)
     int early;             // 1: node operands loaded before the gather (in flight with the indices)
+    int fe_nt;             // 1: element forces gathered with nontemporal loads (read once)
     long long nN;
     double dt;
 };
