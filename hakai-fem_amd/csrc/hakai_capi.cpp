@@ -722,6 +722,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         na.cstride = c->fe_layout == 1 ? c->nEp : 1;
         na.early = c->nodal_early;
         na.fe_nt = c->nodal_fe_nt;
+        na.reverse = c->nodal_reverse;
         na.fe = c->d_fe;
         na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
         na.fext = nullptr;
@@ -824,6 +825,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "nodal_early")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_early must be 0 or 1");
         c->nodal_early = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "nodal_reverse")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_reverse must be 0 or 1");
+        c->nodal_reverse = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "nodal_fe_nt")) {

@@ -95,4 +95,14 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// The same chunks, each walked from its END: a kernel that reads what the previous kernel wrote
+// chunk-wise in ascending order meets the most recently written lines (still in the Infinity
+// Cache) first, instead of evicting them before it gets there.
+__device__ __forceinline__ unsigned xcd_remap_rev(unsigned b, unsigned nwg) {
+    if (nwg < 16) return nwg - 1 - b;
+    const unsigned xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
+    const unsigned len = xcd < r ? q + 1 : q;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (len - 1 - (b >> 3));
+}
+
 }  // namespace hk

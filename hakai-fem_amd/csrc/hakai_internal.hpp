@@ -59,7 +59,8 @@ struct hakai_ctx {
     int pipe_map = 1;            // batch schedule of the persistent kernel (0 per block, 1 per XCD)
     int nodal_early = 1;         // nodal kernel loads its node operands before the gather
     int gp_nt = 3;               // element kernel: Gauss-point state nontemporal (bit 0 loads, bit 1 stores)
-    int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally               // element kernel streams the Gauss-point state nontemporally
+    int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
+    int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end               // element kernel streams the Gauss-point state nontemporally
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
     // bc

@@ -549,7 +549,8 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
 template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false>
 __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
-    const long long n = (long long)xcd_remap(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    const unsigned lb = a.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
+    const long long n = (long long)lb * kBlock + threadIdx.x;
     if (n >= a.nN) return;
     NodeIn in;
     if (EARLY) nodal_load<FEXT>(a, n, in);

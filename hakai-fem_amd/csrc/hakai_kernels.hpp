@@ -49,6 +49,7 @@ struct NodalArgs {
     long long cstride;     // component stride of fe (inc / inc8 hold base offsets)
     int early;             // 1: node operands loaded before the gather (in flight with the indices)
     int fe_nt;             // 1: element forces gathered with nontemporal loads (read once)
+    int reverse;           // 1: each XCD walks its node chunk from the end (xcd_remap_rev)
     long long nN;
     double dt;
 };
