@@ -60,7 +60,7 @@ struct hakai_ctx {
     int nodal_early = 1;         // nodal kernel loads its node operands before the gather
     int gp_nt = 3;               // element kernel: Gauss-point state nontemporal (bit 0 loads, bit 1 stores)
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
-    int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end               // element kernel streams the Gauss-point state nontemporally
+    int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
     // bc
