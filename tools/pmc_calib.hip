@@ -50,6 +50,19 @@ __global__ void calib_write_d2(double2* __restrict__ out, size_t n) {
         out[i] = make_double2((double)i, 1.0);
 }
 
+// Nontemporal forms (the element kernel streams its Gauss-point state with these)
+__global__ void calib_read_nt(const double* __restrict__ in, size_t n, double* __restrict__ sink) {
+    double acc = 0.0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        acc += __builtin_nontemporal_load(in + i);
+    if (acc == -1.0) sink[0] = acc;
+}
+
+__global__ void calib_write_nt(double* __restrict__ out, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store((double)i, out + i);
+}
+
 // The element kernel's force store: lane writes 3 doubles at a 24-B stride ([8 nE][3] AoS).
 __global__ void calib_write_aos3(double* __restrict__ out, size_t n3) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n3; i += (size_t)gridDim.x * blockDim.x) {
@@ -83,6 +96,8 @@ int main() {
         hipLaunchKernelGGL(calib_write<int>, g, b, 0, 0, (int*)a, kBytes / 4);
         hipLaunchKernelGGL(calib_write_d2, g, b, 0, 0, (double2*)a, kBytes / 16);
         hipLaunchKernelGGL(calib_write_aos3, g, b, 0, 0, (double*)a, kBytes / 24);
+        hipLaunchKernelGGL(calib_read_nt, g, b, 0, 0, (const double*)a, kBytes / 8, sink);
+        hipLaunchKernelGGL(calib_write_nt, g, b, 0, 0, (double*)a, kBytes / 8);
         CK(hipGetLastError());
     }
     CK(hipDeviceSynchronize());

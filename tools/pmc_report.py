@@ -25,6 +25,8 @@ CALIB = {  # kernel-name prefix -> (counter, bytes per dispatch, pattern)
     "void calib_write<int>": ("WRITE_SIZE", 1 << 30, "write 4B/lane"),
     "calib_write_d2": ("WRITE_SIZE", 1 << 30, "write 16B/lane"),
     "calib_write_aos3": ("WRITE_SIZE", ((1 << 30) // 24) * 24, "write 3x8B/lane stride 24B"),
+    "calib_read_nt": ("FETCH_SIZE", 1 << 30, "read 8B/lane nontemporal"),
+    "calib_write_nt": ("WRITE_SIZE", 1 << 30, "write 8B/lane nontemporal"),
 }
 
 
@@ -101,6 +103,8 @@ def main():
         "hbm_write_bytes_per_launch": raw_w / fw if raw_w is not None and fw else None,
         "hbm_bytes_per_launch": traffic,
         "correction": "FETCH_SIZE / f(read 8B/lane) + WRITE_SIZE / f(write 8B/lane), factors from tools/pmc_calib.hip",
+        "hbm_bytes_per_launch_nt_factors": (raw_f / fac["read 8B/lane nontemporal"] + raw_w / fac["write 8B/lane nontemporal"])
+        if fac.get("read 8B/lane nontemporal") and fac.get("write 8B/lane nontemporal") and raw_f and raw_w else None,
         "algorithmic_bytes_per_launch": a.alg_bytes,
         "traffic_over_algorithmic": traffic / a.alg_bytes if traffic and a.alg_bytes else None,
         "kernel_trace_avg_ms_timed_region": avg_ms,
