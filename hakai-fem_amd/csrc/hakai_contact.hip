@@ -77,6 +77,7 @@ struct Contact {
     int *d_el_nj_ptr = nullptr, *d_el_nj = nullptr, *d_dlist = nullptr;
     int *d_ni_live = nullptr, *d_nj_live = nullptr, *d_tri_live = nullptr;
     bool force_rebuild = true;
+    bool always_rebuild = false;    // tuning/testing: full rebuild every step (no incremental update)
     long long last_t = -1;
     // hash grid over i-nodes
     int htot = 0;
@@ -1056,7 +1057,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     in.conn = c->d_conn;
     in.mass = c->d_mass;
     in.t = (int)t;
-    if ((long long)in.t != C->last_t + 1) C->force_rebuild = true;
+    if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const int tsel = C->tsel = 1 - C->tsel;
     hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl,
                        C->force_rebuild ? 1 : 0, c->d_del_step + c->nEp + 1, in.t, C->d_touched[1 - tsel], tsel,
@@ -1135,6 +1136,11 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     if (!std::strcmp(key, "contact_tri_lanes")) {
         if (value != 1 && value != 32) return fail(HAKAI_ERR_ARG, "contact_tri_lanes must be 1 or 32");
         C->tri_lanes = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "contact_full_rebuild")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_full_rebuild must be 0 or 1");
+        C->always_rebuild = value != 0;
         return 0;
     }
     if (!std::strcmp(key, "contact_event_cap")) {

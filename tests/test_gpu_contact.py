@@ -95,6 +95,54 @@ def test_contact_with_deletion_surface_update():
     assert rel_err(g.disp, o.s["disp"]) < 1e-6
 
 
+def test_incremental_surface_lists_match_full_rebuild_and_oracle():
+    """The live surface lists updated on the device after each deletion (k_ct_find_del/k_ct_append)
+    give the same run, bit for bit, as a full rebuild every step, and -- after a probe at the next
+    step -- the same list lengths as the oracle's c_triangles / c_nodes_i / c_nodes_j, which grow like
+    the reference's (v2/HAKAI_j.jl:766-804)."""
+    m = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    assert len(o.deletions) >= 4
+    runs = []
+    for full in (0, 1):
+        with Solver(m) as sv:
+            sv.set_tuning("contact_full_rebuild", full)
+            sv.step(1, m.n_steps)
+            g = sv.download()
+            inc = sv.contact_stats()
+            sv.contact_force(m.n_steps + 1)
+            probe = sv.contact_stats()
+            runs.append((g, inc, probe, [tuple(x) for x in sv.deleted()]))
+    (g0, inc0, p0, d0), (g1, inc1, p1, d1) = runs
+    assert d0 == d1 == sorted(o.deletions)
+    assert np.array_equal(g0.disp, g1.disp) and np.array_equal(g0.integ_stress, g1.integ_stress)
+    for k in ("live_triangles", "live_nodes_i", "live_nodes_j"):
+        assert inc0[k] == inc1[k], k
+    cp = o.contact_pairs()
+    assert p0["live_triangles"] == sum(p["n_triangles"] for p in cp)
+    assert p0["live_nodes_i"] == sum(p["n_nodes_i"] for p in cp)
+    assert p0["live_nodes_j"] == sum(p["n_nodes_j"] for p in cp)
+
+
+def test_event_cap_overflow_is_reported():
+    """A contact step with more events than the buffer holds fails loudly (no silent truncation);
+    raising the cap through hakai_set_tuning recovers."""
+    from hakai._abi import HakaiError
+    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.03, seed=4, n_steps=60)
+    with Solver(m) as sv:
+        sv.set_tuning("contact_event_cap", 1)
+        with pytest.raises(HakaiError):
+            sv.step(1, m.n_steps)
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    with Solver(m) as sv:
+        sv.set_tuning("contact_event_cap", 1 << 12)
+        sv.step(1, m.n_steps)
+        g = sv.download()
+    assert rel_err(g.disp, o.s["disp"]) < 1e-9
+
+
 @pytest.mark.parametrize("surfaces", [False, True])
 def test_driver_runs_contact_deck(tmp_path, surfaces):
     """HAKAI(fname) on a *Contact (all exterior) or *Contact Pair deck written from code: contact on
