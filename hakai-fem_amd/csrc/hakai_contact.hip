@@ -87,6 +87,7 @@ struct Contact {
     // events and per-node gather over the touched nodes
     long long cap = 0;
     unsigned int* d_ctl = nullptr;  // kCtl control words (events, max events, dirty, touched counts)
+    unsigned int* d_evs = nullptr;  // [kEvShards][kShardStride] event counters (one per shard)
     int* d_ev_nodes = nullptr;      // [cap][4]
     double* d_ev_f = nullptr;       // [cap][3]
     int* d_cnt = nullptr;           // [nN] terms per node (zero between steps)
@@ -96,8 +97,8 @@ struct Contact {
     long long tcap = 0;
     int* d_toff = nullptr;          // [tcap] start of each touched node's term range
     int* d_tcnt = nullptr;          // [tcap] its length
-    int* d_cand = nullptr;          // [n_tri] triangles passing the prefilter
-    int tri_lanes = 32;             // lanes per candidate triangle (32: one per cell; 1: a loop over cells)
+    void* d_cand = nullptr;         // [cand_cap] TriRec of the triangles passing the prefilter
+    long long cand_cap = 0;
     double* d_terms = nullptr;      // [4 cap][3]
     void* d_tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -176,15 +177,21 @@ __device__ __forceinline__ Range pair_range(const unsigned long long* bb) {
 // incremental update (an element was deleted in the previous step), deleted elements found, and
 // the number of nodes with contact force in each of the two ping-pong "touched" lists.
 enum { kEv = 0, kEvMax = 1, kDirty = 2, kDel = 3, kNdel = 4, kTouched = 5 /* [5], [6] */, kNcand = 7, kTerms = 8,
-       kCtl = 16 };
+       kNcandMax = 9, kEvShardMax = 10, kCtl = 16 };
+// Events are appended into kEvShards shards, each with its own counter on its own 128-B line: with
+// one counter, every wave that found an event waited on the same memory-side atomic (measured:
+// 0.13 ms of a 0.30 ms contact step on C4).
+constexpr int kEvShards = 64;
+constexpr int kShardStride = 32;  // unsigned ints between shard counters
 
 // Step prologue: pair boxes to (+inf, -inf), event counter to 0, full rebuild if the host forces
 // it, incremental update if an element was deleted in the previous step (del_any == t-1), and
 // the contact forces of the previous step's touched nodes back to 0 (external_force is otherwise
 // never rewritten).
-__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, int force, const int* del_any,
-                           int t, const int* touched_prev, int tsel, double* fext) {
+__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs, int force,
+                           const int* del_any, int t, const int* touched_prev, int tsel, double* fext) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kEvShards) evs[i * kShardStride] = 0;
     if (i < 12 * npairs) bbox[i] = ((i % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
     if (i == 0) {
         ctl[kEv] = 0;
@@ -526,24 +533,89 @@ __device__ __forceinline__ unsigned wave_append(unsigned int* ctr, bool pred) {
     return base + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
 }
 
+// Per-candidate triangle record, written by the prefilter: everything of the loop body at
+// :2371-2698 that does not depend on the contact point (same expressions as the reference, so the
+// same bits), so the per-cell threads start from one load instead of a chain of dependent ones.
+struct TriRec {
+    double q0[3], c[3], Rmax, n[3], vdet, im[9], kk;
+    long long mj[3];
+    int j0, j1, j2, eleid, pr, pad;
+};
+
+__device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const Range& r, const PairParam& pp,
+                                         const int* tri_nodes, const int* tri_ele, const double q0[3],
+                                         const double q1[3], const double q2[3], TriRec& T) {
+#pragma clang fp contract(off)
+    const double cx = (q0[0] + q1[0] + q2[0]) / 3.0, cy = (q0[1] + q1[1] + q2[1]) / 3.0,
+                 cz = (q0[2] + q1[2] + q2[2]) / 3.0;
+    const double R0 = my3norm(q0[0] - cx, q0[1] - cy, q0[2] - cz);
+    const double R1 = my3norm(q1[0] - cx, q1[1] - cy, q1[2] - cz);
+    const double R2 = my3norm(q2[0] - cx, q2[1] - cy, q2[2] - cz);
+    const double v1x = q1[0] - q0[0], v1y = q1[1] - q0[1], v1z = q1[2] - q0[2];
+    const double v2x = q2[0] - q0[0], v2y = q2[1] - q0[1], v2z = q2[2] - q0[2];
+    const double L1 = my3norm(v1x, v1y, v1z), L2 = my3norm(v2x, v2y, v2z);
+    const double Lmax = fmax(L1, L2);
+    double nx = v1y * v2z - v1z * v2y, ny = v1z * v2x - v1x * v2z, nz = v1x * v2y - v1y * v2x;  // my3crossNNz
+    const double mag_n = sqrt(nx * nx + ny * ny + nz * nz);
+    nx = nx / mag_n;
+    ny = ny / mag_n;
+    nz = nz / mag_n;
+    const double d12 = v1x * v2x + v1y * v2y + v1z * v2z;
+    const double S = 0.5 * sqrt(L1 * L1 * L2 * L2 - d12 * d12);
+    const double A11 = v1x, A21 = v1y, A31 = v1z, A12 = v2x, A22 = v2y, A32 = v2z, A13 = -nx, A23 = -ny, A33 = -nz;
+    // my3SolveAb (:3342-3373): determinant and adjugate do not depend on the point
+    T.vdet = (A11 * A22 * A33 + A12 * A23 * A31 + A13 * A21 * A32 - A11 * A23 * A32 - A12 * A21 * A33 -
+              A13 * A22 * A31);
+    T.im[0] = A22 * A33 - A23 * A32;  // im11
+    T.im[1] = A13 * A32 - A12 * A33;  // im12
+    T.im[2] = A12 * A23 - A13 * A22;  // im13
+    T.im[3] = A23 * A31 - A21 * A33;  // im21
+    T.im[4] = A11 * A33 - A13 * A31;  // im22
+    T.im[5] = A13 * A21 - A11 * A23;  // im23
+    T.im[6] = A21 * A32 - A22 * A31;  // im31
+    T.im[7] = A12 * A31 - A11 * A32;  // im32
+    T.im[8] = A11 * A22 - A12 * A21;  // im33
+    T.kk = pp.young * S / Lmax * pp.kc;  // :2575
+    for (int d = 0; d < 3; ++d) {
+        T.q0[d] = q0[d];
+        T.mj[d] = (long long)ceil((q0[d] - r.amn[d]) / pp.ddiv);
+    }
+    T.c[0] = cx;
+    T.c[1] = cy;
+    T.c[2] = cz;
+    T.Rmax = fmax(fmax(R0, R1), R2);
+    T.n[0] = nx;
+    T.n[1] = ny;
+    T.n[2] = nz;
+    T.j0 = tri_nodes[3 * j];
+    T.j1 = tri_nodes[3 * j + 1];
+    T.j2 = tri_nodes[3 * j + 2];
+    T.eleid = tri_ele[j];
+    T.pr = pr;
+    T.pad = 0;
+}
+
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
-// side of the range box along any axis -> candidate list
+// side of the range box along any axis -> candidate record
 __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
                                                       const int* tri_pair, const int* tri_nodes, const int* tri_ele,
-                                                      const unsigned long long* bbox, unsigned int* ctl, int* cand) {
+                                                      const PairParam* par, const unsigned long long* bbox,
+                                                      unsigned int* ctl, TriRec* cand, long long cand_cap) {
     const int n = *tri_cnt;
     for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {  // wave-uniform trip count
         const int q = q0 + (int)threadIdx.x;
         bool keep = false;
-        int j = 0;
+        int j = 0, pr = 0;
+        double p0[3], p1[3], p2[3];
+        Range r;
         if (q < n) {
             j = tri_live[q];
             keep = s.flag[tri_ele[j]] == 1;
             if (keep) {
-                const Range r = pair_range(bbox + 12 * tri_pair[j]);
+                pr = tri_pair[j];
+                r = pair_range(bbox + 12 * pr);
                 keep = !r.empty;
                 if (keep) {
-                    double p0[3], p1[3], p2[3];
                     pos(s, tri_nodes[3 * j], p0);
                     pos(s, tri_nodes[3 * j + 1], p1);
                     pos(s, tri_nodes[3 * j + 2], p2);
@@ -555,7 +627,11 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
             }
         }
         const unsigned slot = wave_append(&ctl[kNcand], keep);
-        if (keep) cand[slot] = j;
+        if (keep && (long long)slot < cand_cap) {
+            TriRec T;
+            tri_geom(s, j, pr, r, par[pr], tri_nodes, tri_ele, p0, p1, p2, T);
+            cand[slot] = T;
+        }
     }
 }
 
@@ -581,87 +657,39 @@ __device__ __forceinline__ void ev_write(int* ev_nodes, double* ev_f, long long 
     ef[2] = fz;
 }
 
-// one (candidate triangle, neighbour cell) pair: the body of the @floop at :2371-2698 for the
-// i-nodes of one of the 27 cells around the triangle's first node. The lanes of a triangle each
-// compute its geometry (same expressions, same bits; the loads are shared); a cell whose hash
-// bucket an earlier cell of the same triangle already maps to is skipped, so every bucket is
-// visited once.
-__device__ __forceinline__ void tri_cell(const StepIn& s, int j, int cell, const int* tri_pair, const int* tri_nodes,
-                                         const int* tri_ele, const PairParam* par, const unsigned long long* bbox,
-                                         const int* boff, const int* blist, const int* ni_node,
-                                         const long long* ni_map, double d_lim, double myu, unsigned int* evn,
-                                         long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
+// one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
+// i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
+__device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
+                                         int b, const PairParam* par, const int* boff, const int* blist,
+                                         const int* ni_node, const long long* ni_map, double d_lim, double myu,
+                                         unsigned int* evn, long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
 #pragma clang fp contract(off)
-    const int eleid = tri_ele[j];
-    const int pr = tri_pair[j];
-    const Range r = pair_range(bbox + 12 * pr);
-    const PairParam pp = par[pr];
-    long long mj[3];
-    {
-        double q0[3];
-        pos(s, tri_nodes[3 * j], q0);
-        for (int d = 0; d < 3; ++d) mj[d] = (long long)ceil((q0[d] - r.amn[d]) / pp.ddiv);
-    }
-    const unsigned hmask = (unsigned)(pp.hash_size - 1);
-    const int dz = cell / 9 - 1, dy = (cell / 3) % 3 - 1, dx = cell % 3 - 1;
-    const unsigned hb = hash3(mj[0] + dx, mj[1] + dy, mj[2] + dz) & hmask;
-    for (int c2 = 0; c2 < cell; ++c2)
-        if ((hash3(mj[0] + (c2 % 3 - 1), mj[1] + ((c2 / 3) % 3 - 1), mj[2] + (c2 / 9 - 1)) & hmask) == hb) return;
-    const int b = pp.hash_off + (int)hb;
+    const int pr = rec->pr;
     const int sl0 = boff[b], sl1 = boff[b + 1];
-    if (sl0 == sl1) return;
-    const int j0 = tri_nodes[3 * j], j1 = tri_nodes[3 * j + 1], j2 = tri_nodes[3 * j + 2];
-    double q0[3], q1[3], q2[3];
-    pos(s, j0, q0);
-    pos(s, j1, q1);
-    pos(s, j2, q2);
-    const double cx = (q0[0] + q1[0] + q2[0]) / 3.0, cy = (q0[1] + q1[1] + q2[1]) / 3.0,
-                 cz = (q0[2] + q1[2] + q2[2]) / 3.0;
-    const double R0 = my3norm(q0[0] - cx, q0[1] - cy, q0[2] - cz);
-    const double R1 = my3norm(q1[0] - cx, q1[1] - cy, q1[2] - cz);
-    const double R2 = my3norm(q2[0] - cx, q2[1] - cy, q2[2] - cz);
-    const double Rmax = fmax(fmax(R0, R1), R2);
-    const double v1x = q1[0] - q0[0], v1y = q1[1] - q0[1], v1z = q1[2] - q0[2];
-    const double v2x = q2[0] - q0[0], v2y = q2[1] - q0[1], v2z = q2[2] - q0[2];
-    const double L1 = my3norm(v1x, v1y, v1z), L2 = my3norm(v2x, v2y, v2z);
-    const double Lmax = fmax(L1, L2);
-    double nx = v1y * v2z - v1z * v2y, ny = v1z * v2x - v1x * v2z, nz = v1x * v2y - v1y * v2x;  // my3crossNNz
-    const double mag_n = sqrt(nx * nx + ny * ny + nz * nz);
-    nx = nx / mag_n;
-    ny = ny / mag_n;
-    nz = nz / mag_n;
-    const double d12 = v1x * v2x + v1y * v2y + v1z * v2z;
-    const double S = 0.5 * sqrt(L1 * L1 * L2 * L2 - d12 * d12);
-    const double A11 = v1x, A21 = v1y, A31 = v1z, A12 = v2x, A22 = v2y, A32 = v2z, A13 = -nx, A23 = -ny, A33 = -nz;
-    // my3SolveAb (:3342-3373): determinant and adjugate do not depend on the point
-    const double vdet = (A11 * A22 * A33 + A12 * A23 * A31 + A13 * A21 * A32 - A11 * A23 * A32 - A12 * A21 * A33 -
-                         A13 * A22 * A31);
-    const double im11 = A22 * A33 - A23 * A32, im21 = A23 * A31 - A21 * A33, im31 = A21 * A32 - A22 * A31;
-    const double im12 = A13 * A32 - A12 * A33, im22 = A11 * A33 - A13 * A31, im32 = A12 * A31 - A11 * A32;
-    const double im13 = A12 * A23 - A13 * A22, im23 = A13 * A21 - A11 * A23, im33 = A11 * A22 - A12 * A21;
-    const double kk = pp.young * S / Lmax * pp.kc;  // :2575
-    int el[8];
-    if (pp.self)
-        for (int a = 0; a < 8; ++a) el[a] = s.conn[8 * (long long)eleid + a];
     for (int sl = sl0; sl < sl1; ++sl) {
         const int k = blist[sl];
         const long long* mk = ni_map + 3 * (long long)k;
         if (llabs(mj[0] - mk[0]) > 1 || llabs(mj[1] - mk[1]) > 1 || llabs(mj[2] - mk[2]) > 1) continue;
         const int i = ni_node[k];
+        const PairParam pp = par[pr];
         if (pp.self) {
             bool own = false;
-            for (int a = 0; a < 8; ++a) own |= (i == el[a]);
+            for (int a = 0; a < 8; ++a) own |= (i == s.conn[8 * (long long)rec->eleid + a]);
             if (own) continue;
         }
         double p[3];
         pos(s, i, p);
-        const double dpc = my3norm(p[0] - cx, p[1] - cy, p[2] - cz);
-        if (dpc >= Rmax) continue;
-        const double bx = p[0] - q0[0], by = p[1] - q0[1], bz = p[2] - q0[2];
-        const double x1 = (im11 * bx + im12 * by + im13 * bz) / vdet;
-        const double x2 = (im21 * bx + im22 * by + im23 * bz) / vdet;
-        const double d = (im31 * bx + im32 * by + im33 * bz) / vdet;
+        const double dpc = my3norm(p[0] - rec->c[0], p[1] - rec->c[1], p[2] - rec->c[2]);
+        if (dpc >= rec->Rmax) continue;
+        const double bx = p[0] - rec->q0[0], by = p[1] - rec->q0[1], bz = p[2] - rec->q0[2];
+        const double* im = rec->im;
+        const double vdet = rec->vdet;
+        const double x1 = (im[0] * bx + im[1] * by + im[2] * bz) / vdet;
+        const double x2 = (im[3] * bx + im[4] * by + im[5] * bz) / vdet;
+        const double d = (im[6] * bx + im[7] * by + im[8] * bz) / vdet;
         if (!(0.0 <= x1 && 0.0 <= x2 && x1 + x2 <= 1.0 && d > 0.0 && d <= d_lim)) continue;
+        const int j0 = rec->j0, j1 = rec->j1, j2 = rec->j2;
+        const double nx = rec->n[0], ny = rec->n[1], nz = rec->n[2], kk = rec->kk;
         // velo = d_disp / d_time of the previous step (:628); the IC before step 1
         double vi[3], vj[3];
         for (int c = 0; c < 3; ++c) {
@@ -705,93 +733,124 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, int j, int cell, const
                     eb.f[u][2] = fz;
                 }
             ++eb.n;
-        } else {
-            const unsigned e = atomicAdd(&evn[0], 1u);
+        } else {  // evn: this wave's shard counter, cap: the shard's capacity, ev_*: the shard's slots
+            const unsigned e = atomicAdd(evn, 1u);
             if ((long long)e < cap) ev_write(ev_nodes, ev_f, e, i, j0, j1, j2, fx, fy, fz);
         }
     }
 }
 
-__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, const unsigned int* ncand, const int* cand,
-                                                const int* tri_pair, const int* tri_nodes, const int* tri_ele,
-                                                const PairParam* par, const unsigned long long* bbox, const int* boff,
-                                                const int* blist, const int* ni_node, const long long* ni_map,
-                                                double d_lim, double myu, unsigned int* evn, long long cap,
-                                                int* ev_nodes, double* ev_f) {
-    // 32 lanes per triangle (27 cells used): the triangle's data are wave-uniform loads, fetched once
-    const long long n = 32LL * (long long)*ncand;
+// 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
+__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const TriRec* cand, long long cand_cap,
+                                                const PairParam* par, const int* boff, const int* blist,
+                                                const int* ni_node, const long long* ni_map, double d_lim,
+                                                double myu, unsigned int* evs, long long shard_cap, int* ev_nodes,
+                                                double* ev_f) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&ctl[kNcandMax], ctl[kNcand]);
+    const long long n = 32LL * std::min<long long>((long long)ctl[kNcand], cand_cap);
     const int lane = (int)(threadIdx.x & 63);
+    const int shard = (int)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kEvShards);
+    unsigned int* evn = evs + shard * kShardStride;
+    int* sh_nodes = ev_nodes + 4 * (long long)shard * shard_cap;
+    double* sh_f = ev_f + 3 * (long long)shard * shard_cap;
     for (long long q0 = blockIdx.x * (long long)blockDim.x; q0 < n; q0 += (long long)gridDim.x * blockDim.x) {
         const long long q = q0 + threadIdx.x;  // wave-uniform trip count (the append below is wave-wide)
         EvBuf eb;
         eb.n = 0;
         eb.j0 = eb.j1 = eb.j2 = 0;
-        if (q < n && (q & 31) < 27)
-            tri_cell(s, cand[q >> 5], (int)(q & 31), tri_pair, tri_nodes, tri_ele, par, bbox, boff, blist, ni_node,
-                     ni_map, d_lim, myu, evn, cap, ev_nodes, ev_f, eb);
+        // lane c of a triangle's 32 takes cell c (dz, dy, dx in the reference's loop order); a cell
+        // whose bucket a lower cell of the same triangle maps to is skipped, so every bucket is
+        // visited once. Buckets are compared across lanes (readlane), one hash per lane.
+        const int cell = (int)(q & 31);
+        const bool valid = q < n && cell < 27;
+        const TriRec* rec = cand + (valid ? (q >> 5) : 0);
+        long long mj[3] = {0, 0, 0};
+        unsigned hb = 0x80000000u | (unsigned)lane;  // never equal to a real bucket (< 2^31)
+        int hoff = 0;
+        if (valid) {
+            const int pr = rec->pr;
+            hoff = par[pr].hash_off;
+            mj[0] = rec->mj[0];
+            mj[1] = rec->mj[1];
+            mj[2] = rec->mj[2];
+            hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
+                 (unsigned)(par[pr].hash_size - 1);
+        }
+        bool dup = false;
+        const int half = lane & 32;
+#pragma unroll
+        for (int c2 = 0; c2 < 26; ++c2) {
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)hb, c2);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)hb, 32 + c2);
+            dup |= c2 < cell && (half ? hi : lo) == hb;
+        }
+        if (valid && !dup)
+            tri_cell(s, rec, mj, hoff + (int)hb, par, boff, blist, ni_node, ni_map, d_lim, myu, evn, shard_cap,
+                     sh_nodes, sh_f, eb);
         const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
         int x = c;  // wave inclusive scan of the buffered counts
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(x, o);
             if (lane >= o) x += y;
         }
+        if (__builtin_amdgcn_readlane(x, 63) == 0) continue;  // wave-uniform: no events this iteration
         unsigned base = 0;
-        if (lane == 63 && x > 0) base = atomicAdd(&evn[0], (unsigned)x);
+        if (lane == 63) base = atomicAdd(evn, (unsigned)x);
         base = __shfl(base, 63) + (unsigned)(x - c);
 #pragma unroll
         for (int u = 0; u < kEvLocal; ++u)
-            if (u < c && (long long)(base + u) < cap)
-                ev_write(ev_nodes, ev_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+            if (u < c && (long long)(base + u) < shard_cap)
+                ev_write(sh_nodes, sh_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
     }
 }
 
-// one thread per candidate triangle, the 27 cells in a loop (the reference's loop structure)
-__global__ __launch_bounds__(128) void k_ct_tri1(StepIn s, const unsigned int* ncand, const int* cand,
-                                                 const int* tri_pair, const int* tri_nodes, const int* tri_ele,
-                                                 const PairParam* par, const unsigned long long* bbox,
-                                                 const int* boff, const int* blist, const int* ni_node,
-                                                 const long long* ni_map, double d_lim, double myu, unsigned int* evn,
-                                                 long long cap, int* ev_nodes, double* ev_f) {
-    const int n = (int)*ncand;
-    const int lane = (int)(threadIdx.x & 63);
-    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {
-        const int q = q0 + (int)threadIdx.x;
-        EvBuf eb;
-        eb.n = 0;
-        eb.j0 = eb.j1 = eb.j2 = 0;
-        if (q < n)
-            for (int cell = 0; cell < 27; ++cell)
-                tri_cell(s, cand[q], cell, tri_pair, tri_nodes, tri_ele, par, bbox, boff, blist, ni_node, ni_map,
-                         d_lim, myu, evn, cap, ev_nodes, ev_f, eb);
-        const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
-        int x = c;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
+// Shard prefix of the event counts (clamped to the shard capacity) in LDS; thread 0 of block 0
+// also publishes the totals for the overflow check and the stats.
+__device__ __forceinline__ long long shard_prefix(unsigned int* ctl, const unsigned int* evs, long long shard_cap,
+                                                  unsigned* s_pre) {
+    if (threadIdx.x == 0) {
+        unsigned run = 0, raw = 0, mx = 0;
+        for (int q = 0; q < kEvShards; ++q) {
+            const unsigned v = evs[q * kShardStride];
+            s_pre[q] = run;
+            run += (long long)v < shard_cap ? v : (unsigned)shard_cap;
+            raw += v;
+            mx = v > mx ? v : mx;
         }
-        unsigned base = 0;
-        if (lane == 63 && x > 0) base = atomicAdd(&evn[0], (unsigned)x);
-        base = __shfl(base, 63) + (unsigned)(x - c);
-#pragma unroll
-        for (int u = 0; u < kEvLocal; ++u)
-            if (u < c && (long long)(base + u) < cap)
-                ev_write(ev_nodes, ev_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+        s_pre[kEvShards] = run;
+        if (blockIdx.x == 0) {
+            ctl[kEv] = raw;
+            atomicMax(&ctl[kEvMax], raw);
+            atomicMax(&ctl[kEvShardMax], mx);
+        }
     }
+    __syncthreads();
+    return s_pre[kEvShards];
+}
+
+// event index (in shard-prefix order) -> slot of the shard buffers
+__device__ __forceinline__ long long ev_slot(const unsigned* s_pre, long long shard_cap, long long ev) {
+    int lo = 0, hi = kEvShards;  // s_pre[lo] <= ev < s_pre[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((long long)s_pre[mid] <= ev) lo = mid; else hi = mid;
+    }
+    return (long long)lo * shard_cap + (ev - s_pre[lo]);
 }
 
 // Per-node gather of the event terms over the nodes that received one ("touched", a compact list
 // instead of a pass over all nN nodes): count -> per-node term ranges by a wave-aggregated bump
 // allocator (ranges are disjoint; their order is irrelevant) -> scatter -> sum.
-__global__ void k_ct_count(unsigned int* ctl, long long cap, const int* ev_nodes, int* cnt, int* touched, int* tpos,
-                           int tsel) {
-    const long long n = 4 * std::min<long long>((long long)ctl[kEv], cap);
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&ctl[kEvMax], ctl[kEv]);
+__global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
+                           int* cnt, int* touched, int* tpos, int tsel) {
+    __shared__ unsigned s_pre[kEvShards + 1];
+    const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
         bool first = false;
         if (e < n) {
-            node = ev_nodes[e];
+            node = ev_nodes[4 * ev_slot(s_pre, shard_cap, e >> 2) + (e & 3)];
             first = atomicAdd(&cnt[node], 1) == 0;
         }
         const unsigned q = wave_append(&ctl[kTouched + tsel], first);
@@ -823,15 +882,16 @@ __global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, cons
     }
 }
 
-__global__ void k_ct_scatter(const unsigned int* ctl, long long cap, const int* ev_nodes, const double* ev_f,
-                             const int* toff, const int* tpos, int* cnt, double* terms) {
+__global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
+                             const double* ev_f, const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
-    const long long n = std::min<long long>((long long)ctl[kEv], cap);
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < 4 * n;
+    __shared__ unsigned s_pre[kEvShards + 1];
+    const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const int node = ev_nodes[e];
-        const long long ev = e >> 2;
+        const long long ev = ev_slot(s_pre, shard_cap, e >> 2);
         const int role = (int)(e & 3);
+        const int node = ev_nodes[4 * ev + role];
         const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
         const double* f = ev_f + 3 * ev;
         double* o = terms + 3 * (long long)slot;
@@ -1023,8 +1083,8 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_el_nj); dfree(C->d_dlist);
     dfree(C->d_ni_live); dfree(C->d_nj_live); dfree(C->d_tri_live);
     dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_ni_map);
-    dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
-    dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); dfree(C->d_cand);
+    dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
+    dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0);
     if (C->d_tmp) (void)hipFree(C->d_tmp);
     delete C;
@@ -1059,7 +1119,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     in.t = (int)t;
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const int tsel = C->tsel = 1 - C->tsel;
-    hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl,
+    hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
                        C->force_rebuild ? 1 : 0, c->d_del_step + c->nEp + 1, in.t, C->d_touched[1 - tsel], tsel,
                        c->d_fext);
     C->force_rebuild = false;
@@ -1106,23 +1166,19 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     if (C->n_tri > 0) {
         hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, 2048))),
                            dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
-                           C->d_tri_nodes, C->d_tri_ele, C->d_bbox, C->d_ctl, C->d_cand);
-        if (C->tri_lanes == 32)
-            hipLaunchKernelGGL(k_ct_tri, dim3(4096), dim3(128), 0, s, in, C->d_ctl + kNcand, C->d_cand, C->d_tri_pair,
-                               C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_boff, C->d_blist, C->d_ni_node,
-                               C->d_ni_map, C->d_lim, C->myu, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f);
-        else
-            hipLaunchKernelGGL(k_ct_tri1, dim3(1024), dim3(128), 0, s, in, C->d_ctl + kNcand, C->d_cand,
-                               C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_boff, C->d_blist,
-                               C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f);
+                           C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ctl, (TriRec*)C->d_cand,
+                           C->cand_cap);
+        hipLaunchKernelGGL(k_ct_tri, dim3(4096), dim3(128), 0, s, in, C->d_ctl, (const TriRec*)C->d_cand, C->cand_cap,
+                           C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
+                           C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
     }
     const unsigned ge = (unsigned)std::min<long long>((4 * C->cap + kB - 1) / kB, 1024);
-    hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->cap, C->d_ev_nodes, C->d_cnt,
-                       C->d_touched[tsel], C->d_tpos, tsel);
+    hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
+                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel);
     hipLaunchKernelGGL(k_ct_alloc, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
-    hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->cap, C->d_ev_nodes, C->d_ev_f,
-                       C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
+    hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
+                       C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
                        C->d_terms, c->d_fext);
     HIPCHK(hipGetLastError());
@@ -1133,9 +1189,14 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
-    if (!std::strcmp(key, "contact_tri_lanes")) {
-        if (value != 1 && value != 32) return fail(HAKAI_ERR_ARG, "contact_tri_lanes must be 1 or 32");
-        C->tri_lanes = (int)value;
+    if (!std::strcmp(key, "contact_candidate_cap")) {
+        if (value < 1 || value > (1LL << 31) - 1) return fail(HAKAI_ERR_ARG, "contact_candidate_cap out of range");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (C->d_cand) (void)hipFree(C->d_cand);
+        C->d_cand = nullptr;
+        C->cand_cap = value;
+        HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
+        HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, sizeof(unsigned int), c->stream));
         return 0;
     }
     if (!std::strcmp(key, "contact_full_rebuild")) {
@@ -1153,7 +1214,7 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         dfree(C->d_touched[1]);
         dfree(C->d_toff);
         dfree(C->d_tcnt);
-        C->cap = value;
+        C->cap = (value + kEvShards - 1) / kEvShards * kEvShards;
         C->tcap = std::min<long long>(c->nN, 4 * C->cap);
         HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
@@ -1165,6 +1226,8 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         // the previous step's touched list is gone: clear external_force and its count
         HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kTouched, 0, 2 * sizeof(unsigned int), c->stream));
+        HIPCHK(hipMemsetAsync(C->d_ctl + kEvMax, 0, sizeof(unsigned int), c->stream));
+        HIPCHK(hipMemsetAsync(C->d_ctl + kEvShardMax, 0, sizeof(unsigned int), c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         return 0;
     }
@@ -1174,12 +1237,18 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
 int contact_check(hakai_ctx* c) {
     Contact* C = c->contact;
     if (!C) return 0;
-    unsigned int mx = 0;
+    unsigned int mx = 0, mc = 0;
     HIPCHK(hipMemcpyAsync(&mx, C->d_ctl + kEvMax, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&mc, C->d_ctl + kNcandMax, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if ((long long)mx > C->cap)
-        return fail(HAKAI_ERR_STATE, "contact: %u events in one step exceed the buffer (%lld); raise "
-                    "hakai_set_tuning(\"contact_event_cap\")", mx, C->cap);
+    if ((long long)mc > C->cand_cap)
+        return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step exceed the buffer (%lld); raise "
+                    "hakai_set_tuning(\"contact_candidate_cap\")", mc, C->cand_cap);
+    unsigned int ms = 0;
+    HIPCHK(hipMemcpy(&ms, C->d_ctl + kEvShardMax, sizeof(unsigned int), hipMemcpyDeviceToHost));
+    if ((long long)ms > C->cap / kEvShards)
+        return fail(HAKAI_ERR_STATE, "contact: %u events in one step (%u in one of %d shards) exceed the buffer "
+                    "(%lld); raise hakai_set_tuning(\"contact_event_cap\")", mx, ms, kEvShards, C->cap);
     return 0;
 }
 
@@ -1405,7 +1474,12 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     C->n_nj = (int)nj_node.size();
     C->n_tri = (int)tri_ele.size();
     C->nseg = (int)seg.size() / 8;
-    C->cap = std::max<long long>(1 << 16, 8LL * C->n_ni);
+    {  // event buffer: 8 events per initial contact point (overflow is detected and reported)
+        long long ci0 = 0;
+        for (int p = 0; p < C->npairs; ++p) ci0 += C->pair_counts[3 * p];
+        C->cap = std::max<long long>(1 << 16, 8LL * ci0);
+        C->cap = (C->cap + kEvShards - 1) / kEvShards * kEvShards;
+    }
     C->tcap = std::min<long long>(c->nN, 4 * C->cap);
     // live-list regions: i-node segments, j-node segments, then the triangle list; tiles of
     // kTile entries inside one region each (full rebuild)
@@ -1495,6 +1569,8 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     HIPCHK(dalloc(&C->d_tri_live, (size_t)C->n_tri));
     HIPCHK(dalloc(&C->d_bbox, 12 * (size_t)C->npairs));
     HIPCHK(dalloc(&C->d_ctl, (size_t)kCtl));
+    HIPCHK(dalloc(&C->d_evs, (size_t)kEvShards * kShardStride));
+    HIPCHK(hipMemsetAsync(C->d_evs, 0, (size_t)kEvShards * kShardStride * sizeof(unsigned int), s));
     HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_cnt, (size_t)c->nN + 1));
@@ -1503,7 +1579,12 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     HIPCHK(dalloc(&C->d_touched[1], (size_t)C->tcap));
     HIPCHK(dalloc(&C->d_toff, (size_t)C->tcap));
     HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
-    HIPCHK(dalloc(&C->d_cand, (size_t)C->n_tri));
+    {
+        long long t0 = 0;  // initial live triangles
+        for (int p = 0; p < C->npairs; ++p) t0 += C->pair_counts[3 * p + 1];
+        C->cand_cap = std::min<long long>(std::max<long long>(C->n_tri, 1), std::max<long long>(1 << 16, 4 * t0));
+    }
+    HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));

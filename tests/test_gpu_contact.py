@@ -129,7 +129,9 @@ def test_event_cap_overflow_is_reported():
     """A contact step with more events than the buffer holds fails loudly (no silent truncation);
     raising the cap through hakai_set_tuning recovers."""
     from hakai._abi import HakaiError
-    m = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.03, seed=4, n_steps=60)
+    # > 64 events per step once the 9x9-node impactor face is in contact: the smallest buffer (one
+    # event in each of the 64 shards) must overflow
+    m = mesh.two_body_model(plate=(12, 12, 1), impactor=(8, 8, 1), v=-1e5, perturb=0.03, seed=4, n_steps=60)
     with Solver(m) as sv:
         sv.set_tuning("contact_event_cap", 1)
         with pytest.raises(HakaiError):

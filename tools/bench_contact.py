@@ -20,7 +20,6 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--preload", type=int, default=30, help="steps before timing (contact starts at ~10)")
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--tri-lanes", type=int, default=0, help="contact_tri_lanes tuning (0: library default)")
     a = ap.parse_args()
     import numpy as np
     from hakai import mesh
@@ -32,8 +31,6 @@ def main():
     sv = Solver(m)
     t2 = time.time()
     pairs, sizes = sv.contact_info()
-    if a.tri_lanes:
-        sv.set_tuning("contact_tri_lanes", a.tri_lanes)
     sv.step(1, a.preload)
     sv.sync()
     sv.profile(True)
