@@ -551,9 +551,9 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
         HIPCHK(hipMemcpyAsync(c->d_u[1 - c->cur], dpre.data(), fn * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    hkc::contact_state_reset(c, c->h_velo0.data());
-    HIPCHK(hipStreamSynchronize(s));
     c->state_ok = true;
+    if (int r = hkc::contact_state_reset(c, c->h_velo0.data())) return r;
+    HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
 
@@ -621,11 +621,11 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
     hkc::comm_reset(c);
+    c->state_ok = true;
     if (c->contact) {
-        hkc::contact_state_reset(c, c->h_velo0.empty() ? nullptr : c->h_velo0.data());
+        if (int r = hkc::contact_state_reset(c, c->h_velo0.empty() ? nullptr : c->h_velo0.data())) return r;
         HIPCHK(hipStreamSynchronize(s));
     }
-    c->state_ok = true;
     return 0;
 }
 
@@ -770,6 +770,8 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         HIPCHK(hk::launch_element(ea, c->has_ductile, it == n_steps - 1, s));
         hkc::prof_end(c, &ep);
         rc = hkc::comm_post_element(c, (long long)t);
+        if (rc) return rc;
+        rc = hkc::contact_post_step(c);
         if (rc) return rc;
         c->steps_done++;
         c->last_dt = d_time;

@@ -46,6 +46,11 @@ struct Comm {
     double* d_saved = nullptr;                   // u_pre of interface nodes [n_up+n_dn][3]
     bool pending = false;
     int pending_par = 0;
+    // all-gather of equal-size blocks (the contact mirror, hakai_contact.hip): per-parity send
+    // buffers registered by their owner, "packed" events recorded on the context's stream
+    void* ag_send[2] = {nullptr, nullptr};
+    hipEvent_t ev_ag[2] = {nullptr, nullptr};
+    hipEvent_t ev_ag_ready = nullptr, ev_ag_done = nullptr;
 };
 
 struct LocalGroup {
@@ -125,7 +130,7 @@ __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const i
 __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
                       const double* fe, long long cs, int nslot, const double* up_sendP, const double* up_recvC,
                       const double* dn_recvP, const double* saved, const double* u, double* out, const double* mass,
-                      double dt) {
+                      const double* fext, double dt) {
 #pragma clang fp contract(off)
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_up + n_dn) return;
@@ -158,7 +163,8 @@ __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const in
     for (int c = 0; c < 3; ++c) {
         const double uc = u[3 * n + c];
         const double up_ = saved[3 * j + c];
-        out[3 * n + c] = inv * (0.0 - Q[c] + mdt2 * (2.0 * uc - up_) + dC / 2.0 / dt * up_);
+        const double f = fext ? fext[3 * n + c] : 0.0;  // contact force (external_force, :500-564)
+        out[3 * n + c] = inv * (f - Q[c] + mdt2 * (2.0 * uc - up_) + dC / 2.0 / dt * up_);
     }
 }
 
@@ -198,6 +204,10 @@ int comm_common_init(hakai_ctx* c, hkc::Comm* m) {
     if (hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_packed[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_packed[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_ag[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_ag[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_ag_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_ag_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess) {
         c->comm = m;
         hkc::comm_destroy(c);
@@ -226,8 +236,12 @@ void comm_destroy(hakai_ctx* c) {
             delete m->group;
         }
     }
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p) {
         if (m->ev_packed[p]) (void)hipEventDestroy(m->ev_packed[p]);
+        if (m->ev_ag[p]) (void)hipEventDestroy(m->ev_ag[p]);
+    }
+    if (m->ev_ag_ready) (void)hipEventDestroy(m->ev_ag_ready);
+    if (m->ev_ag_done) (void)hipEventDestroy(m->ev_ag_done);
     if (m->ev_done) (void)hipEventDestroy(m->ev_done);
     if (m->cs) (void)hipStreamDestroy(m->cs);
     delete m;
@@ -235,7 +249,51 @@ void comm_destroy(hakai_ctx* c) {
 }
 
 bool comm_is_local(const hakai_ctx* c) {
-    return c->comm && c->comm->mode == 1 && c->comm->n_up + c->comm->n_dn > 0;
+    return c->comm && c->comm->mode == 1 && (c->comm->n_up + c->comm->n_dn > 0 || c->comm->ag_send[0]);
+}
+
+int comm_rank(const hakai_ctx* c) { return c->comm ? c->comm->rank : 0; }
+int comm_size(const hakai_ctx* c) { return c->comm ? c->comm->nranks : 1; }
+
+int comm_gather_register(hakai_ctx* c, void* send0, void* send1) {
+    Comm* m = c->comm;
+    if (!m) return send0 ? fail(HAKAI_ERR_STATE, "all-gather without a communicator") : 0;
+    m->ag_send[0] = send0;
+    m->ag_send[1] = send1;
+    return 0;
+}
+
+int comm_gather_mark(hakai_ctx* c, int par) {
+    Comm* m = c->comm;
+    if (!m) return fail(HAKAI_ERR_STATE, "all-gather without a communicator");
+    HIPCHK(hipEventRecord(m->ev_ag[par], c->stream));
+    return 0;
+}
+
+// recv[q*bytes .. (q+1)*bytes) = rank q's send block of parity par, ordered on c->stream. RCCL runs
+// on the communicator's own stream, like the interface exchange, so every RCCL operation of a
+// rank is issued to ONE stream in one order (no cross-stream interleaving between ranks).
+int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes) {
+    Comm* m = c->comm;
+    if (!m || !m->ag_send[par]) return fail(HAKAI_ERR_STATE, "all-gather: no registered send buffer");
+    if (m->mode == 0) {
+        HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
+        HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
+        NCCLCHK(ncclAllGather(m->ag_send[par], recv, bytes, ncclUint8, m->nc, m->cs));
+        HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
+        HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
+        return 0;
+    }
+    // in-process group: pull every rank's block (the peers packed it at the end of their previous
+    // step, or at their state reset / set_contact_global; see hakai_contact.hip, "mirror")
+    for (int q = 0; q < m->nranks; ++q) {
+        Comm* p = q == m->rank ? m : peer(m, q);
+        if (!p || !p->ag_send[par]) return fail(HAKAI_ERR_COMM, "local group: rank %d has no contact mirror", q);
+        HIPCHK(hipStreamWaitEvent(c->stream, p->ev_ag[par], 0));
+        HIPCHK(hipMemcpyAsync((char*)recv + (size_t)q * bytes, p->ag_send[par], bytes, hipMemcpyDeviceToDevice,
+                              c->stream));
+    }
+    return 0;
 }
 
 int comm_reset(hakai_ctx* c) {
@@ -282,7 +340,8 @@ int comm_post_nodal(hakai_ctx* c, double d_time) {
         const int n = m->n_up + m->n_dn;
         hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
                            c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
-                           m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, d_time);
+                           m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, c->contact ? c->d_fext : nullptr,
+                           d_time);
         HIPCHK(hipGetLastError());
     }
     prof_end(c, &ep);

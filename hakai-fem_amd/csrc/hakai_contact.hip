@@ -50,7 +50,44 @@ struct PairParam {
     int pad;
 };
 
+// Multi-GPU contact (hakai_set_contact_global, §8f-3). Every rank keeps a mirror of the GLOBAL
+// contact model -- coordinates, connectivity, masses of the whole mesh (static), plus the
+// displacements of the contact nodes and the deletion state of the contact elements (per step) --
+// and runs the single-GPU kernels below on it, so every rank computes the same events and the same
+// correctly rounded nodal sums as one GPU: N ranks are bit-identical to one. Per step each rank
+// packs, for the contact nodes it owns (owner = rank of the lowest incident element) and its own
+// contact elements, one fixed-size block; the blocks are all-gathered (RCCL over xGMI, or device
+// copies in an in-process group) and scattered into the mirror. The block of step s is packed at
+// the end of step s-1 (or at the state reset, s = 0), so an in-process group stepped rank by rank
+// finds every peer's block ready. Contact work is replicated, not divided.
+struct Mirror {
+    int rank = 0, nranks = 1;
+    int maxx = 0, maxe = 0;           // block capacity: owned contact nodes, contact elements per rank
+    int nxo = 0, neo = 0;             // this rank's counts
+    int* d_xo = nullptr;              // [nxo] local node ids of the owned contact nodes (ascending global id)
+    int* d_eo = nullptr;              // [neo] local element ids of this rank's contact elements
+    int* d_xg = nullptr;              // [nranks*maxx] global node id of each block slot (-1: padding)
+    int* d_eg = nullptr;              // [nranks*maxe] global element id of each block slot (-1: padding)
+    int* d_g2l = nullptr;             // [nN global] local node id or -1
+    double* g_coord = nullptr;        // [nN][3] global mesh (static)
+    double* g_mass = nullptr;         // [nN]
+    int* g_conn = nullptr;            // [nE][8]
+    double* g_u[2] = {nullptr, nullptr};  // displacement of step s in g_u[s&1], of step s-1 in the other
+    int* g_flag = nullptr;            // [nE] 1 active, 0 deleted (derived from the deletion step)
+    int* g_del = nullptr;             // [nE+2] deletion step; [nE+1] last step with any deletion
+    double* g_fext = nullptr;         // [nN][3] contact force on the global node space
+    double* d_velo0_loc = nullptr;    // [nN local][3] velocity before the first step (packed at s = 0)
+    char* d_send[2] = {nullptr, nullptr};
+    char* d_recv = nullptr;           // [nranks] blocks
+    // block layout (bytes): header (last deletion step), u, deletion steps; at s = 0 also u_pre, velo0
+    size_t off_u = 16, off_del = 0, off_upre = 0, off_v0 = 0, blk_step = 0, blk_full = 0;
+    long long seq = 0;                // step index since the last state reset (the block a step consumes)
+};
+
 struct Contact {
+    // node / element space of the kernels: the context's own (one GPU) or the global mirror
+    long long nN = 0, nE = 0;
+    Mirror* mir = nullptr;
     int npairs = 0;
     std::vector<PairParam> h_par;
     PairParam* d_par = nullptr;
@@ -930,6 +967,97 @@ __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, 
     }
 }
 
+// ---- multi-GPU mirror (see hkc::Mirror) -----------------------------------------------------
+struct MirLayout {
+    size_t off_u, off_del, off_upre, off_v0;
+};
+
+// this rank's block: last deletion step, u of the owned contact nodes, deletion step of its contact
+// elements; with `full` also u_pre and the velocity before the first step
+__global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const double* u, const double* upre,
+                           const double* velo0, const int* del_step, const int* del_any, char* blk, MirLayout L,
+                           int full) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) reinterpret_cast<int*>(blk)[0] = *del_any;
+    if (i < nxo) {
+        const long long n = xo[i];
+        double* pu = reinterpret_cast<double*>(blk + L.off_u) + 3 * (long long)i;
+        for (int c = 0; c < 3; ++c) pu[c] = u[3 * n + c];
+        if (full) {
+            double* pp = reinterpret_cast<double*>(blk + L.off_upre) + 3 * (long long)i;
+            double* pv = reinterpret_cast<double*>(blk + L.off_v0) + 3 * (long long)i;
+            for (int c = 0; c < 3; ++c) {
+                pp[c] = upre[3 * n + c];
+                pv[c] = velo0 ? velo0[3 * n + c] : 0.0;
+            }
+        }
+    }
+    if (i < neo) reinterpret_cast<int*>(blk + L.off_del)[i] = del_step[eo[i]];
+}
+
+// all ranks' blocks -> the mirror. Slots are disjoint (one owner per node, one rank per element).
+__global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx, int maxe, const int* xg,
+                             const int* eg, MirLayout L, int full, double* gu, double* gupre, double* gvelo0,
+                             int* gdel, int* gflag, long long nE) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < (long long)nranks * maxx) {
+        const int g = xg[i];
+        if (g >= 0) {
+            const int q = (int)(i / maxx), k = (int)(i % maxx);
+            const char* b = recv + (size_t)q * blk;
+            const double* pu = reinterpret_cast<const double*>(b + L.off_u) + 3 * (long long)k;
+            for (int c = 0; c < 3; ++c) gu[3 * (long long)g + c] = pu[c];
+            if (full) {
+                const double* pp = reinterpret_cast<const double*>(b + L.off_upre) + 3 * (long long)k;
+                const double* pv = reinterpret_cast<const double*>(b + L.off_v0) + 3 * (long long)k;
+                for (int c = 0; c < 3; ++c) {
+                    gupre[3 * (long long)g + c] = pp[c];
+                    gvelo0[3 * (long long)g + c] = pv[c];
+                }
+            }
+        }
+    }
+    if (i < (long long)nranks * maxe) {
+        const int e = eg[i];
+        if (e >= 0) {
+            const int q = (int)(i / maxe), k = (int)(i % maxe);
+            const int d = reinterpret_cast<const int*>(recv + (size_t)q * blk + L.off_del)[k];
+            gdel[e] = d;
+            gflag[e] = d == 0 ? 1 : 0;
+        }
+    }
+    if (i == 0) {
+        int mx = 0;
+        for (int q = 0; q < nranks; ++q) mx = max(mx, reinterpret_cast<const int*>(recv + (size_t)q * blk)[0]);
+        gdel[nE + 1] = mx;
+    }
+}
+
+// the local external force follows the global one on the touched nodes this rank holds: the
+// previous step's back to 0 (after k_ct_reset), this step's copied (after k_ct_sum)
+__global__ void k_mir_fext_zero(const unsigned int* ctl, int sel, const int* touched, const int* g2l, double* fext) {
+    const int nt = (int)ctl[kTouched + sel];
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
+        const long long l = g2l[touched[q]];
+        if (l < 0) continue;
+        fext[3 * l] = 0.0;
+        fext[3 * l + 1] = 0.0;
+        fext[3 * l + 2] = 0.0;
+    }
+}
+
+__global__ void k_mir_fext_copy(const unsigned int* ctl, int sel, const int* touched, const int* g2l,
+                                const double* gfext, double* fext) {
+    const int nt = (int)ctl[kTouched + sel];
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
+        const long long n = touched[q], l = g2l[n];
+        if (l < 0) continue;
+        fext[3 * l] = gfext[3 * n];
+        fext[3 * l + 1] = gfext[3 * n + 1];
+        fext[3 * l + 2] = gfext[3 * n + 2];
+    }
+}
+
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
     *p = nullptr;
@@ -1087,41 +1215,105 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0);
     if (C->d_tmp) (void)hipFree(C->d_tmp);
+    if (Mirror* M = C->mir) {
+        (void)comm_gather_register(c, nullptr, nullptr);
+        dfree(M->d_xo); dfree(M->d_eo); dfree(M->d_xg); dfree(M->d_eg); dfree(M->d_g2l);
+        dfree(M->g_coord); dfree(M->g_mass); dfree(M->g_conn); dfree(M->g_u[0]); dfree(M->g_u[1]);
+        dfree(M->g_flag); dfree(M->g_del); dfree(M->g_fext); dfree(M->d_velo0_loc);
+        dfree(M->d_send[0]); dfree(M->d_send[1]); dfree(M->d_recv);
+        delete M;
+    }
     delete C;
     c->contact = nullptr;
     dfree(c->d_fext);
 }
 
-void contact_state_reset(hakai_ctx* c, const double* velo0_host) {
+// multi-GPU: pack this rank's mirror block for step M->seq (full = with u_pre and velo0)
+static int mir_pack(hakai_ctx* c, bool full) {
     Contact* C = c->contact;
-    if (!C) return;
+    Mirror* M = C->mir;
+    const int par = (int)(M->seq & 1);
+    const int n = std::max(std::max(M->nxo, M->neo), 1);
+    const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
+    hipLaunchKernelGGL(k_mir_pack, dim3((n + kB - 1) / kB), dim3(kB), 0, c->stream, M->d_xo, M->nxo, M->d_eo, M->neo,
+                       c->d_u[c->cur], c->d_u[1 - c->cur], C->use_velo0 ? M->d_velo0_loc : nullptr, c->d_del_step,
+                       c->d_del_step + c->nEp + 1, M->d_send[par], L, full ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    return comm_gather_mark(c, par);
+}
+
+int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
+    Contact* C = c->contact;
+    if (!C) return 0;
     C->use_velo0 = true;
     C->force_rebuild = true;
+    if (Mirror* M = C->mir) {
+        if (velo0_host)
+            HIPCHK(hipMemcpyAsync(M->d_velo0_loc, velo0_host, 3 * (size_t)c->nN * sizeof(double),
+                                  hipMemcpyHostToDevice, c->stream));
+        M->seq = 0;
+        return mir_pack(c, true);
+    }
     if (velo0_host)
-        (void)hipMemcpyAsync(C->d_velo0, velo0_host, 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice,
-                             c->stream);
+        HIPCHK(hipMemcpyAsync(C->d_velo0, velo0_host, 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice,
+                              c->stream));
+    return 0;
+}
+
+int contact_post_step(hakai_ctx* c) {
+    Contact* C = c->contact;
+    if (!C || !C->mir) return 0;
+    C->mir->seq++;
+    return mir_pack(c, false);
 }
 
 // contact force of step t into c->d_fext (before the nodal update, :500-560)
 int contact_step(hakai_ctx* c, double t, double d_time) {
     Contact* C = c->contact;
+    Mirror* M = C->mir;
     hipStream_t s = c->stream;
     StepIn in;
-    in.coord = c->d_coord;
-    in.u = c->d_u[c->cur];
-    in.u_pre = c->d_u[1 - c->cur];
+    int* del_step = c->d_del_step;
+    const int* del_any = c->d_del_step + c->nEp + 1;
+    double* fext = c->d_fext;
+    if (M) {  // all-gather the ranks' blocks of this step into the global mirror
+        const int par = (int)(M->seq & 1);
+        const bool full = M->seq == 0;
+        const size_t blk = full ? M->blk_full : M->blk_step;
+        if (int rc = comm_allgather(c, par, M->d_recv, blk)) return rc;
+        const long long nslot = std::max(1LL, (long long)M->nranks * std::max(M->maxx, M->maxe));
+        const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
+        hipLaunchKernelGGL(k_mir_unpack, dim3((unsigned)((nslot + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
+                           M->nranks, M->maxx, M->maxe, M->d_xg, M->d_eg, L, full ? 1 : 0, M->g_u[par],
+                           M->g_u[1 - par], C->d_velo0, M->g_del, M->g_flag, C->nE);
+        in.coord = M->g_coord;
+        in.u = M->g_u[par];
+        in.u_pre = M->g_u[1 - par];
+        in.flag = M->g_flag;
+        in.conn = M->g_conn;
+        in.mass = M->g_mass;
+        del_step = M->g_del;
+        del_any = M->g_del + C->nE + 1;
+        fext = M->g_fext;
+    } else {
+        in.coord = c->d_coord;
+        in.u = c->d_u[c->cur];
+        in.u_pre = c->d_u[1 - c->cur];
+        in.flag = c->d_flag;
+        in.conn = c->d_conn;
+        in.mass = c->d_mass;
+    }
     in.velo0 = C->use_velo0 ? C->d_velo0 : nullptr;
     in.d_time = d_time;
-    in.del_step = c->d_del_step;
-    in.flag = c->d_flag;
-    in.conn = c->d_conn;
-    in.mass = c->d_mass;
+    in.del_step = del_step;
     in.t = (int)t;
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const int tsel = C->tsel = 1 - C->tsel;
     hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
-                       C->force_rebuild ? 1 : 0, c->d_del_step + c->nEp + 1, in.t, C->d_touched[1 - tsel], tsel,
-                       c->d_fext);
+                       C->force_rebuild ? 1 : 0, del_any, in.t, C->d_touched[1 - tsel], tsel, fext);
+    if (M)
+        hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
+                           M->d_g2l, c->d_fext);
     C->force_rebuild = false;
     C->last_t = in.t;
     if (C->ntile > 0) {
@@ -1129,7 +1321,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
         L.nj_orig = C->d_nj_orig; L.nj_aptr = C->d_nj_aptr; L.nj_add = C->d_nj_add;
         L.tri_ele = C->d_tri_ele; L.tri_adder = C->d_tri_adder;
-        L.flag = c->d_flag; L.del_step = c->d_del_step; L.t = in.t;
+        L.flag = in.flag; L.del_step = del_step; L.t = in.t;
         const Tile* tl = (const Tile*)C->d_tiles;
         const unsigned gt = (unsigned)std::min(C->ntile, 2048);
         // full rebuild (forced steps only)
@@ -1139,7 +1331,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
                            C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
         // incremental update (steps after a deletion)
-        hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, c->d_del_step, (int)c->nE, in.t,
+        hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
                            C->d_dlist);
         AppendIn A;
         A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
@@ -1148,7 +1340,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         A.nj_orig = C->d_nj_orig; A.nj_aptr = C->d_nj_aptr; A.nj_add = C->d_nj_add; A.nj_pair = C->d_nj_pair;
         A.pair_reg = C->d_pair_reg;
         A.tri_reg = C->tri_reg;
-        hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, c->d_del_step, in.t,
+        hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
                            C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
     }
     if (C->nseg > 0) {
@@ -1180,7 +1372,10 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, c->d_fext);
+                       C->d_terms, fext);
+    if (M)
+        hipLaunchKernelGGL(k_mir_fext_copy, dim3(64), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], M->d_g2l,
+                           M->g_fext, c->d_fext);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
@@ -1215,7 +1410,7 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         dfree(C->d_toff);
         dfree(C->d_tcnt);
         C->cap = (value + kEvShards - 1) / kEvShards * kEvShards;
-        C->tcap = std::min<long long>(c->nN, 4 * C->cap);
+        C->tcap = std::min<long long>(C->nN, 4 * C->cap);
         HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
@@ -1225,6 +1420,7 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
         // the previous step's touched list is gone: clear external_force and its count
         HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), c->stream));
+        if (C->mir) HIPCHK(hipMemsetAsync(C->mir->g_fext, 0, 3 * (size_t)C->nN * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kTouched, 0, 2 * sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvMax, 0, sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvShardMax, 0, sizeof(unsigned int), c->stream));
@@ -1254,24 +1450,25 @@ int contact_check(hakai_ctx* c) {
 
 }  // namespace hkc
 
-extern "C" {
+namespace {
 
-int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance) {
-    return hakai_set_contact_cp(c, contact_flag, element_instance, 0, nullptr, nullptr, nullptr);
-}
+// the mesh contact is set up on: the context's own, or the global one (multi-GPU)
+struct HostMesh {
+    long long nN, nE;
+    const std::vector<double>* coord;  // 3nN
+    const std::vector<int>* conn;      // 8nE, 0-based
+    const std::vector<int>* mat;       // nE, 0-based
+};
+// multi-GPU: the nodes and elements the contact kernels can ever read
+struct SetupOut {
+    std::vector<char> xmask, emask;
+};
 
-int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
-                         const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems) {
-    if (!c) return fail(HAKAI_ERR_ARG, "null");
-    if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
-        return fail(HAKAI_ERR_ARG, "set_contact_cp: bad contact-pair arrays");
-    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_contact before upload_model");
-    HIPCHK(hipSetDevice(c->device));
-    hkc::contact_destroy(c);
-    if (contact_flag < 1) return 0;
-    if (contact_flag > 2) return fail(HAKAI_ERR_ARG, "contact_flag %d (0, 1 or 2)", contact_flag);
-    if (c->comm) return fail(HAKAI_ERR_STATE, "contact with a multi-GPU communicator is not supported");
-    const int nE = (int)c->nE;
+// builds c->contact on mesh H (the surfaces, pairs and entry lists of hakai_set_contact_cp);
+// contact_flag is 1 or 2, c->contact was destroyed by the caller
+int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
+                  const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems, SetupOut* out) {
+    const int nE = (int)H.nE;
     // instances: contiguous element blocks 1, 2, ... (readInpFile numbers them this way)
     std::vector<Inst> inst;
     for (int e = 0; e < nE; ++e) {
@@ -1282,7 +1479,7 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
                 return fail(HAKAI_ERR_ARG, "element_instance must number contiguous element blocks 1, 2, ...");
             inst.emplace_back();
             inst.back().e0 = e;
-            inst.back().young = c->h_young[c->h_mat[e]];
+            inst.back().young = c->h_young[(*H.mat)[e]];
         } else if ((size_t)id != inst.size()) {
             return fail(HAKAI_ERR_ARG, "element_instance must number contiguous element blocks 1, 2, ...");
         }
@@ -1290,7 +1487,7 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     }
     const int ni = (int)inst.size();
     if (ni == 0) return 0;
-    for (auto& I : inst) build_instance(I, c->h_coord, c->h_conn);
+    for (auto& I : inst) build_instance(I, *H.coord, *H.conn);
     // pairs (:273-311) and CT entries (:332-396). With *Contact Pair surfaces the exterior faces of
     // each side are restricted to the surface's elements (get_surface_triangle's "pick up only
     // contact element", :2087-2112 -- applied only when the list is not the whole instance).
@@ -1342,17 +1539,19 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
         if (cp[k].first != cp[k].second) ct.push_back({cp[k].second, cp[k].first, cpf[k].second, cpf[k].first});
     }
     auto* C = new hkc::Contact();
+    C->nN = H.nN;
+    C->nE = H.nE;
     C->npairs = (int)ct.size();
     // element sizes (:404-421)
     {
 #pragma clang fp contract(off)
         double mn = INFINITY, mx = -INFINITY;
         for (int e = 0; e < nE; ++e) {
-            const int* el = &c->h_conn[8 * (size_t)e];
-            const double* p1 = &c->h_coord[3 * (size_t)el[0]];
+            const int* el = &(*H.conn)[8 * (size_t)e];
+            const double* p1 = &(*H.coord)[3 * (size_t)el[0]];
             const int oth[3] = {1, 3, 4};
             for (int q = 0; q < 3; ++q) {
-                const double* p = &c->h_coord[3 * (size_t)el[oth[q]]];
+                const double* p = &(*H.coord)[3 * (size_t)el[oth[q]]];
                 const double a = p1[0] - p[0], b = p1[1] - p[1], d = p1[2] - p[2];
                 const double L = std::sqrt(a * a + b * b + d * d);
                 mn = std::min(mn, L);
@@ -1374,7 +1573,7 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
                          std::vector<int>& vn, std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd) {
         // per node: initial (exterior) or the ascending list of elements whose deletion exposes it;
         // bucketed by node id in linear time (adders arrive in ascending element order)
-        const int nN = (int)c->nN;
+        const int nN = (int)H.nN;
         std::vector<char> orig((size_t)nN, 0), seen((size_t)nN, 0);
         for (int f : I.exterior)
             if (keep(I, filt, f))
@@ -1480,7 +1679,7 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
         C->cap = std::max<long long>(1 << 16, 8LL * ci0);
         C->cap = (C->cap + kEvShards - 1) / kEvShards * kEvShards;
     }
-    C->tcap = std::min<long long>(c->nN, 4 * C->cap);
+    C->tcap = std::min<long long>(H.nN, 4 * C->cap);
     // live-list regions: i-node segments, j-node segments, then the triangle list; tiles of
     // kTile entries inside one region each (full rebuild)
     std::vector<Tile> tiles;
@@ -1529,6 +1728,18 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
         }
         invert(taptr, tadd, C->n_tri, el_tri_ptr, el_tri);
     }
+    if (out) {  // every node / element an entry refers to (positions, masses, adders, triangle owners)
+        out->xmask.assign((size_t)H.nN, 0);
+        out->emask.assign((size_t)H.nE, 0);
+        for (int n : ni_node) out->xmask[n] = 1;
+        for (int n : nj_node) out->xmask[n] = 1;
+        for (int n : tri_nodes) out->xmask[n] = 1;
+        for (int e : ni_add) out->emask[e] = 1;
+        for (int e : nj_add) out->emask[e] = 1;
+        for (int e : tri_ele) out->emask[e] = 1;
+        for (int e : tri_adder)
+            if (e >= 0) out->emask[e] = 1;
+    }
     hipStream_t s = c->stream;
     int rc = 0;
 #define UP(dst, v)                                          \
@@ -1573,8 +1784,8 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     HIPCHK(hipMemsetAsync(C->d_evs, 0, (size_t)kEvShards * kShardStride * sizeof(unsigned int), s));
     HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
-    HIPCHK(dalloc(&C->d_cnt, (size_t)c->nN + 1));
-    HIPCHK(dalloc(&C->d_tpos, (size_t)c->nN + 1));
+    HIPCHK(dalloc(&C->d_cnt, (size_t)H.nN + 1));
+    HIPCHK(dalloc(&C->d_tpos, (size_t)H.nN + 1));
     HIPCHK(dalloc(&C->d_touched[0], (size_t)C->tcap));
     HIPCHK(dalloc(&C->d_touched[1], (size_t)C->tcap));
     HIPCHK(dalloc(&C->d_toff, (size_t)C->tcap));
@@ -1586,18 +1797,19 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     }
     HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
-    HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
+    HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)H.nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));
     HIPCHK(hipMemsetAsync(C->d_bcnt, 0, ((size_t)C->htot + 1) * sizeof(int), s));
-    HIPCHK(hipMemsetAsync(C->d_cnt, 0, ((size_t)c->nN + 1) * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(C->d_cnt, 0, ((size_t)H.nN + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_ctl, 0, kCtl * sizeof(unsigned int), s));
     HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), s));
     C->force_rebuild = true;
-    // velocity before the first step: the state's (IC / uploaded) velocity
-    if (!c->h_velo0.empty())
+    // velocity before the first step: the state's (IC / uploaded) velocity (multi-GPU: gathered
+    // into the mirror with the first block)
+    if (!c->h_velo0.empty() && !out)
         HIPCHK(hipMemcpyAsync(C->d_velo0, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice, s));
     else
-        HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)c->nN * sizeof(double), s));
+        HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)H.nN * sizeof(double), s));
     C->use_velo0 = c->steps_done == 0 || !c->h_velo0.empty();
     size_t t1 = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, C->d_bcnt, C->d_boff, C->htot + 1, s));
@@ -1605,6 +1817,177 @@ int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* elem
     HIPCHK(hipMalloc(&C->d_tmp, std::max<size_t>(C->tmp_bytes, 1)));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
+}
+
+// Multi-GPU mirror of the global contact model (hkc::Mirror) for a contact set up on the global
+// mesh: block layout, owners, exchange slots, static global arrays; packs block 0 if a state exists.
+int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nElement,
+                 const std::vector<double>& gx, const std::vector<int>& gconn, const double* diag_M,
+                 const std::vector<int>& g2l, const int64_t* rank_elem_off) {
+    hkc::Contact* C = c->contact;
+    auto* M = new hkc::Mirror();
+    C->mir = M;
+    const int nr = hkc::comm_size(c), rank = hkc::comm_rank(c);
+    M->rank = rank;
+    M->nranks = nr;
+    // owner of a node: the rank of its lowest incident element (ranks hold ascending element ranges)
+    std::vector<int> minel((size_t)nNode, INT32_MAX);
+    for (long long e = 0; e < nElement; ++e)
+        for (int i = 0; i < 8; ++i) {
+            int& m = minel[gconn[8 * e + i]];
+            m = std::min(m, (int)e);
+        }
+    auto rank_of = [&](long long e) {
+        return (int)(std::upper_bound(rank_elem_off, rank_elem_off + nr + 1, (int64_t)e) - rank_elem_off) - 1;
+    };
+    std::vector<std::vector<int>> xs((size_t)nr), es((size_t)nr);
+    for (long long n = 0; n < nNode; ++n)
+        if (so.xmask[n] && minel[n] != INT32_MAX) xs[rank_of(minel[n])].push_back((int)n);
+    for (long long e = 0; e < nElement; ++e)
+        if (so.emask[e]) es[rank_of(e)].push_back((int)e);
+    for (int q = 0; q < nr; ++q) {
+        M->maxx = std::max(M->maxx, (int)xs[q].size());
+        M->maxe = std::max(M->maxe, (int)es[q].size());
+    }
+    std::vector<int> xg((size_t)nr * M->maxx, -1), eg((size_t)nr * M->maxe, -1), xo, eo;
+    for (int q = 0; q < nr; ++q) {
+        std::copy(xs[q].begin(), xs[q].end(), xg.begin() + (size_t)q * M->maxx);
+        std::copy(es[q].begin(), es[q].end(), eg.begin() + (size_t)q * M->maxe);
+    }
+    for (int n : xs[rank]) {
+        if (g2l[n] < 0) return fail(HAKAI_ERR_ARG, "set_contact_global: owned contact node %d is not in the local model", n + 1);
+        xo.push_back(g2l[n]);
+    }
+    for (int e : es[rank]) eo.push_back(e - (int)rank_elem_off[rank]);
+    M->nxo = (int)xo.size();
+    M->neo = (int)eo.size();
+    M->off_u = 16;
+    M->off_del = M->off_u + 24 * (size_t)M->maxx;
+    M->blk_step = M->off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
+    M->off_upre = M->blk_step;
+    M->off_v0 = M->off_upre + 24 * (size_t)M->maxx;
+    M->blk_full = M->off_v0 + 24 * (size_t)M->maxx;
+    std::vector<double> gmass((size_t)nNode);
+    for (long long n = 0; n < nNode; ++n) gmass[n] = diag_M[3 * n];
+    std::vector<int> ones((size_t)nElement, 1);
+    hipStream_t s = c->stream;
+    HIPCHK(upload(&M->d_xo, xo, s));
+    HIPCHK(upload(&M->d_eo, eo, s));
+    HIPCHK(upload(&M->d_xg, xg, s));
+    HIPCHK(upload(&M->d_eg, eg, s));
+    HIPCHK(upload(&M->d_g2l, g2l, s));
+    HIPCHK(upload(&M->g_coord, gx, s));
+    HIPCHK(upload(&M->g_mass, gmass, s));
+    HIPCHK(upload(&M->g_conn, gconn, s));
+    HIPCHK(upload(&M->g_flag, ones, s));
+    for (int p = 0; p < 2; ++p) {
+        HIPCHK(dalloc(&M->g_u[p], 3 * (size_t)nNode));
+        HIPCHK(hipMemsetAsync(M->g_u[p], 0, 3 * (size_t)nNode * sizeof(double), s));
+        HIPCHK(dalloc(&M->d_send[p], M->blk_full));
+        HIPCHK(hipMemsetAsync(M->d_send[p], 0, M->blk_full, s));
+    }
+    HIPCHK(dalloc(&M->d_recv, (size_t)nr * M->blk_full));
+    HIPCHK(dalloc(&M->g_del, (size_t)nElement + 2));
+    HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
+    HIPCHK(dalloc(&M->g_fext, 3 * (size_t)nNode));
+    HIPCHK(hipMemsetAsync(M->g_fext, 0, 3 * (size_t)nNode * sizeof(double), s));
+    HIPCHK(dalloc(&M->d_velo0_loc, 3 * (size_t)c->nN));
+    if (!c->h_velo0.empty())
+        HIPCHK(hipMemcpyAsync(M->d_velo0_loc, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double),
+                              hipMemcpyHostToDevice, s));
+    else
+        HIPCHK(hipMemsetAsync(M->d_velo0_loc, 0, 3 * (size_t)c->nN * sizeof(double), s));
+    if (int rc = hkc::comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
+    M->seq = 0;
+    if (c->state_ok)
+        if (int rc = hkc::mir_pack(c, true)) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance) {
+    return hakai_set_contact_cp(c, contact_flag, element_instance, 0, nullptr, nullptr, nullptr);
+}
+
+int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
+                         const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
+        return fail(HAKAI_ERR_ARG, "set_contact_cp: bad contact-pair arrays");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_contact before upload_model");
+    HIPCHK(hipSetDevice(c->device));
+    hkc::contact_destroy(c);
+    if (contact_flag < 1) return 0;
+    if (contact_flag > 2) return fail(HAKAI_ERR_ARG, "contact_flag %d (0, 1 or 2)", contact_flag);
+    if (c->comm)
+        return fail(HAKAI_ERR_STATE, "contact on a rank of a multi-GPU group: use hakai_set_contact_global");
+    const HostMesh H{c->nN, c->nE, &c->h_coord, &c->h_conn, &c->h_mat};
+    return contact_setup(c, H, contact_flag, element_instance, n_cp, cp_instance, cp_elem_off, cp_elems, nullptr);
+}
+
+int hakai_set_contact_global(hakai_ctx* c, int32_t contact_flag, int64_t nNode, const double* coordmat,
+                             int64_t nElement, const int64_t* elementmat, const int64_t* element_material,
+                             const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
+                             const int64_t* rank_elem_off, int32_t n_cp, const int32_t* cp_instance,
+                             const int64_t* cp_elem_off, const int64_t* cp_elems) {
+    if (!c) return fail(HAKAI_ERR_ARG, "null");
+    if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
+        return fail(HAKAI_ERR_ARG, "set_contact_global: bad contact-pair arrays");
+    if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_contact_global before upload_model");
+    if (!c->comm) return fail(HAKAI_ERR_STATE, "set_contact_global before comm_init / comm_init_local");
+    HIPCHK(hipSetDevice(c->device));
+    hkc::contact_destroy(c);
+    if (contact_flag < 1) return 0;
+    if (contact_flag > 2) return fail(HAKAI_ERR_ARG, "contact_flag %d (0, 1 or 2)", contact_flag);
+    if (nNode <= 0 || nElement <= 0 || !coordmat || !elementmat || !element_material || !diag_M ||
+        !local_node_global || !rank_elem_off)
+        return fail(HAKAI_ERR_ARG, "set_contact_global: bad arguments");
+    if (nNode >= (int64_t)INT32_MAX || 8 * nElement >= (int64_t)INT32_MAX)
+        return fail(HAKAI_ERR_ARG, "set_contact_global: mesh too large for int32 indexing");
+    const int nr = hkc::comm_size(c), rank = hkc::comm_rank(c);
+    if (rank_elem_off[0] != 0 || rank_elem_off[nr] != nElement)
+        return fail(HAKAI_ERR_ARG, "set_contact_global: rank_elem_off must run from 0 to nElement");
+    for (int q = 0; q < nr; ++q)
+        if (rank_elem_off[q + 1] < rank_elem_off[q]) return fail(HAKAI_ERR_ARG, "set_contact_global: rank_elem_off decreases");
+    if (rank_elem_off[rank] != c->elem_offset || rank_elem_off[rank + 1] - rank_elem_off[rank] != c->nE)
+        return fail(HAKAI_ERR_ARG, "set_contact_global: rank %d holds elements %lld..+%lld, rank_elem_off says %lld..%lld",
+                    rank, c->elem_offset, c->nE, (long long)rank_elem_off[rank], (long long)rank_elem_off[rank + 1]);
+    std::vector<double> gx(coordmat, coordmat + 3 * nNode);
+    std::vector<int> gconn(8 * (size_t)nElement), gmat((size_t)nElement);
+    for (int64_t e = 0; e < nElement; ++e) {
+        for (int i = 0; i < 8; ++i) {
+            const int64_t n = elementmat[8 * e + i];
+            if (n < 1 || n > nNode) return fail(HAKAI_ERR_ARG, "set_contact_global: elementmat[%d,%lld] = %lld", i + 1, (long long)e + 1, (long long)n);
+            gconn[8 * e + i] = (int)(n - 1);
+        }
+        const int64_t m = element_material[e];
+        if (m < 1 || m > c->nmat) return fail(HAKAI_ERR_ARG, "set_contact_global: element_material[%lld] = %lld", (long long)e + 1, (long long)m);
+        gmat[e] = (int)(m - 1);
+    }
+    // local -> global nodes, checked against this rank's uploaded connectivity
+    std::vector<int> g2l((size_t)nNode, -1);
+    for (long long l = 0; l < c->nN; ++l) {
+        const int64_t g = local_node_global[l];
+        if (g < 1 || g > nNode || g2l[g - 1] >= 0)
+            return fail(HAKAI_ERR_ARG, "set_contact_global: local_node_global[%lld] = %lld", l + 1, (long long)g);
+        g2l[g - 1] = (int)l;
+    }
+    for (long long e = 0; e < c->nE; ++e)
+        for (int i = 0; i < 8; ++i)
+            if (gconn[8 * (c->elem_offset + e) + i] != local_node_global[c->h_conn[8 * e + i]] - 1)
+                return fail(HAKAI_ERR_ARG, "set_contact_global: local element %lld differs from global element %lld", e + 1,
+                            c->elem_offset + e + 1);
+    const HostMesh H{nNode, nElement, &gx, &gconn, &gmat};
+    SetupOut so;
+    int rc = contact_setup(c, H, contact_flag, element_instance, n_cp, cp_instance, cp_elem_off, cp_elems, &so);
+    if (rc || !c->contact) return rc;
+    rc = mirror_build(c, so, nNode, nElement, gx, gconn, diag_M, g2l, rank_elem_off);
+    if (rc) hkc::contact_destroy(c);
+    return rc;
 }
 
 int hakai_set_contact_params(hakai_ctx* c, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s) {

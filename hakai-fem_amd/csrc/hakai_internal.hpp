@@ -113,11 +113,19 @@ int comm_reset(hakai_ctx* c);
 int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface nodes
 int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
 int comm_post_element(hakai_ctx* c, long long step); // pack interface forces, start exchange
-bool comm_is_local(const hakai_ctx* c);              // in-process group with interfaces
+bool comm_is_local(const hakai_ctx* c);              // in-process group stepped in lockstep
+int comm_rank(const hakai_ctx* c);
+int comm_size(const hakai_ctx* c);
+// All-gather of equal-size device blocks, one per rank, from per-parity send buffers (RCCL
+// ncclAllGather, or device copies between the contexts of an in-process group).
+int comm_gather_register(hakai_ctx* c, void* send0, void* send1);
+int comm_gather_mark(hakai_ctx* c, int par);                             // send[par] packed (c->stream)
+int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes);     // ordered on c->stream
 // Contact (no-ops without hakai_set_contact).
 void contact_destroy(hakai_ctx* c);
-void contact_state_reset(hakai_ctx* c, const double* velo0_host);
+int contact_state_reset(hakai_ctx* c, const double* velo0_host);
 int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
+int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack the mirror block of the next step
 int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
 int contact_tuning(hakai_ctx* c, const char* key, long long value);  // "contact_*" tuning keys
 }  // namespace hkc

@@ -105,6 +105,8 @@ def lib() -> ctypes.CDLL:
         "hakai_set_tuning": (c_int, [c_void_p, c_char_p, c_int64]),
         "hakai_set_contact": (c_int, [c_void_p, c_int32, PI64]),
         "hakai_set_contact_cp": (c_int, [c_void_p, c_int32, PI64, c_int32, PI32, PI64, PI64]),
+        "hakai_set_contact_global": (c_int, [c_void_p, c_int32, c_int64, PD, c_int64, PI64, PI64, PI64, PD, PI64,
+                                             PI64, c_int32, PI32, PI64, PI64]),
         "hakai_set_contact_params": (c_int, [c_void_p, c_double, c_double, c_double, c_double, c_double]),
         "hakai_contact_info": (c_int, [c_void_p, POINTER(c_int32), PI64, c_int32, PD]),
         "hakai_contact_stats": (c_int, [c_void_p, PI64, c_int32]),
@@ -136,7 +138,7 @@ def exported_symbols() -> list[str]:
         "hakai_download_state", "hakai_step", "hakai_sync", "hakai_deleted", "hakai_negative_jacobians",
         "hakai_node_stress_strain", "hakai_stress_hexa", "hakai_triax_stress", "hakai_lumped_mass",
         "hakai_profile_enable", "hakai_profile_mask", "hakai_profile_read", "hakai_set_tuning", "hakai_set_contact",
-        "hakai_set_contact_cp", "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_stats", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",
+        "hakai_set_contact_cp", "hakai_set_contact_global", "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_stats", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",
         "hakai_comm_init_local", "hakai_set_interface", "hakai_set_element_offset", "hakai_inp_read", "hakai_inp_free", "hakai_write_vtk", "hakai_run_inp",
     ]
 

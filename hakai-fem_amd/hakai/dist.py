@@ -25,6 +25,60 @@ def partition_ranges(n: int, world: int) -> list[tuple[int, int]]:
     return out
 
 
+def range_partition(glob: Model, rank: int, world: int, glob_diag: np.ndarray | None = None):
+    """Contiguous global element ranges of a general mesh (e.g. a multi-instance contact model).
+
+    Rank r holds elements [off[r], off[r+1]) (partition_ranges) and the nodes they touch, numbered
+    in ascending global id. A node may be shared by two ADJACENT ranks only (the interface protocol
+    of hakai_comm.cpp); other cuts raise ValueError. The lumped mass is the global one restricted,
+    so it is bit-identical to the single-GPU mass.
+
+    Returns (local Model, local diag_M (3 nN_local), (local_node, rank_lo, rank_hi),
+    local_node_global (1-based, nN_local), rank_elem_off (world+1))."""
+    rng = partition_ranges(glob.nElement, world)
+    off = np.array([r[0] for r in rng] + [glob.nElement], np.int64)
+    e0, e1 = rng[rank]
+    E = glob.elementmat - 1
+    elem_rank = np.repeat(np.arange(world, dtype=np.int64), np.diff(off))
+    lo = np.full(glob.nNode, world, np.int64)
+    hi = np.full(glob.nNode, -1, np.int64)
+    np.minimum.at(lo, E.ravel(), np.repeat(elem_rank, 8))
+    np.maximum.at(hi, E.ravel(), np.repeat(elem_rank, 8))
+    if np.any(hi - lo > 1):
+        bad = int(np.argmax(hi - lo > 1))
+        raise ValueError(f"node {bad + 1} is shared by ranks {lo[bad]} and {hi[bad]}: only adjacent ranks may "
+                         "share nodes (use fewer ranks or renumber the elements)")
+    mine = np.unique(E[e0:e1].ravel())
+    g2l = np.full(glob.nNode, -1, np.int64)
+    g2l[mine] = np.arange(mine.shape[0])
+    if glob_diag is None:
+        glob_diag, _ = glob.lumped_mass()
+    diag = np.ascontiguousarray(np.asarray(glob_diag).reshape(-1, 3)[mine].ravel())
+
+    def to_local_dofs(d):
+        d = np.asarray(d, np.int64)
+        ln = g2l[(d - 1) // 3]
+        keep = ln >= 0
+        return 3 * ln[keep] + (d[keep] - 1) % 3 + 1
+
+    bc = []
+    for g in glob.bc:
+        ents = [(to_local_dofs(d), v) for d, v in g.entries]
+        ents = [(d, v) for d, v in ents if len(d)]
+        if ents:
+            bc.append(type(g)(ents, g.amp_time, g.amp_value))
+    ic_l = g2l[(glob.ic_dofs - 1) // 3]
+    keep = ic_l >= 0
+    local = Model(np.ascontiguousarray(glob.coordmat[mine]), g2l[E[e0:e1]] + 1,
+                  glob.element_material[e0:e1].copy(), glob.materials, bc,
+                  3 * ic_l[keep] + (glob.ic_dofs[keep] - 1) % 3 + 1, glob.ic_values[keep], glob.d_time,
+                  glob.end_time, glob.mass_scaling, name=f"{glob.name}[rank {rank}/{world}]")
+    shared = mine[lo[mine] != hi[mine]]
+    iface = (g2l[shared], lo[shared].astype(np.int32), hi[shared].astype(np.int32))
+    local.global_element_offset = int(e0)
+    return local, diag, iface, (mine + 1).astype(np.int64), off
+
+
 def _bar_layers(nx, ny, k0, k1, coord_global):
     """Nodes of layers k0..k1 (inclusive) and elements of layers k0..k1-1 of a structured bar,
     renumbered locally (1-based). coord_global: (nN_global, 3)."""

@@ -202,6 +202,27 @@ class Solver:
     def set_element_offset(self, offset: int):
         check(self.L.hakai_set_element_offset(self.ctx, int(offset)))
 
+    def set_contact_global(self, glob: Model, local_node_global: np.ndarray, rank_elem_off: np.ndarray,
+                           glob_diag_M: np.ndarray | None = None):
+        """Multi-GPU contact (hakai_set_contact_global): this rank mirrors the contact model of the
+        global mesh `glob` (its contact_flag, instances, *Contact Pair surfaces and constants).
+        Call after comm_init[_local], set_element_offset and set_interface."""
+        if glob_diag_M is None:
+            glob_diag_M, _ = glob.lumped_mass()
+        diag = np.ascontiguousarray(glob_diag_M, np.float64)
+        inst = glob.element_instance
+        inst = np.ones(glob.nElement, np.int64) if inst is None else np.ascontiguousarray(inst, np.int64)
+        ncp, cpi, cpo, cpe = glob.c_contact_pairs()
+        l2g = np.ascontiguousarray(local_node_global, np.int64)
+        off = np.ascontiguousarray(rank_elem_off, np.int64)
+        check(self.L.hakai_set_contact_global(self.ctx, int(glob.contact_flag), glob.nNode, ptr(glob.coordmat),
+                                              glob.nElement, ptr(glob.elementmat, I64),
+                                              ptr(glob.element_material, I64), ptr(inst, I64), ptr(diag),
+                                              ptr(l2g, I64), ptr(off, I64), ncp, ptr(cpi, ctypes.c_int32),
+                                              ptr(cpo, I64), ptr(cpe, I64)))
+        if glob.contact_flag >= 1 and getattr(glob, "contact_params", None) is not None:
+            check(self.L.hakai_set_contact_params(self.ctx, *[float(x) for x in glob.contact_params]))
+
     def set_interface(self, local_node: np.ndarray, rank_lo: np.ndarray, rank_hi: np.ndarray):
         ln = np.ascontiguousarray(local_node, np.int64)
         lo = np.ascontiguousarray(rank_lo, np.int32)

@@ -171,6 +171,20 @@ int hakai_set_contact(hakai_ctx* ctx, int32_t contact_flag, const int64_t* eleme
  * (instance-local, 1-based). n_cp = 0 is the all-exterior case of hakai_set_contact. */
 int hakai_set_contact_cp(hakai_ctx* ctx, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
                          const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems);
+/* Multi-GPU contact (same reference seams as hakai_set_contact_cp). Call on every
+ * rank after hakai_comm_init[_local], hakai_set_element_offset and hakai_set_interface, with the
+ * GLOBAL model (the arrays of hakai_upload_model / hakai_set_contact_cp for the whole mesh, and
+ * its global diag_M), local_node_global[l] = global 1-based id of this rank's local node l, and
+ * rank_elem_off[0..nranks] = the ranks' contiguous global element ranges (0-based, rank r holds
+ * [rank_elem_off[r], rank_elem_off[r+1])). Every rank then mirrors the global contact model and
+ * all-gathers, each step, the displacements of the contact nodes and the deletion steps of the
+ * contact elements; the contact force is bit-identical to one GPU. hakai_set_contact[_cp] on a
+ * rank with a communicator returns HAKAI_ERR_STATE. */
+int hakai_set_contact_global(hakai_ctx* ctx, int32_t contact_flag, int64_t nNode, const double* coordmat,
+                             int64_t nElement, const int64_t* elementmat, const int64_t* element_material,
+                             const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
+                             const int64_t* rank_elem_off, int32_t n_cp, const int32_t* cp_instance,
+                             const int64_t* cp_elem_off, const int64_t* cp_elems);
 /* The constants hard-coded at v2/HAKAI_j.jl:2255-2259 (defaults myu 0.25, kc_o 1, kc_s 1,
  * Cr_o 0, Cr_s 0). BASELINE's C4 runs frictionless: myu = 0. */
 int hakai_set_contact_params(hakai_ctx* ctx, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s);

@@ -135,3 +135,36 @@ def test_partition_ranges():
     assert dist.partition_ranges(10, 3) == [(0, 4), (4, 7), (7, 10)]
     with pytest.raises(ValueError):
         dist.slab_partition(fast_deletion_bar(NX, NY, 4), 1, 3, NX, NY)
+
+
+def test_range_partition_two_body():
+    """General-mesh partition (contact models): contiguous element ranges, nodes renumbered in
+    global order, the global lumped mass restricted, IC/BC dofs mapped, adjacent-rank sharing."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3))
+    gdiag, _ = glob.lumped_mass()
+    for world in (1, 2, 3):
+        parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
+        assert sum(p[0].nElement for p in parts) == glob.nElement
+        ups, dns = {}, {}
+        for r, (loc, diag, (ln, lo, hi), l2g, off) in enumerate(parts):
+            assert off[0] == 0 and off[-1] == glob.nElement and loc.global_element_offset == off[r]
+            assert np.array_equal(l2g[loc.elementmat - 1], glob.elementmat[off[r]:off[r + 1]])
+            assert np.array_equal(loc.coordmat, glob.coordmat[l2g - 1])
+            assert np.array_equal(diag, gdiag.reshape(-1, 3)[l2g - 1].ravel())
+            assert np.all(hi == lo + 1) and np.all((lo == r) | (hi == r))
+            assert np.all(np.diff(l2g[ln]) > 0)
+            ups[r], dns[r] = l2g[ln[lo == r]], l2g[ln[hi == r]]
+            held = set(l2g.tolist())
+            gic = {(int(d), float(v)) for d, v in zip(glob.ic_dofs, glob.ic_values) if (d - 1) // 3 + 1 in held}
+            lic = {(int(3 * (l2g[(d - 1) // 3] - 1) + (d - 1) % 3 + 1), float(v))
+                   for d, v in zip(loc.ic_dofs, loc.ic_values)}
+            assert gic == lic
+            gbc = {int(d) for g in glob.bc for dd, _ in g.entries for d in dd if (d - 1) // 3 + 1 in held}
+            lbc = {int(3 * (l2g[(d - 1) // 3] - 1) + (d - 1) % 3 + 1) for g in loc.bc for dd, _ in g.entries
+                   for d in dd}
+            assert gbc == lbc
+        for r in range(world - 1):  # the two sides of a cut list the same nodes in the same order
+            assert np.array_equal(ups[r], dns[r + 1])
+    with pytest.raises(ValueError):  # a cut that makes ranks 0 and 2 share nodes
+        dist.range_partition(mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 3)), 0, 3)

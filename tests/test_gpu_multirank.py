@@ -72,3 +72,86 @@ def test_local_group_rejects_multi_step_calls():
         svs[0].step(1, 5)
     for sv in svs:
         sv.close()
+
+
+def _run_contact_group(glob, world, n_steps, key):
+    """Range-partitioned contact model on an in-process group, each rank mirroring the global
+    contact model (hakai_set_contact_global)."""
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, world, key)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        svs.append(sv)
+    step_group(svs, 1, n_steps)
+    out = [(loc, l2g, sv.download(), [tuple(x) for x in sv.deleted()], sv.contact_stats())
+           for sv, (loc, _, _, l2g, _) in zip(svs, parts)]
+    for sv in svs:
+        sv.close()
+    return out
+
+
+def _assert_group_equals_single(glob, parts, g, gdel):
+    dels = sorted(d for _, _, _, dl, _ in parts for d in dl)
+    assert dels == gdel
+    for loc, l2g, st, _, _ in parts:
+        n = l2g - 1
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[n])
+        assert np.array_equal(st.disp_pre.reshape(-1, 3), g.disp_pre.reshape(-1, 3)[n])
+        e0, el = loc.global_element_offset, loc.nElement
+        gp = slice(8 * e0, 8 * (e0 + el))
+        assert np.array_equal(st.integ_stress, g.integ_stress[gp])
+        assert np.array_equal(st.integ_eq_plastic_strain, g.integ_eq_plastic_strain[gp])
+        assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_contact_group_bitexact_with_deletion(world):
+    """Multi-GPU contact: contact-driven deletion with the surface update, the
+    impactor and the plate split over ranks; every rank's displacements, stresses and the
+    deletion log equal the single-context run bit for bit."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+        gst = sv.contact_stats()
+    assert len(gdel) >= 4
+    parts = _run_contact_group(glob, world, glob.n_steps, key=300 + world)
+    _assert_group_equals_single(glob, parts, g, gdel)
+    for *_, st in parts:  # every rank ran the whole (replicated) contact search
+        assert st["live_triangles"] == gst["live_triangles"] and st["events"] == gst["events"]
+
+
+@pytest.mark.parametrize("flag,myu,surfaces", [(1, None, False), (2, 0.0, False), (1, None, True)])
+def test_contact_group_bitexact_variants(flag, myu, surfaces):
+    """Friction (reference myu 0.25), self-contact, *Contact Pair surfaces on 2 ranks."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 3), v=-1e5, perturb=0.02, seed=1, myu=myu,
+                               contact_flag=flag, surfaces=surfaces, n_steps=300)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+    parts = _run_contact_group(glob, 2, glob.n_steps, key=400 + 10 * flag + int(surfaces))
+    _assert_group_equals_single(glob, parts, g, gdel)
+    assert np.max(np.abs(g.disp)) > 0
+
+
+def test_contact_on_communicator_requires_global_model():
+    from hakai import mesh
+    from hakai._abi import HakaiError, ptr
+    glob = mesh.two_body_model(plate=(4, 4, 1), impactor=(2, 2, 2))
+    loc, diag, iface, l2g, off = dist.range_partition(glob, 0, 2)
+    with Solver(loc, diag_M=diag) as sv:
+        sv.comm_init_local(0, 2, 999)
+        inst = np.ones(loc.nElement, np.int64)
+        with pytest.raises(HakaiError):
+            from hakai._abi import check
+            import ctypes
+            check(sv.L.hakai_set_contact(sv.ctx, 1, ptr(inst, ctypes.c_int64)))
