@@ -8,6 +8,7 @@
 // *Boundary append every match while *Initial Conditions take the first; ENCASTRE fixes the 3 dofs;
 // directions > 3 are ignored; a BC block ends at "**" or the next "*Boundary".
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -57,19 +58,30 @@ std::vector<std::string> split(const std::string& s, char d, bool keepempty) {
 
 bool has(const std::string& s, const char* pat) { return s.find(pat) != std::string::npos; }
 
-double parse_f(const std::string& s) {
-    if (s.empty()) throw ParseError{"parse(Float64, \"\")"};
+// Julia's parse(Float64 / Int, s) accepts leading and trailing whitespace (tabs in decks written
+// by spreadsheets, e.g. HAKAI-v0.0.1/input/projectile-impact-d1mm.inp *Plastic rows)
+static std::string trim_ws(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) ++a;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) --b;
+    return s.substr(a, b - a);
+}
+
+double parse_f(const std::string& s0) {
+    const std::string s = trim_ws(s0);
+    if (s.empty()) throw ParseError{"parse(Float64, \"" + s0 + "\")"};
     char* end = nullptr;
     const double v = std::strtod(s.c_str(), &end);
-    if (end != s.c_str() + s.size()) throw ParseError{"parse(Float64, \"" + s + "\")"};
+    if (end != s.c_str() + s.size()) throw ParseError{"parse(Float64, \"" + s0 + "\")"};
     return v;
 }
 
-long long parse_i(const std::string& s) {
-    if (s.empty()) throw ParseError{"parse(Int, \"\")"};
+long long parse_i(const std::string& s0) {
+    const std::string s = trim_ws(s0);
+    if (s.empty()) throw ParseError{"parse(Int, \"" + s0 + "\")"};
     char* end = nullptr;
     const long long v = std::strtoll(s.c_str(), &end, 10);
-    if (end != s.c_str() + s.size()) throw ParseError{"parse(Int, \"" + s + "\")"};
+    if (end != s.c_str() + s.size()) throw ParseError{"parse(Int, \"" + s0 + "\")"};
     return v;
 }
 

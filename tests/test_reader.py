@@ -69,8 +69,10 @@ def _py_nodes_elems(path):
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_DIR), reason="reference decks not present")
-@pytest.mark.parametrize("deck", ["car-crash-N2k.inp", "car-wall-N2k.inp"])
+@pytest.mark.parametrize("deck", ["car-crash-N2k.inp", "car-wall-N2k.inp", "carx2-crash-N43k.inp",
+                                  "../../HAKAI-v0.0.1/input/projectile-impact-d1mm.inp"])
 def test_multi_instance_decks(deck):
+    """Multi-instance decks: translations and rotations of *Instance (v2/readInpFile_j.jl:566-620)."""
     path = os.path.join(REF_DIR, deck)
     m = hakai.read_inp(path)
     parts, insts = _py_nodes_elems(path)
@@ -82,13 +84,21 @@ def test_multi_instance_decks(deck):
             s = [x for x in t.split(",") if x]
             if len(s) == 3:
                 c = c + np.array([float(x) for x in s])
+            elif len(s) == 7:  # rotation about the axis (p1 -> p2) by s[6] degrees (readInpFile_j.jl:590-604)
+                v = [float(x) for x in s]
+                n = np.array(v[3:6]) - np.array(v[0:3])
+                n = n / np.linalg.norm(n)
+                d = v[6] / 180.0 * np.pi
+                K = np.array([[0, -n[2], n[1]], [n[2], 0, -n[0]], [-n[1], n[0], 0]])
+                T = np.cos(d) * np.eye(3) + (1 - np.cos(d)) * np.outer(n, n) + np.sin(d) * K
+                c = c @ T.T
         coords.append(c)
         elems.append(e + off)
         off += c.shape[0]
     assert np.allclose(m.coordmat, np.vstack(coords), rtol=0, atol=1e-9)
     assert np.array_equal(m.elementmat, np.vstack(elems))
     assert m.contact_flag >= 1
-    assert m.mass_scaling == 100.0
+    assert m.mass_scaling == {"carx2-crash-N43k.inp": 60.0, "../../HAKAI-v0.0.1/input/projectile-impact-d1mm.inp": 1.0}.get(deck, 100.0)
     assert len(m.ic_dofs) > 0 and np.all(m.ic_dofs >= 1)
     diag, vol = m.lumped_mass()
     assert np.all(diag > 0)
@@ -130,3 +140,17 @@ def test_written_decks_round_trip(tmp_path, which):
     for p, q in zip(a.contact_pairs or [], m.contact_pairs or []):
         for (ia, ea), (ib, eb) in zip(p, q):
             assert ia == ib and np.array_equal(ea, eb)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DIR), reason="reference decks not present")
+def test_every_reference_deck_parses():
+    """readInpFile on every deck the reference ships (v0.0.0-v0.0.2): sizes, positive lumped mass."""
+    import glob
+    decks = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(REF_DIR)), "..", "**", "*.inp"),
+                             recursive=True))
+    assert len(decks) >= 20
+    for d in decks:
+        m = hakai.read_inp(d)
+        assert m.nNode > 0 and m.nElement > 0 and m.elementmat.min() >= 1 and m.elementmat.max() <= m.nNode
+        diag, _ = m.lumped_mass()
+        assert np.all(diag > 0), d
