@@ -154,3 +154,22 @@ def test_every_reference_deck_parses():
         assert m.nNode > 0 and m.nElement > 0 and m.elementmat.min() >= 1 and m.elementmat.max() <= m.nNode
         diag, _ = m.lumped_mass()
         assert np.all(diag > 0), d
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DIR), reason="reference decks not present")
+def test_deck_fixtures_round_trip():
+    """tests/golden/deck_*.npz hold exactly what readInpFile makes of the shipped decks."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+    from deck_fixtures import model_from_arrays, model_to_arrays
+    from make_deck_golden import DECKS, REF
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    for deck, steps in DECKS:
+        name = os.path.splitext(os.path.basename(deck))[0].replace("-", "_")
+        z = np.load(os.path.join(gold, f"deck_{name}.npz"))
+        assert int(z["steps"]) == steps
+        a = model_to_arrays(hakai.read_inp(os.path.join(REF, deck)))
+        for k, v in a.items():
+            assert np.array_equal(np.asarray(v), z[k]), (deck, k)
+        b = model_to_arrays(model_from_arrays(z))
+        assert sorted(b) == sorted(a)
