@@ -20,7 +20,12 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--preload", type=int, default=30, help="steps before timing (contact starts at ~10)")
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--ranks", type=int, default=1,
+                    help=">1: range-partitioned in-process group on this one GPU (multi-GPU contact mirror; "
+                         "measures the per-rank contact cost incl. the all-gather, not scaling)")
     a = ap.parse_args()
+    if a.ranks > 1:
+        return group(a)
     import numpy as np
     from hakai import mesh
     from hakai._abi import K_BC, K_CONTACT, K_ELEMENT, K_NODAL
@@ -61,6 +66,49 @@ def main():
         "setup_s": {"mesh": round(t1 - t0, 2), "upload_contact_setup": round(t2 - t1, 2)},
     }
     sv.close()
+    print(json.dumps(out), flush=True)
+
+
+def group(a):
+    import numpy as np
+    from hakai import dist, mesh
+    from hakai._abi import K_BC, K_CONTACT, K_ELEMENT, K_EXCHANGE, K_NODAL
+    from hakai.solver import Solver, step_group
+    m = mesh.config_c4(a.scale)
+    gdiag, _ = m.lumped_mass()
+    parts = [dist.range_partition(m, r, a.ranks, gdiag) for r in range(a.ranks)]
+    svs = []
+    t0 = time.time()
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, a.ranks, 4242)
+        sv.set_interface(*iface)
+        sv.set_contact_global(m, l2g, off, gdiag)
+        svs.append(sv)
+    t1 = time.time()
+    step_group(svs, 1, a.preload)
+    for sv in svs:
+        sv.sync()
+        sv.profile(True)
+    ts = time.perf_counter()
+    step_group(svs, 1 + a.preload, a.steps)
+    for sv in svs:
+        sv.sync()
+    el = time.perf_counter() - ts
+    ranks = []
+    for sv, (loc, *_) in zip(svs, parts):
+        k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
+                                                (K_CONTACT, "contact"), (K_EXCHANGE, "exchange"))}
+        ranks.append({"elements": loc.nElement, "nodes": loc.nNode,
+                      "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
+                      "contact_stats_last_step": sv.contact_stats()})
+    out = {"workload": f"C4 two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group)",
+           "elements": m.nElement, "steps": a.steps, "preload": a.preload,
+           "group_ms_per_step_all_ranks": round(el / a.steps * 1e3, 4), "setup_s": round(t1 - t0, 2),
+           "ranks": ranks}
+    for sv in svs:
+        sv.close()
     print(json.dumps(out), flush=True)
 
 
