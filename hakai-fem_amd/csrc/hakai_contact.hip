@@ -60,6 +60,12 @@ struct PairParam {
 // copies in an in-process group) and scattered into the mirror. The block of step s is packed at
 // the end of step s-1 (or at the state reset, s = 0), so an in-process group stepped rank by rank
 // finds every peer's block ready. Contact work is replicated, not divided.
+// Two node sets travel: X0, the nodes of the entries live from the start (every step, owner
+// packs), and X1, the nodes only a deletion exposes. An X1 node is shipped by every rank that
+// deleted one of its adders (the adder contains the node, so that rank holds it), from the step
+// after that deletion on, together with its u_pre; X1 nodes travel in chunks of 64 (rank segment,
+// ascending global id), and a chunk is sent once any of its nodes is. Sender and receivers mark
+// chunks from the same deletion steps, so both sides agree on the slot order.
 struct Mirror {
     int rank = 0, nranks = 1;
     int maxx = 0, maxe = 0;           // block capacity: owned contact nodes, contact elements per rank
@@ -82,6 +88,21 @@ struct Mirror {
     // block layout (bytes): header (last deletion step), u, deletion steps; at s = 0 also u_pre, velo0
     size_t off_u = 16, off_del = 0, off_upre = 0, off_v0 = 0, blk_step = 0, blk_full = 0;
     long long seq = 0;                // step index since the last state reset (the block a step consumes)
+    // X1: entries j = (rank segment q, node), chunks of 64 entries inside a segment
+    int nx1 = 0, nchunk = 0, capc = 0;    // entries, chunks (all ranks), block capacity in chunks
+    int* d_seg_chunk = nullptr;       // [nranks+1] first chunk of each rank's segment
+    int* d_chunk_first = nullptr;     // [nchunk] first entry
+    int* d_chunk_end = nullptr;       // [nchunk] one past the last entry
+    int* d_x1_gid = nullptr;          // [nx1] global node
+    int* d_x1_loc = nullptr;          // [nx1] local node of this rank's entries, else -1
+    int* d_x1_chunk = nullptr;        // [nx1] chunk of each entry
+    int *d_el2x_ptr = nullptr, *d_el2x = nullptr;  // global element -> X1 entries it is an adder of
+    int* d_chunk_flag = nullptr;      // [nchunk] 1 once the chunk travels
+    int* d_slot_chunk = nullptr;      // [nranks*capc] chunk of each block slot
+    int* d_counts = nullptr;          // [nranks] chunks each rank sends
+    int* d_x1ctl = nullptr;           // [4] new marks since the last slot scan, max chunks needed, -, -
+    int* d_last_del = nullptr;        // [neo] deletion step of own contact elements at the last pack
+    size_t off_x1 = 0, off_x1v0 = 0;  // X1 region (u, u_pre per slot entry); at s = 0 also velo0
 };
 
 struct Contact {
@@ -972,11 +993,25 @@ struct MirLayout {
     size_t off_u, off_del, off_upre, off_v0;
 };
 
+struct X1Map {
+    const int *el2x_ptr, *el2x, *x1_chunk;
+    int* chunk_flag;
+    int* x1ctl;
+};
+
+// a deleted element's X1 entries: their chunks travel from now on
+__device__ __forceinline__ void x1_mark(const X1Map& X, int e) {
+    const int a0 = X.el2x_ptr[e], a1 = X.el2x_ptr[e + 1];
+    for (int a = a0; a < a1; ++a) X.chunk_flag[X.x1_chunk[X.el2x[a]]] = 1;
+    if (a1 > a0) X.x1ctl[0] = 1;
+}
+
 // this rank's block: last deletion step, u of the owned contact nodes, deletion step of its contact
-// elements; with `full` also u_pre and the velocity before the first step
+// elements; with `full` also u_pre and the velocity before the first step. Own deletions since the
+// last pack mark their X1 chunks.
 __global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const double* u, const double* upre,
                            const double* velo0, const int* del_step, const int* del_any, char* blk, MirLayout L,
-                           int full) {
+                           int full, int* last_del, int elem_off, X1Map X) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) reinterpret_cast<int*>(blk)[0] = *del_any;
     if (i < nxo) {
@@ -992,13 +1027,18 @@ __global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const
             }
         }
     }
-    if (i < neo) reinterpret_cast<int*>(blk + L.off_del)[i] = del_step[eo[i]];
+    if (i < neo) {
+        const int d = del_step[eo[i]];
+        reinterpret_cast<int*>(blk + L.off_del)[i] = d;
+        if (d != 0 && last_del[i] == 0) x1_mark(X, eo[i] + elem_off);
+        last_del[i] = d;
+    }
 }
 
 // all ranks' blocks -> the mirror. Slots are disjoint (one owner per node, one rank per element).
 __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx, int maxe, const int* xg,
                              const int* eg, MirLayout L, int full, double* gu, double* gupre, double* gvelo0,
-                             int* gdel, int* gflag, long long nE) {
+                             int* gdel, int* gflag, long long nE, X1Map X) {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i < (long long)nranks * maxx) {
         const int g = xg[i];
@@ -1022,6 +1062,7 @@ __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx,
         if (e >= 0) {
             const int q = (int)(i / maxe), k = (int)(i % maxe);
             const int d = reinterpret_cast<const int*>(recv + (size_t)q * blk + L.off_del)[k];
+            if (d != 0 && gdel[e] == 0) x1_mark(X, e);
             gdel[e] = d;
             gflag[e] = d == 0 ? 1 : 0;
         }
@@ -1030,6 +1071,88 @@ __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx,
         int mx = 0;
         for (int q = 0; q < nranks; ++q) mx = max(mx, reinterpret_cast<const int*>(recv + (size_t)q * blk)[0]);
         gdel[nE + 1] = mx;
+    }
+}
+
+// X1 slots: the marked chunks of ranks q0..q1-1 in ascending chunk order (one block; skipped when
+// nothing was marked since the last scan). counts[q] = chunks rank q sends; more than capc is an
+// overflow, recorded in x1ctl[1] and reported by contact_check.
+__global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* seg_chunk, const int* chunk_flag,
+                                                   int* slot_chunk, int capc, int* counts, int* x1ctl) {
+    if (x1ctl[0] == 0) return;
+    __shared__ int s_w[1024 / 64];
+    for (int q = q0; q < q1; ++q) {
+        const int c0 = seg_chunk[q], c1 = seg_chunk[q + 1];
+        int carry = 0;
+        for (int b = c0; b < c1; b += (int)blockDim.x) {
+            const int c = b + (int)threadIdx.x;
+            const int f = c < c1 ? chunk_flag[c] : 0;
+            int tot;
+            const int slot = carry + block_excl_scan(f, s_w, tot);
+            if (f && slot < capc) slot_chunk[(long long)q * capc + slot] = c;
+            carry += tot;
+        }
+        if (threadIdx.x == 0) {
+            counts[q] = carry;
+            x1ctl[1] = max(x1ctl[1], carry);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) x1ctl[0] = 0;
+}
+
+struct X1Slots {
+    const int *counts, *slot_chunk, *chunk_first, *chunk_end;
+    int capc;
+};
+
+__device__ __forceinline__ int x1_entry(const X1Slots& S, int q, long long i, int& slot) {
+    slot = (int)(i >> 6);
+    if (slot >= min(S.counts[q], S.capc)) return -1;
+    const int c = S.slot_chunk[(long long)q * S.capc + slot];
+    const int j = S.chunk_first[c] + (int)(i & 63);
+    return j < S.chunk_end[c] ? j : -1;
+}
+
+// this rank's X1 slots: u and u_pre (and velo0 at s = 0) of every node of its marked chunks
+__global__ void k_x1_pack(int rank, X1Slots S, const int* x1_loc, const double* u, const double* upre,
+                          const double* velo0, char* blk, size_t off_x1, size_t off_x1v0, int full) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    int slot;
+    const int j = x1_entry(S, rank, i, slot);
+    if (j < 0) return;
+    const long long n = x1_loc[j];
+    const long long o = 64LL * slot + (i & 63);
+    double* p = reinterpret_cast<double*>(blk + off_x1) + 6 * o;
+    for (int c = 0; c < 3; ++c) {
+        p[c] = u[3 * n + c];
+        p[3 + c] = upre[3 * n + c];
+    }
+    if (full) {
+        double* v = reinterpret_cast<double*>(blk + off_x1v0) + 3 * o;
+        for (int c = 0; c < 3; ++c) v[c] = velo0 ? velo0[3 * n + c] : 0.0;
+    }
+}
+
+__global__ void k_x1_unpack(const char* recv, size_t blk, int nranks, X1Slots S, const int* x1_gid, size_t off_x1,
+                            size_t off_x1v0, int full, double* gu, double* gupre, double* gvelo0) {
+    const long long per = 64LL * S.capc;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= per * nranks) return;
+    const int q = (int)(i / per);
+    int slot;
+    const int j = x1_entry(S, q, i % per, slot);
+    if (j < 0) return;
+    const long long g = x1_gid[j];
+    const long long o = 64LL * slot + (i & 63);
+    const double* p = reinterpret_cast<const double*>(recv + (size_t)q * blk + off_x1) + 6 * o;
+    for (int c = 0; c < 3; ++c) {
+        gu[3 * g + c] = p[c];
+        gupre[3 * g + c] = p[3 + c];
+    }
+    if (full) {
+        const double* v = reinterpret_cast<const double*>(recv + (size_t)q * blk + off_x1v0) + 3 * o;
+        for (int c = 0; c < 3; ++c) gvelo0[3 * g + c] = v[c];
     }
 }
 
@@ -1221,11 +1344,31 @@ void contact_destroy(hakai_ctx* c) {
         dfree(M->g_coord); dfree(M->g_mass); dfree(M->g_conn); dfree(M->g_u[0]); dfree(M->g_u[1]);
         dfree(M->g_flag); dfree(M->g_del); dfree(M->g_fext); dfree(M->d_velo0_loc);
         dfree(M->d_send[0]); dfree(M->d_send[1]); dfree(M->d_recv);
+        dfree(M->d_seg_chunk); dfree(M->d_chunk_first); dfree(M->d_chunk_end); dfree(M->d_x1_gid); dfree(M->d_x1_loc);
+        dfree(M->d_x1_chunk); dfree(M->d_el2x_ptr); dfree(M->d_el2x); dfree(M->d_chunk_flag); dfree(M->d_slot_chunk);
+        dfree(M->d_counts); dfree(M->d_x1ctl); dfree(M->d_last_del);
         delete M;
     }
     delete C;
     c->contact = nullptr;
     dfree(c->d_fext);
+}
+
+static X1Map x1map(Mirror* M) { return X1Map{M->d_el2x_ptr, M->d_el2x, M->d_x1_chunk, M->d_chunk_flag, M->d_x1ctl}; }
+static X1Slots x1slots(Mirror* M) {
+    return X1Slots{M->d_counts, M->d_slot_chunk, M->d_chunk_first, M->d_chunk_end, M->capc};
+}
+
+// block layout from the capacities (bytes, 8-byte aligned regions)
+static void mir_layout(Mirror* M) {
+    M->off_u = 16;
+    M->off_del = M->off_u + 24 * (size_t)M->maxx;
+    M->off_x1 = M->off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
+    M->blk_step = M->off_x1 + 48 * 64 * (size_t)M->capc;
+    M->off_upre = M->blk_step;
+    M->off_v0 = M->off_upre + 24 * (size_t)M->maxx;
+    M->off_x1v0 = M->off_v0 + 24 * (size_t)M->maxx;
+    M->blk_full = M->off_x1v0 + 24 * 64 * (size_t)M->capc;
 }
 
 // multi-GPU: pack this rank's mirror block for step M->seq (full = with u_pre and velo0)
@@ -1235,11 +1378,37 @@ static int mir_pack(hakai_ctx* c, bool full) {
     const int par = (int)(M->seq & 1);
     const int n = std::max(std::max(M->nxo, M->neo), 1);
     const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
+    const double* velo0 = C->use_velo0 ? M->d_velo0_loc : nullptr;
     hipLaunchKernelGGL(k_mir_pack, dim3((n + kB - 1) / kB), dim3(kB), 0, c->stream, M->d_xo, M->nxo, M->d_eo, M->neo,
-                       c->d_u[c->cur], c->d_u[1 - c->cur], C->use_velo0 ? M->d_velo0_loc : nullptr, c->d_del_step,
-                       c->d_del_step + c->nEp + 1, M->d_send[par], L, full ? 1 : 0);
+                       c->d_u[c->cur], c->d_u[1 - c->cur], velo0, c->d_del_step, c->d_del_step + c->nEp + 1,
+                       M->d_send[par], L, full ? 1 : 0, M->d_last_del, (int)c->elem_offset, x1map(M));
+    if (M->nchunk > 0)  // also with capc = 0: the counts are what the overflow check reads
+        hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, c->stream, M->rank, M->rank + 1, M->d_seg_chunk,
+                           M->d_chunk_flag, M->d_slot_chunk, M->capc, M->d_counts, M->d_x1ctl);
+    if (M->nchunk > 0 && M->capc > 0) {
+        const long long nt = 64LL * M->capc;
+        hipLaunchKernelGGL(k_x1_pack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, c->stream, M->rank,
+                           x1slots(M), M->d_x1_loc, c->d_u[c->cur], c->d_u[1 - c->cur], velo0, M->d_send[par],
+                           M->off_x1, M->off_x1v0, full ? 1 : 0);
+    }
     HIPCHK(hipGetLastError());
     return comm_gather_mark(c, par);
+}
+
+// forget all deletions (state reset / upload): the next block is a full one
+static int mir_reset(hakai_ctx* c) {
+    Contact* C = c->contact;
+    Mirror* M = C->mir;
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)C->nE + 2) * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(M->d_last_del, 0, std::max(M->neo, 1) * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(M->d_chunk_flag, 0, std::max(M->nchunk, 1) * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(M->d_counts, 0, M->nranks * sizeof(int), s));
+    const int ctl[4] = {1, 0, 0, 0};  // slots stale
+    HIPCHK(hipMemcpyAsync(M->d_x1ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    M->seq = 0;
+    return 0;
 }
 
 int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
@@ -1251,7 +1420,7 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
         if (velo0_host)
             HIPCHK(hipMemcpyAsync(M->d_velo0_loc, velo0_host, 3 * (size_t)c->nN * sizeof(double),
                                   hipMemcpyHostToDevice, c->stream));
-        M->seq = 0;
+        if (int rc = mir_reset(c)) return rc;
         return mir_pack(c, true);
     }
     if (velo0_host)
@@ -1285,7 +1454,16 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
         hipLaunchKernelGGL(k_mir_unpack, dim3((unsigned)((nslot + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
                            M->nranks, M->maxx, M->maxe, M->d_xg, M->d_eg, L, full ? 1 : 0, M->g_u[par],
-                           M->g_u[1 - par], C->d_velo0, M->g_del, M->g_flag, C->nE);
+                           M->g_u[1 - par], C->d_velo0, M->g_del, M->g_flag, C->nE, x1map(M));
+        if (M->nchunk > 0)
+            hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, s, 0, M->nranks, M->d_seg_chunk, M->d_chunk_flag,
+                               M->d_slot_chunk, M->capc, M->d_counts, M->d_x1ctl);
+        if (M->nchunk > 0 && M->capc > 0) {
+            const long long nt = 64LL * M->capc * M->nranks;
+            hipLaunchKernelGGL(k_x1_unpack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
+                               M->nranks, x1slots(M), M->d_x1_gid, M->off_x1, M->off_x1v0, full ? 1 : 0, M->g_u[par],
+                               M->g_u[1 - par], C->d_velo0);
+        }
         in.coord = M->g_coord;
         in.u = M->g_u[par];
         in.u_pre = M->g_u[1 - par];
@@ -1394,6 +1572,32 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, sizeof(unsigned int), c->stream));
         return 0;
     }
+    if (!std::strcmp(key, "contact_mirror_chunks")) {  // multi-GPU: block capacity for exposed-node chunks
+        Mirror* M = C->mir;
+        if (!M) return fail(HAKAI_ERR_STATE, "contact_mirror_chunks without hakai_set_contact_global");
+        if (value < 0 || value > (1LL << 24)) return fail(HAKAI_ERR_ARG, "contact_mirror_chunks out of range");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        M->capc = (int)std::min<long long>(value, M->nchunk);
+        mir_layout(M);
+        for (int p = 0; p < 2; ++p) {
+            dfree(M->d_send[p]);
+            HIPCHK(dalloc(&M->d_send[p], M->blk_full));
+        }
+        dfree(M->d_recv);
+        HIPCHK(dalloc(&M->d_recv, (size_t)M->nranks * M->blk_full));
+        dfree(M->d_slot_chunk);
+        HIPCHK(dalloc(&M->d_slot_chunk, (size_t)M->nranks * std::max(M->capc, 1)));
+        if (int rc = comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
+        // the next block again, in the new layout; every slot table is rebuilt at the next unpack
+        const int ctl[2] = {1, 0};
+        HIPCHK(hipMemcpy(M->d_x1ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice));
+        if (c->state_ok) {
+            if (int rc = mir_pack(c, M->seq == 0)) return rc;
+            HIPCHK(hipMemcpyAsync(M->d_x1ctl, ctl, sizeof(int), hipMemcpyHostToDevice, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return 0;
+    }
     if (!std::strcmp(key, "contact_full_rebuild")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_full_rebuild must be 0 or 1");
         C->always_rebuild = value != 0;
@@ -1440,6 +1644,13 @@ int contact_check(hakai_ctx* c) {
     if ((long long)mc > C->cand_cap)
         return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step exceed the buffer (%lld); raise "
                     "hakai_set_tuning(\"contact_candidate_cap\")", mc, C->cand_cap);
+    if (Mirror* M = C->mir) {
+        int x1[4];
+        HIPCHK(hipMemcpy(x1, M->d_x1ctl, sizeof(x1), hipMemcpyDeviceToHost));
+        if (x1[1] > M->capc)
+            return fail(HAKAI_ERR_STATE, "contact mirror: a rank must send %d chunks of exposed contact nodes, the "
+                        "block holds %d; raise hakai_set_tuning(\"contact_mirror_chunks\") on every rank", x1[1], M->capc);
+    }
     unsigned int ms = 0;
     HIPCHK(hipMemcpy(&ms, C->d_ctl + kEvShardMax, sizeof(unsigned int), hipMemcpyDeviceToHost));
     if ((long long)ms > C->cap / kEvShards)
@@ -1461,7 +1672,9 @@ struct HostMesh {
 };
 // multi-GPU: the nodes and elements the contact kernels can ever read
 struct SetupOut {
-    std::vector<char> xmask, emask;
+    std::vector<char> x0mask;                     // nodes of the initially live entries
+    std::vector<std::pair<int, int>> x1;          // (node, adder element) of the entries a deletion exposes
+    std::vector<char> emask;                      // adders and triangle owners
 };
 
 // builds c->contact on mesh H (the surfaces, pairs and entry lists of hakai_set_contact_cp);
@@ -1729,11 +1942,23 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         invert(taptr, tadd, C->n_tri, el_tri_ptr, el_tri);
     }
     if (out) {  // every node / element an entry refers to (positions, masses, adders, triangle owners)
-        out->xmask.assign((size_t)H.nN, 0);
+        out->x0mask.assign((size_t)H.nN, 0);
         out->emask.assign((size_t)H.nE, 0);
-        for (int n : ni_node) out->xmask[n] = 1;
-        for (int n : nj_node) out->xmask[n] = 1;
-        for (int n : tri_nodes) out->xmask[n] = 1;
+        out->x1.clear();
+        auto nodes_of = [&](const std::vector<int>& node, const std::vector<int>& orig, const std::vector<int>& aptr,
+                            const std::vector<int>& add) {
+            for (size_t k = 0; k < node.size(); ++k) {
+                if (orig[k]) out->x0mask[node[k]] = 1;
+                for (int a = aptr[k]; a < aptr[k + 1]; ++a) out->x1.push_back({node[k], add[a]});
+            }
+        };
+        nodes_of(ni_node, ni_orig, ni_aptr, ni_add);
+        nodes_of(nj_node, nj_orig, nj_aptr, nj_add);
+        for (size_t j = 0; j < tri_adder.size(); ++j)
+            for (int q = 0; q < 3; ++q) {
+                if (tri_adder[j] < 0) out->x0mask[tri_nodes[3 * j + q]] = 1;
+                else out->x1.push_back({tri_nodes[3 * j + q], tri_adder[j]});
+            }
         for (int e : ni_add) out->emask[e] = 1;
         for (int e : nj_add) out->emask[e] = 1;
         for (int e : tri_ele) out->emask[e] = 1;
@@ -1842,7 +2067,7 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     };
     std::vector<std::vector<int>> xs((size_t)nr), es((size_t)nr);
     for (long long n = 0; n < nNode; ++n)
-        if (so.xmask[n] && minel[n] != INT32_MAX) xs[rank_of(minel[n])].push_back((int)n);
+        if (so.x0mask[n] && minel[n] != INT32_MAX) xs[rank_of(minel[n])].push_back((int)n);
     for (long long e = 0; e < nElement; ++e)
         if (so.emask[e]) es[rank_of(e)].push_back((int)e);
     for (int q = 0; q < nr; ++q) {
@@ -1861,12 +2086,72 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     for (int e : es[rank]) eo.push_back(e - (int)rank_elem_off[rank]);
     M->nxo = (int)xo.size();
     M->neo = (int)eo.size();
-    M->off_u = 16;
-    M->off_del = M->off_u + 24 * (size_t)M->maxx;
-    M->blk_step = M->off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
-    M->off_upre = M->blk_step;
-    M->off_v0 = M->off_upre + 24 * (size_t)M->maxx;
-    M->blk_full = M->off_v0 + 24 * (size_t)M->maxx;
+    // X1: per rank q the nodes outside X0 with an adder on q (ascending global id), in chunks of
+    // 64; el2x lists, per adder, the entries it makes travel. Triangle nodes exposed by a deletion
+    // are j-side node entries with the same adder, so the node entries' pairs cover them.
+    std::vector<int> pcnt((size_t)nNode + 1, 0);
+    for (const auto& pa : so.x1)
+        if (!so.x0mask[pa.first]) pcnt[pa.first + 1]++;
+    for (long long n = 0; n < nNode; ++n) pcnt[n + 1] += pcnt[n];
+    std::vector<int> padd((size_t)pcnt[nNode]);
+    {
+        std::vector<int> fill(pcnt.begin(), pcnt.end() - 1);
+        for (const auto& pa : so.x1)
+            if (!so.x0mask[pa.first]) padd[fill[pa.first]++] = pa.second;
+    }
+    std::vector<std::vector<int>> x1n((size_t)nr);                  // per rank: nodes
+    std::vector<std::vector<std::pair<int, int>>> x1a((size_t)nr);  // per rank: (adder, index in x1n[q])
+    for (long long n = 0; n < nNode; ++n) {
+        if (pcnt[n] == pcnt[n + 1]) continue;
+        std::sort(padd.begin() + pcnt[n], padd.begin() + pcnt[n + 1]);
+        int last_q = -1, last_a = -1;
+        for (int k = pcnt[n]; k < pcnt[n + 1]; ++k) {
+            const int a = padd[k];
+            if (a == last_a) continue;
+            last_a = a;
+            const int q = rank_of(a);  // adders ascend, so their ranks do too
+            if (q != last_q) x1n[q].push_back((int)n);
+            last_q = q;
+            x1a[q].push_back({a, (int)x1n[q].size() - 1});
+        }
+    }
+    std::vector<int> seg_chunk(1, 0), chunk_first, chunk_end, x1_gid, x1_loc, x1_chunk;
+    std::vector<int> el2x_ptr((size_t)nElement + 1, 0), el2x;
+    for (int q = 0; q < nr; ++q) {
+        const int e0 = (int)x1_gid.size(), m = (int)x1n[q].size();
+        for (int k = 0; k < m; k += 64) {
+            chunk_first.push_back(e0 + k);
+            chunk_end.push_back(e0 + std::min(m, k + 64));
+        }
+        seg_chunk.push_back((int)chunk_first.size());
+        for (int k = 0; k < m; ++k) {
+            const int n = x1n[q][k];
+            x1_gid.push_back(n);
+            x1_chunk.push_back(seg_chunk[q] + k / 64);
+            if (q == rank && g2l[n] < 0)
+                return fail(HAKAI_ERR_ARG, "set_contact_global: exposed contact node %d is not in the local model", n + 1);
+            x1_loc.push_back(q == rank ? g2l[n] : -1);
+        }
+        for (const auto& ai : x1a[q]) el2x_ptr[ai.first + 1]++;
+    }
+    for (long long e = 0; e < nElement; ++e) el2x_ptr[e + 1] += el2x_ptr[e];
+    el2x.resize((size_t)el2x_ptr[nElement]);
+    {
+        std::vector<int> fill(el2x_ptr.begin(), el2x_ptr.end() - 1);
+        int base = 0;
+        for (int q = 0; q < nr; ++q) {
+            for (const auto& ai : x1a[q]) el2x[fill[ai.first]++] = base + ai.second;
+            base += (int)x1n[q].size();
+        }
+    }
+    M->nx1 = (int)x1_gid.size();
+    M->nchunk = (int)chunk_first.size();
+    {
+        int mx = 0;
+        for (int q = 0; q < nr; ++q) mx = std::max(mx, seg_chunk[q + 1] - seg_chunk[q]);
+        M->capc = std::min(mx, std::max(32, (mx + 7) / 8));  // 1/8 of the largest segment; tuning raises it
+    }
+    mir_layout(M);
     std::vector<double> gmass((size_t)nNode);
     for (long long n = 0; n < nNode; ++n) gmass[n] = diag_M[3 * n];
     std::vector<int> ones((size_t)nElement, 1);
@@ -1891,6 +2176,19 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
     HIPCHK(dalloc(&M->g_fext, 3 * (size_t)nNode));
     HIPCHK(hipMemsetAsync(M->g_fext, 0, 3 * (size_t)nNode * sizeof(double), s));
+    HIPCHK(upload(&M->d_seg_chunk, seg_chunk, s));
+    HIPCHK(upload(&M->d_chunk_first, chunk_first, s));
+    HIPCHK(upload(&M->d_chunk_end, chunk_end, s));
+    HIPCHK(upload(&M->d_x1_gid, x1_gid, s));
+    HIPCHK(upload(&M->d_x1_loc, x1_loc, s));
+    HIPCHK(upload(&M->d_x1_chunk, x1_chunk, s));
+    HIPCHK(upload(&M->d_el2x_ptr, el2x_ptr, s));
+    HIPCHK(upload(&M->d_el2x, el2x, s));
+    HIPCHK(dalloc(&M->d_chunk_flag, (size_t)std::max(M->nchunk, 1)));
+    HIPCHK(dalloc(&M->d_slot_chunk, (size_t)nr * std::max(M->capc, 1)));
+    HIPCHK(dalloc(&M->d_counts, (size_t)nr));
+    HIPCHK(dalloc(&M->d_x1ctl, 4));
+    HIPCHK(dalloc(&M->d_last_del, (size_t)std::max(M->neo, 1)));
     HIPCHK(dalloc(&M->d_velo0_loc, 3 * (size_t)c->nN));
     if (!c->h_velo0.empty())
         HIPCHK(hipMemcpyAsync(M->d_velo0_loc, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double),
@@ -1898,7 +2196,7 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     else
         HIPCHK(hipMemsetAsync(M->d_velo0_loc, 0, 3 * (size_t)c->nN * sizeof(double), s));
     if (int rc = hkc::comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
-    M->seq = 0;
+    if (int rc = hkc::mir_reset(c)) return rc;
     if (c->state_ok)
         if (int rc = hkc::mir_pack(c, true)) return rc;
     HIPCHK(hipStreamSynchronize(s));
@@ -2044,6 +2342,17 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
     const int64_t v[7] = {ctl[kEv], ctl[kEvMax], ctl[kNcand], ctl[kTouched + C->tsel], 0, 0, 0};
     for (int r = 0; r < C->nreg; ++r) live[C->reg_list_h[r]] += reg[2 * r + 1];
     for (int k = 0; k < cap && k < 7; ++k) stats[k] = k < 4 ? v[k] : live[k == 4 ? 2 : k - 5];
+    if (cap > 7) {  // multi-GPU mirror: exposed-node chunks all ranks sent in the last step, bytes per block
+        long long sent = 0, bytes = 0;
+        if (hkc::Mirror* M = C->mir) {
+            std::vector<int> cnt((size_t)M->nranks);
+            HIPCHK(hipMemcpy(cnt.data(), M->d_counts, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+            for (int q : cnt) sent += std::min(q, M->capc);
+            bytes = (long long)M->blk_step;
+        }
+        stats[7] = sent;
+        if (cap > 8) stats[8] = bytes;
+    }
     return 0;
 }
 

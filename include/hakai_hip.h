@@ -194,7 +194,9 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
 /* Counters of the last contact step (diagnostics; syncs the stream): stats[0..cap) = events,
  * max events in any step, prefiltered triangles, nodes with contact force, live triangles, live
  * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
- * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included). */
+ * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
+ * [7] chunks of deletion-exposed contact nodes all ranks sent in the last step, [8] bytes of one
+ * rank's per-step block (hakai_set_contact_global). */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);

@@ -155,3 +155,45 @@ def test_contact_on_communicator_requires_global_model():
             from hakai._abi import check
             import ctypes
             check(sv.L.hakai_set_contact(sv.ctx, 1, ptr(inst, ctypes.c_int64)))
+
+
+def test_contact_group_exposed_node_chunks():
+    """The nodes only a deletion exposes travel in chunks once an adder is deleted: the run with
+    the default block capacity is bit-identical to one context and sends chunks; a block without
+    room for them fails loudly (no silent stale positions) and a raised capacity recovers."""
+    from hakai import mesh
+    from hakai._abi import HakaiError
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+    parts = _run_contact_group(glob, 2, glob.n_steps, key=610)
+    _assert_group_equals_single(glob, parts, g, gdel)
+    assert all(st["mirror_chunks_sent"] > 0 for *_, st in parts)
+
+    def build(key, chunks):
+        gdiag, _ = glob.lumped_mass()
+        ps = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+        svs = []
+        for r, (loc, diag, iface, l2g, off) in enumerate(ps):
+            sv = Solver(loc, diag_M=diag)
+            sv.set_element_offset(loc.global_element_offset)
+            sv.comm_init_local(r, 2, key)
+            sv.set_interface(*iface)
+            sv.set_contact_global(glob, l2g, off, gdiag)
+            sv.set_tuning("contact_mirror_chunks", chunks)
+            svs.append(sv)
+        return ps, svs
+
+    _, svs = build(611, 0)
+    with pytest.raises(HakaiError):
+        step_group(svs, 1, glob.n_steps)
+    for sv in svs:
+        sv.close()
+    ps, svs = build(612, 1 << 20)
+    step_group(svs, 1, glob.n_steps)
+    for sv, (loc, _, _, l2g, _) in zip(svs, ps):
+        st = sv.download()
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
+        sv.close()
