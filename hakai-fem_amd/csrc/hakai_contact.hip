@@ -66,6 +66,13 @@ struct PairParam {
 // after that deletion on, together with its u_pre; X1 nodes travel in chunks of 64 (rank segment,
 // ascending global id), and a chunk is sent once any of its nodes is. Sender and receivers mark
 // chunks from the same deletion steps, so both sides agree on the slot order.
+// Block layout of one step's exchange (see the kernels, "multi-GPU mirror")
+struct MirLayout {
+    int capc = 0, capd = 0;  // X1 chunks, deletion-list entries
+    size_t off_u = 0, off_dl = 0, off_x1 = 0, blk_step = 0, off_upre = 0, off_v0 = 0, off_del = 0, off_x1v0 = 0,
+           blk_full = 0;
+};
+
 struct Mirror {
     int rank = 0, nranks = 1;
     int maxx = 0, maxe = 0;           // block capacity: owned contact nodes, contact elements per rank
@@ -85,11 +92,15 @@ struct Mirror {
     double* d_velo0_loc = nullptr;    // [nN local][3] velocity before the first step (packed at s = 0)
     char* d_send[2] = {nullptr, nullptr};
     char* d_recv = nullptr;           // [nranks] blocks
-    // block layout (bytes): header (last deletion step), u, deletion steps; at s = 0 also u_pre, velo0
-    size_t off_u = 16, off_del = 0, off_upre = 0, off_v0 = 0, blk_step = 0, blk_full = 0;
+    size_t send_bytes[2] = {0, 0}, recv_bytes = 0;
+    // layout of the block of step s in lay[s&1]: capacities grow between steps, identically on all
+    // ranks, from the needs every rank computes at the unpack two steps earlier (h_need ring)
+    MirLayout lay[2];
+    int* h_need = nullptr;            // pinned [4][2]: max X1 chunks, max deletions of the unpack of step s; [8] = 1
+    hipEvent_t ev_need[4] = {nullptr, nullptr, nullptr, nullptr};
     long long seq = 0;                // step index since the last state reset (the block a step consumes)
     // X1: entries j = (rank segment q, node), chunks of 64 entries inside a segment
-    int nx1 = 0, nchunk = 0, capc = 0;    // entries, chunks (all ranks), block capacity in chunks
+    int nx1 = 0, nchunk = 0, maxseg = 0, slot_cap = 0;  // entries, chunks (all ranks), largest segment, slot table
     int* d_seg_chunk = nullptr;       // [nranks+1] first chunk of each rank's segment
     int* d_chunk_first = nullptr;     // [nchunk] first entry
     int* d_chunk_end = nullptr;       // [nchunk] one past the last entry
@@ -989,14 +1000,16 @@ __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, 
 }
 
 // ---- multi-GPU mirror (see hkc::Mirror) -----------------------------------------------------
-struct MirLayout {
-    size_t off_u, off_del, off_upre, off_v0;
-};
+// Block of one rank (bytes; regions 8-byte aligned). Every block: header int[4] = (last deletion
+// step, entries in the deletion list, -, -), X0 u, the deletion list (global element, step) of the
+// previous step, X1 slots (u, u_pre). Blocks of step 0 (after a state reset) add X0 u_pre and
+// velo0, the deletion step of every contact element, and X1 velo0.
+using hkc::MirLayout;
 
 struct X1Map {
     const int *el2x_ptr, *el2x, *x1_chunk;
     int* chunk_flag;
-    int* x1ctl;
+    int* x1ctl;  // [0] new marks since the last slot scan, [1] overflow bits, [2] max X1 chunks, [3] max deletions
 };
 
 // a deleted element's X1 entries: their chunks travel from now on
@@ -1006,14 +1019,15 @@ __device__ __forceinline__ void x1_mark(const X1Map& X, int e) {
     if (a1 > a0) X.x1ctl[0] = 1;
 }
 
-// this rank's block: last deletion step, u of the owned contact nodes, deletion step of its contact
-// elements; with `full` also u_pre and the velocity before the first step. Own deletions since the
-// last pack mark their X1 chunks.
+// this rank's block (header zeroed before): u of the owned X0 nodes; own contact elements deleted
+// since the last pack go to the deletion list and mark their X1 chunks; with `full` also u_pre,
+// velo0 and every contact element's deletion step.
 __global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const double* u, const double* upre,
                            const double* velo0, const int* del_step, const int* del_any, char* blk, MirLayout L,
                            int full, int* last_del, int elem_off, X1Map X) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) reinterpret_cast<int*>(blk)[0] = *del_any;
+    int* hdr = reinterpret_cast<int*>(blk);
+    if (i == 0) hdr[0] = *del_any;
     if (i < nxo) {
         const long long n = xo[i];
         double* pu = reinterpret_cast<double*>(blk + L.off_u) + 3 * (long long)i;
@@ -1029,8 +1043,20 @@ __global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const
     }
     if (i < neo) {
         const int d = del_step[eo[i]];
-        reinterpret_cast<int*>(blk + L.off_del)[i] = d;
-        if (d != 0 && last_del[i] == 0) x1_mark(X, eo[i] + elem_off);
+        if (full) reinterpret_cast<int*>(blk + L.off_del)[i] = d;
+        if (d != 0 && last_del[i] == 0) {
+            x1_mark(X, eo[i] + elem_off);
+            if (!full) {
+                const int k = atomicAdd(&hdr[1], 1);
+                if (k < L.capd) {
+                    int* dl = reinterpret_cast<int*>(blk + L.off_dl) + 2 * (long long)k;
+                    dl[0] = eo[i] + elem_off;
+                    dl[1] = d;
+                } else {
+                    atomicOr(&X.x1ctl[1], 2);
+                }
+            }
+        }
         last_del[i] = d;
     }
 }
@@ -1057,20 +1083,37 @@ __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx,
             }
         }
     }
-    if (i < (long long)nranks * maxe) {
-        const int e = eg[i];
-        if (e >= 0) {
-            const int q = (int)(i / maxe), k = (int)(i % maxe);
-            const int d = reinterpret_cast<const int*>(recv + (size_t)q * blk + L.off_del)[k];
-            if (d != 0 && gdel[e] == 0) x1_mark(X, e);
+    if (full) {
+        if (i < (long long)nranks * maxe) {
+            const int e = eg[i];
+            if (e >= 0) {
+                const int q = (int)(i / maxe), k = (int)(i % maxe);
+                const int d = reinterpret_cast<const int*>(recv + (size_t)q * blk + L.off_del)[k];
+                if (d != 0 && gdel[e] == 0) x1_mark(X, e);
+                gdel[e] = d;
+                gflag[e] = d == 0 ? 1 : 0;
+            }
+        }
+    } else if (i < (long long)nranks * L.capd) {
+        const int q = (int)(i / L.capd), k = (int)(i % L.capd);
+        const char* b = recv + (size_t)q * blk;
+        if (k < min(reinterpret_cast<const int*>(b)[1], L.capd)) {
+            const int* dl = reinterpret_cast<const int*>(b + L.off_dl) + 2 * (long long)k;
+            const int e = dl[0], d = dl[1];
+            if (gdel[e] == 0) x1_mark(X, e);
             gdel[e] = d;
-            gflag[e] = d == 0 ? 1 : 0;
+            gflag[e] = 0;
         }
     }
     if (i == 0) {
-        int mx = 0;
-        for (int q = 0; q < nranks; ++q) mx = max(mx, reinterpret_cast<const int*>(recv + (size_t)q * blk)[0]);
+        int mx = 0, nd = 0;
+        for (int q = 0; q < nranks; ++q) {
+            const int* h = reinterpret_cast<const int*>(recv + (size_t)q * blk);
+            mx = max(mx, h[0]);
+            nd = max(nd, h[1]);
+        }
         gdel[nE + 1] = mx;
+        X.x1ctl[3] = nd;
     }
 }
 
@@ -1078,8 +1121,10 @@ __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx,
 // nothing was marked since the last scan). counts[q] = chunks rank q sends; more than capc is an
 // overflow, recorded in x1ctl[1] and reported by contact_check.
 __global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* seg_chunk, const int* chunk_flag,
-                                                   int* slot_chunk, int capc, int* counts, int* x1ctl) {
+                                                   int* slot_chunk, int capc, int* counts, int* x1ctl,
+                                                   int record) {
     if (x1ctl[0] == 0) return;
+    int need = 0;
     __shared__ int s_w[1024 / 64];
     for (int q = q0; q < q1; ++q) {
         const int c0 = seg_chunk[q], c1 = seg_chunk[q + 1];
@@ -1094,11 +1139,15 @@ __global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* se
         }
         if (threadIdx.x == 0) {
             counts[q] = carry;
-            x1ctl[1] = max(x1ctl[1], carry);
+            if (carry > capc) x1ctl[1] |= 1;
         }
+        need = max(need, carry);
     }
     __syncthreads();
-    if (threadIdx.x == 0) x1ctl[0] = 0;
+    if (threadIdx.x == 0) {
+        x1ctl[0] = 0;
+        if (record) x1ctl[2] = need;  // the unpack's scan over all ranks: the same on every rank
+    }
 }
 
 struct X1Slots {
@@ -1347,6 +1396,9 @@ void contact_destroy(hakai_ctx* c) {
         dfree(M->d_seg_chunk); dfree(M->d_chunk_first); dfree(M->d_chunk_end); dfree(M->d_x1_gid); dfree(M->d_x1_loc);
         dfree(M->d_x1_chunk); dfree(M->d_el2x_ptr); dfree(M->d_el2x); dfree(M->d_chunk_flag); dfree(M->d_slot_chunk);
         dfree(M->d_counts); dfree(M->d_x1ctl); dfree(M->d_last_del);
+        if (M->h_need) (void)hipHostFree(M->h_need);
+        for (auto& e : M->ev_need)
+            if (e) (void)hipEventDestroy(e);
         delete M;
     }
     delete C;
@@ -1355,41 +1407,72 @@ void contact_destroy(hakai_ctx* c) {
 }
 
 static X1Map x1map(Mirror* M) { return X1Map{M->d_el2x_ptr, M->d_el2x, M->d_x1_chunk, M->d_chunk_flag, M->d_x1ctl}; }
-static X1Slots x1slots(Mirror* M) {
-    return X1Slots{M->d_counts, M->d_slot_chunk, M->d_chunk_first, M->d_chunk_end, M->capc};
+static X1Slots x1slots(Mirror* M, const MirLayout& L) {
+    return X1Slots{M->d_counts, M->d_slot_chunk, M->d_chunk_first, M->d_chunk_end, L.capc};
 }
 
-// block layout from the capacities (bytes, 8-byte aligned regions)
-static void mir_layout(Mirror* M) {
-    M->off_u = 16;
-    M->off_del = M->off_u + 24 * (size_t)M->maxx;
-    M->off_x1 = M->off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
-    M->blk_step = M->off_x1 + 48 * 64 * (size_t)M->capc;
-    M->off_upre = M->blk_step;
-    M->off_v0 = M->off_upre + 24 * (size_t)M->maxx;
-    M->off_x1v0 = M->off_v0 + 24 * (size_t)M->maxx;
-    M->blk_full = M->off_x1v0 + 24 * 64 * (size_t)M->capc;
+// block layout for the capacities (bytes, 8-byte aligned regions)
+static MirLayout mir_layout(const Mirror* M, int capc, int capd) {
+    MirLayout L;
+    L.capc = capc;
+    L.capd = capd;
+    L.off_u = 16;
+    L.off_dl = L.off_u + 24 * (size_t)M->maxx;
+    L.off_x1 = L.off_dl + 8 * (size_t)capd;
+    L.blk_step = L.off_x1 + 48 * 64 * (size_t)capc;
+    L.off_upre = L.blk_step;
+    L.off_v0 = L.off_upre + 24 * (size_t)M->maxx;
+    L.off_del = L.off_v0 + 24 * (size_t)M->maxx;
+    L.off_x1v0 = L.off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
+    L.blk_full = L.off_x1v0 + 24 * 64 * (size_t)capc;
+    return L;
 }
 
-// multi-GPU: pack this rank's mirror block for step M->seq (full = with u_pre and velo0)
+// buffers for the layout of parity par: its send block, the receive blocks, the slot table. A
+// grown slot table is rebuilt by the next scan (marked stale).
+static int mir_buffers(hakai_ctx* c, int par) {
+    Mirror* M = c->contact->mir;
+    const MirLayout& L = M->lay[par];
+    if (M->send_bytes[par] < L.blk_full) {
+        dfree(M->d_send[par]);
+        HIPCHK(dalloc(&M->d_send[par], L.blk_full));
+        M->send_bytes[par] = L.blk_full;
+        if (int rc = comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
+    }
+    if (M->recv_bytes < (size_t)M->nranks * L.blk_full) {
+        dfree(M->d_recv);
+        HIPCHK(dalloc(&M->d_recv, (size_t)M->nranks * L.blk_full));
+        M->recv_bytes = (size_t)M->nranks * L.blk_full;
+    }
+    if (M->slot_cap < L.capc) {
+        dfree(M->d_slot_chunk);
+        HIPCHK(dalloc(&M->d_slot_chunk, (size_t)M->nranks * L.capc));
+        M->slot_cap = L.capc;
+    }
+    return 0;
+}
+
+// multi-GPU: pack this rank's mirror block for step M->seq (full = with u_pre, velo0, all deletion
+// steps) in the layout of that step
 static int mir_pack(hakai_ctx* c, bool full) {
     Contact* C = c->contact;
     Mirror* M = C->mir;
     const int par = (int)(M->seq & 1);
+    const MirLayout& L = M->lay[par];
     const int n = std::max(std::max(M->nxo, M->neo), 1);
-    const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
     const double* velo0 = C->use_velo0 ? M->d_velo0_loc : nullptr;
+    HIPCHK(hipMemsetAsync(M->d_send[par], 0, 16, c->stream));  // header: the deletion-list counter
     hipLaunchKernelGGL(k_mir_pack, dim3((n + kB - 1) / kB), dim3(kB), 0, c->stream, M->d_xo, M->nxo, M->d_eo, M->neo,
                        c->d_u[c->cur], c->d_u[1 - c->cur], velo0, c->d_del_step, c->d_del_step + c->nEp + 1,
                        M->d_send[par], L, full ? 1 : 0, M->d_last_del, (int)c->elem_offset, x1map(M));
     if (M->nchunk > 0)  // also with capc = 0: the counts are what the overflow check reads
         hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, c->stream, M->rank, M->rank + 1, M->d_seg_chunk,
-                           M->d_chunk_flag, M->d_slot_chunk, M->capc, M->d_counts, M->d_x1ctl);
-    if (M->nchunk > 0 && M->capc > 0) {
-        const long long nt = 64LL * M->capc;
+                           M->d_chunk_flag, M->d_slot_chunk, L.capc, M->d_counts, M->d_x1ctl, 0);
+    if (M->nchunk > 0 && L.capc > 0) {
+        const long long nt = 64LL * L.capc;
         hipLaunchKernelGGL(k_x1_pack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, c->stream, M->rank,
-                           x1slots(M), M->d_x1_loc, c->d_u[c->cur], c->d_u[1 - c->cur], velo0, M->d_send[par],
-                           M->off_x1, M->off_x1v0, full ? 1 : 0);
+                           x1slots(M, L), M->d_x1_loc, c->d_u[c->cur], c->d_u[1 - c->cur], velo0, M->d_send[par],
+                           L.off_x1, L.off_x1v0, full ? 1 : 0);
     }
     HIPCHK(hipGetLastError());
     return comm_gather_mark(c, par);
@@ -1408,6 +1491,7 @@ static int mir_reset(hakai_ctx* c) {
     HIPCHK(hipMemcpyAsync(M->d_x1ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     M->seq = 0;
+    M->lay[1] = M->lay[0];
     return 0;
 }
 
@@ -1432,7 +1516,23 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
 int contact_post_step(hakai_ctx* c) {
     Contact* C = c->contact;
     if (!C || !C->mir) return 0;
-    C->mir->seq++;
+    Mirror* M = C->mir;
+    const long long s = M->seq++;  // the step just done consumed block s; pack block s+1
+    MirLayout L = M->lay[s & 1];
+    if (s >= 1) {  // grow from the needs of the unpack of step s-1 (the same numbers on every rank)
+        HIPCHK(hipEventSynchronize(M->ev_need[(s - 1) & 3]));
+        const int need_c = M->h_need[2 * ((s - 1) & 3)], need_d = M->h_need[2 * ((s - 1) & 3) + 1];
+        int capc = L.capc, capd = L.capd;
+        if (2 * need_c > capc) capc = std::min(M->maxseg, std::max(2 * capc, 2 * need_c + 64));
+        if (4 * need_d > capd) capd = std::max(2 * capd, 4 * need_d);
+        if (capc != L.capc || capd != L.capd) {
+            L = mir_layout(M, capc, capd);
+            // slot tables in the new stride (h_need[8] is a pinned constant 1)
+            HIPCHK(hipMemcpyAsync(M->d_x1ctl, M->h_need + 8, sizeof(int), hipMemcpyHostToDevice, c->stream));
+        }
+    }
+    M->lay[M->seq & 1] = L;
+    if (int rc = mir_buffers(c, (int)(M->seq & 1))) return rc;
     return mir_pack(c, false);
 }
 
@@ -1448,22 +1548,26 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     if (M) {  // all-gather the ranks' blocks of this step into the global mirror
         const int par = (int)(M->seq & 1);
         const bool full = M->seq == 0;
-        const size_t blk = full ? M->blk_full : M->blk_step;
+        const MirLayout& Ly = M->lay[par];
+        const size_t blk = full ? Ly.blk_full : Ly.blk_step;
         if (int rc = comm_allgather(c, par, M->d_recv, blk)) return rc;
-        const long long nslot = std::max(1LL, (long long)M->nranks * std::max(M->maxx, M->maxe));
-        const MirLayout L{M->off_u, M->off_del, M->off_upre, M->off_v0};
+        const long long nslot =
+            std::max(1LL, (long long)M->nranks * std::max(std::max(M->maxx, full ? M->maxe : Ly.capd), 1));
         hipLaunchKernelGGL(k_mir_unpack, dim3((unsigned)((nslot + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
-                           M->nranks, M->maxx, M->maxe, M->d_xg, M->d_eg, L, full ? 1 : 0, M->g_u[par],
+                           M->nranks, M->maxx, M->maxe, M->d_xg, M->d_eg, Ly, full ? 1 : 0, M->g_u[par],
                            M->g_u[1 - par], C->d_velo0, M->g_del, M->g_flag, C->nE, x1map(M));
         if (M->nchunk > 0)
             hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, s, 0, M->nranks, M->d_seg_chunk, M->d_chunk_flag,
-                               M->d_slot_chunk, M->capc, M->d_counts, M->d_x1ctl);
-        if (M->nchunk > 0 && M->capc > 0) {
-            const long long nt = 64LL * M->capc * M->nranks;
+                               M->d_slot_chunk, Ly.capc, M->d_counts, M->d_x1ctl, 1);
+        if (M->nchunk > 0 && Ly.capc > 0) {
+            const long long nt = 64LL * Ly.capc * M->nranks;
             hipLaunchKernelGGL(k_x1_unpack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
-                               M->nranks, x1slots(M), M->d_x1_gid, M->off_x1, M->off_x1v0, full ? 1 : 0, M->g_u[par],
-                               M->g_u[1 - par], C->d_velo0);
+                               M->nranks, x1slots(M, Ly), M->d_x1_gid, Ly.off_x1, Ly.off_x1v0, full ? 1 : 0,
+                               M->g_u[par], M->g_u[1 - par], C->d_velo0);
         }
+        HIPCHK(hipMemcpyAsync(M->h_need + 2 * (M->seq & 3), M->d_x1ctl + 2, 2 * sizeof(int), hipMemcpyDeviceToHost,
+                              s));
+        HIPCHK(hipEventRecord(M->ev_need[M->seq & 3], s));
         in.coord = M->g_coord;
         in.u = M->g_u[par];
         in.u_pre = M->g_u[1 - par];
@@ -1572,28 +1676,26 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, sizeof(unsigned int), c->stream));
         return 0;
     }
-    if (!std::strcmp(key, "contact_mirror_chunks")) {  // multi-GPU: block capacity for exposed-node chunks
+    if (!std::strcmp(key, "contact_mirror_chunks") || !std::strcmp(key, "contact_mirror_deletions")) {
+        // multi-GPU: block capacity for exposed-node chunks / deletion-list entries (both parities;
+        // call on every rank). Capacities also grow on their own between steps.
         Mirror* M = C->mir;
-        if (!M) return fail(HAKAI_ERR_STATE, "contact_mirror_chunks without hakai_set_contact_global");
-        if (value < 0 || value > (1LL << 24)) return fail(HAKAI_ERR_ARG, "contact_mirror_chunks out of range");
+        if (!M) return fail(HAKAI_ERR_STATE, "%s without hakai_set_contact_global", key);
+        if (value < 0 || value > (1LL << 24)) return fail(HAKAI_ERR_ARG, "%s out of range", key);
         HIPCHK(hipStreamSynchronize(c->stream));
-        M->capc = (int)std::min<long long>(value, M->nchunk);
-        mir_layout(M);
+        const bool ch = key[15] == 'c';
         for (int p = 0; p < 2; ++p) {
-            dfree(M->d_send[p]);
-            HIPCHK(dalloc(&M->d_send[p], M->blk_full));
+            const int capc = ch ? (int)std::min<long long>(value, M->maxseg) : M->lay[p].capc;
+            const int capd = ch ? M->lay[p].capd : (int)value;
+            M->lay[p] = mir_layout(M, capc, capd);
+            if (int rc = mir_buffers(c, p)) return rc;
         }
-        dfree(M->d_recv);
-        HIPCHK(dalloc(&M->d_recv, (size_t)M->nranks * M->blk_full));
-        dfree(M->d_slot_chunk);
-        HIPCHK(dalloc(&M->d_slot_chunk, (size_t)M->nranks * std::max(M->capc, 1)));
-        if (int rc = comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
         // the next block again, in the new layout; every slot table is rebuilt at the next unpack
-        const int ctl[2] = {1, 0};
-        HIPCHK(hipMemcpy(M->d_x1ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice));
+        const int one = 1;
+        HIPCHK(hipMemcpy(M->d_x1ctl, &one, sizeof(int), hipMemcpyHostToDevice));
         if (c->state_ok) {
             if (int rc = mir_pack(c, M->seq == 0)) return rc;
-            HIPCHK(hipMemcpyAsync(M->d_x1ctl, ctl, sizeof(int), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(M->d_x1ctl, M->h_need + 8, sizeof(int), hipMemcpyHostToDevice, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         return 0;
@@ -1647,9 +1749,14 @@ int contact_check(hakai_ctx* c) {
     if (Mirror* M = C->mir) {
         int x1[4];
         HIPCHK(hipMemcpy(x1, M->d_x1ctl, sizeof(x1), hipMemcpyDeviceToHost));
-        if (x1[1] > M->capc)
-            return fail(HAKAI_ERR_STATE, "contact mirror: a rank must send %d chunks of exposed contact nodes, the "
-                        "block holds %d; raise hakai_set_tuning(\"contact_mirror_chunks\") on every rank", x1[1], M->capc);
+        const MirLayout& L = M->lay[M->seq & 1];
+        if (x1[1] & 1)
+            return fail(HAKAI_ERR_STATE, "contact mirror: a rank had more chunks of exposed contact nodes to send "
+                        "than its block holds (now %d); raise hakai_set_tuning(\"contact_mirror_chunks\") on every "
+                        "rank", L.capc);
+        if (x1[1] & 2)
+            return fail(HAKAI_ERR_STATE, "contact mirror: a rank deleted more elements in one step than its block "
+                        "lists (now %d); raise hakai_set_tuning(\"contact_mirror_deletions\") on every rank", L.capd);
     }
     unsigned int ms = 0;
     HIPCHK(hipMemcpy(&ms, C->d_ctl + kEvShardMax, sizeof(unsigned int), hipMemcpyDeviceToHost));
@@ -2146,12 +2253,9 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     }
     M->nx1 = (int)x1_gid.size();
     M->nchunk = (int)chunk_first.size();
-    {
-        int mx = 0;
-        for (int q = 0; q < nr; ++q) mx = std::max(mx, seg_chunk[q + 1] - seg_chunk[q]);
-        M->capc = std::min(mx, std::max(32, (mx + 7) / 8));  // 1/8 of the largest segment; tuning raises it
-    }
-    mir_layout(M);
+    for (int q = 0; q < nr; ++q) M->maxseg = std::max(M->maxseg, seg_chunk[q + 1] - seg_chunk[q]);
+    // initial capacities (they grow between steps): 64 chunks of exposed nodes, 4096 deletions
+    M->lay[0] = M->lay[1] = hkc::mir_layout(M, std::min(M->maxseg, 64), 4096);
     std::vector<double> gmass((size_t)nNode);
     for (long long n = 0; n < nNode; ++n) gmass[n] = diag_M[3 * n];
     std::vector<int> ones((size_t)nElement, 1);
@@ -2168,10 +2272,11 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     for (int p = 0; p < 2; ++p) {
         HIPCHK(dalloc(&M->g_u[p], 3 * (size_t)nNode));
         HIPCHK(hipMemsetAsync(M->g_u[p], 0, 3 * (size_t)nNode * sizeof(double), s));
-        HIPCHK(dalloc(&M->d_send[p], M->blk_full));
-        HIPCHK(hipMemsetAsync(M->d_send[p], 0, M->blk_full, s));
     }
-    HIPCHK(dalloc(&M->d_recv, (size_t)nr * M->blk_full));
+    HIPCHK(hipHostMalloc((void**)&M->h_need, 16 * sizeof(int), hipHostMallocDefault));
+    std::fill(M->h_need, M->h_need + 16, 0);
+    M->h_need[8] = 1;
+    for (auto& e : M->ev_need) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(dalloc(&M->g_del, (size_t)nElement + 2));
     HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
     HIPCHK(dalloc(&M->g_fext, 3 * (size_t)nNode));
@@ -2185,7 +2290,6 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     HIPCHK(upload(&M->d_el2x_ptr, el2x_ptr, s));
     HIPCHK(upload(&M->d_el2x, el2x, s));
     HIPCHK(dalloc(&M->d_chunk_flag, (size_t)std::max(M->nchunk, 1)));
-    HIPCHK(dalloc(&M->d_slot_chunk, (size_t)nr * std::max(M->capc, 1)));
     HIPCHK(dalloc(&M->d_counts, (size_t)nr));
     HIPCHK(dalloc(&M->d_x1ctl, 4));
     HIPCHK(dalloc(&M->d_last_del, (size_t)std::max(M->neo, 1)));
@@ -2195,7 +2299,8 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
                               hipMemcpyHostToDevice, s));
     else
         HIPCHK(hipMemsetAsync(M->d_velo0_loc, 0, 3 * (size_t)c->nN * sizeof(double), s));
-    if (int rc = hkc::comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
+    for (int p = 0; p < 2; ++p)
+        if (int rc = hkc::mir_buffers(c, p)) return rc;
     if (int rc = hkc::mir_reset(c)) return rc;
     if (c->state_ok)
         if (int rc = hkc::mir_pack(c, true)) return rc;
@@ -2347,8 +2452,8 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
         if (hkc::Mirror* M = C->mir) {
             std::vector<int> cnt((size_t)M->nranks);
             HIPCHK(hipMemcpy(cnt.data(), M->d_counts, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
-            for (int q : cnt) sent += std::min(q, M->capc);
-            bytes = (long long)M->blk_step;
+            for (int q : cnt) sent += std::min(q, M->lay[M->seq & 1].capc);
+            bytes = (long long)M->lay[M->seq & 1].blk_step;
         }
         stats[7] = sent;
         if (cap > 8) stats[8] = bytes;
