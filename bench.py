@@ -51,14 +51,16 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--dist-path", action="store_true",
+                    help="rehearsal: take the N>1 path (C5 slab, RCCL communicator) even with one rank")
     return ap.parse_args()
 
 
-def build_rank_model(rank, world, layers_override=0):
+def build_rank_model(rank, world, layers_override=0, dist_path=False):
     """Returns (local Model, local diag_M, interface arrays or None, config dict)."""
     from hakai import mesh
     from hakai.dist import slab_partition
-    if world == 1:
+    if world == 1 and not dist_path:
         nz = layers_override or 5000
         m = mesh.config_c3(v_end=5e5) if nz == 5000 else mesh.bar_model(
             20, 20, nz, mesh.steel_ductile(), lambda z, L: 5e5 * z / L, name="C3")
@@ -111,14 +113,19 @@ def main():
     import hakai
     from hakai._abi import K_ELEMENT, K_EXCHANGE, K_NODAL, K_BC
     from hakai.solver import Solver, comm_unique_id
-    if world > 1:
+    multi = world > 1 or a.dist_path
+    if multi:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    model, diag, iface, cfg, preload = build_rank_model(rank, world, a.layers)
+    model, diag, iface, cfg, preload = build_rank_model(rank, world, a.layers, a.dist_path)
     if a.preload >= 0:
         preload = a.preload
-    sv = Solver(model, device=local_rank if world > 1 else 0, diag_M=diag)
-    if world > 1:
+    sv = Solver(model, device=local_rank if multi else 0, diag_M=diag)
+    if multi:
         uid = comm_unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
         dist.broadcast(t, 0)
@@ -134,7 +141,7 @@ def main():
     sv.sync()
 
     def barrier():
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -148,7 +155,7 @@ def main():
     sv.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if multi:
         dist.barrier()
     elapsed = t1 - t0
     t += a.steps
@@ -165,7 +172,7 @@ def main():
     plastic_frac = float(np.mean(st.integ_eq_plastic_strain > 0))
     n_active = int(st.element_flag.sum())
     n_deleted = model.nElement - n_active
-    if world > 1:
+    if multi:
         v = torch.tensor([elapsed, float(n_active)], dtype=torch.float64, device="cuda")
         mx = v.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -232,7 +239,7 @@ def main():
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
