@@ -3,6 +3,8 @@ same partition, pack / interface-sum / fix kernels and exchange protocol as the 
 (hakai_comm.cpp), and must reproduce the single-context run BIT FOR BIT: the interface Q is summed
 in the reference's serial element order (v2/HAKAI_j.jl:669-675) on both sides of every cut.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -197,3 +199,21 @@ def test_contact_group_exposed_node_chunks():
         st = sv.download()
         assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
         sv.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_multi_gpu_driver_writes_the_same_vtk(tmp_path, ranks):
+    """HAKAI(fname) over ranks (hakai.run.hakai_multi, here as an in-process group): contact with
+    deletion, 101 VTK files byte-identical to the one-GPU driver's."""
+    import hakai
+    from hakai import mesh
+    from hakai.run import hakai_multi
+    from inp_writer import write_inp
+    m = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    deck = write_inp(str(tmp_path / "impact.inp"), m)
+    hakai.hakai(deck, str(tmp_path / "one"), verbose=False)
+    hakai_multi(deck, str(tmp_path / "multi"), local_ranks=ranks, verbose=False)
+    files = sorted(os.listdir(tmp_path / "one"))
+    assert len(files) == 101 and sorted(os.listdir(tmp_path / "multi")) == files
+    for f in files:
+        assert (tmp_path / "one" / f).read_bytes() == (tmp_path / "multi" / f).read_bytes(), f
