@@ -179,7 +179,9 @@ int hakai_set_contact_cp(hakai_ctx* ctx, int32_t contact_flag, const int64_t* el
  * [rank_elem_off[r], rank_elem_off[r+1])). Every rank then mirrors the global contact model and
  * all-gathers, each step, the displacements of the contact nodes and the deletion steps of the
  * contact elements; the contact force is bit-identical to one GPU. hakai_set_contact[_cp] on a
- * rank with a communicator returns HAKAI_ERR_STATE. */
+ * rank with a communicator returns HAKAI_ERR_STATE. With a mirror, hakai_step, hakai_reset_state,
+ * hakai_upload_state, hakai_contact_force and hakai_set_tuning("contact_mirror_chunks" /
+ * "contact_mirror_deletions") are collective: every rank calls them in the same order. */
 int hakai_set_contact_global(hakai_ctx* ctx, int32_t contact_flag, int64_t nNode, const double* coordmat,
                              int64_t nElement, const int64_t* elementmat, const int64_t* element_material,
                              const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
