@@ -217,3 +217,45 @@ def test_multi_gpu_driver_writes_the_same_vtk(tmp_path, ranks):
     assert len(files) == 101 and sorted(os.listdir(tmp_path / "multi")) == files
     for f in files:
         assert (tmp_path / "one" / f).read_bytes() == (tmp_path / "multi" / f).read_bytes(), f
+
+
+def test_contact_group_after_state_upload():
+    """hakai_upload_state on every rank (a mid-run state with deleted elements, restricted to each
+    rank's nodes and elements) starts the mirror afresh: the next steps equal a single context
+    that uploaded the same state, bit for bit."""
+    from hakai import mesh
+    from hakai.solver import State
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    with Solver(glob) as sv:
+        sv.step(1, 250)
+        S = sv.download()
+    assert np.count_nonzero(S.element_flag == 0) > 0
+    with Solver(glob) as sv:
+        sv.upload(S)
+        sv.step(251, 150)
+        g = sv.download()
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, 2, 7070)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        n = l2g - 1
+        e0, ne = loc.global_element_offset, loc.nElement
+        nd = lambda a: np.ascontiguousarray(a.reshape(-1, 3)[n].ravel())  # noqa: E731
+        gp = slice(8 * e0, 8 * (e0 + ne))
+        sv.upload(State(nd(S.disp), nd(S.disp_pre), nd(S.velo), nd(S.Q), S.integ_stress[gp].copy(),
+                        S.integ_strain[gp].copy(), S.integ_yield_stress[gp].copy(),
+                        S.integ_eq_plastic_strain[gp].copy(), S.integ_triax_stress[gp].copy(),
+                        S.element_flag[e0:e0 + ne].copy(), S.Qe[e0:e0 + ne].copy()))
+        svs.append(sv)
+    step_group(svs, 251, 150)
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
+        e0 = loc.global_element_offset
+        assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + loc.nElement])
+        sv.close()
