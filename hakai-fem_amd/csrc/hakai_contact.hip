@@ -1590,6 +1590,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     in.del_step = del_step;
     in.t = (int)t;
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
+    const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
     hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
                        C->force_rebuild ? 1 : 0, del_any, in.t, C->d_touched[1 - tsel], tsel, fext);
@@ -1606,12 +1607,15 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         L.flag = in.flag; L.del_step = del_step; L.t = in.t;
         const Tile* tl = (const Tile*)C->d_tiles;
         const unsigned gt = (unsigned)std::min(C->ntile, 2048);
-        // full rebuild (forced steps only)
-        hipLaunchKernelGGL(k_ct_live_count, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_cnt);
-        hipLaunchKernelGGL(k_ct_live_scan, dim3(1), dim3(kB), 0, s, C->d_ctl, C->ntile, C->d_tile_cnt, C->d_tile_off,
-                           C->nreg, C->d_reg_first, C->d_reg);
-        hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
-                           C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+        // full rebuild (forced steps only: the host knows them, so the kernels are not even launched
+        // otherwise)
+        if (rebuild) {
+            hipLaunchKernelGGL(k_ct_live_count, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_cnt);
+            hipLaunchKernelGGL(k_ct_live_scan, dim3(1), dim3(kB), 0, s, C->d_ctl, C->ntile, C->d_tile_cnt,
+                               C->d_tile_off, C->nreg, C->d_reg_first, C->d_reg);
+            hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
+                               C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+        }
         // incremental update (steps after a deletion)
         hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
                            C->d_dlist);
