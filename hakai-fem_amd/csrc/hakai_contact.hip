@@ -1118,7 +1118,7 @@ __global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx,
 }
 
 // X1 slots: the marked chunks of ranks q0..q1-1 in ascending chunk order (one block; skipped when
-// nothing was marked since the last scan). counts[q] = chunks rank q sends; more than capc is an
+// nothing was marked since the last all-rank scan). counts[q] = chunks rank q sends; more than capc is an
 // overflow, recorded in x1ctl[1] and reported by contact_check.
 __global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* seg_chunk, const int* chunk_flag,
                                                    int* slot_chunk, int capc, int* counts, int* x1ctl,
@@ -1144,9 +1144,12 @@ __global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* se
         need = max(need, carry);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    // only the unpack's scan over all ranks clears the flag and records the need (the same on every
+    // rank): a pack-time scan of the own segment leaves the other segments' tables to it, which
+    // matters when a capacity change moved the table stride
+    if (threadIdx.x == 0 && record) {
         x1ctl[0] = 0;
-        if (record) x1ctl[2] = need;  // the unpack's scan over all ranks: the same on every rank
+        x1ctl[2] = need;
     }
 }
 
@@ -1523,8 +1526,8 @@ int contact_post_step(hakai_ctx* c) {
         HIPCHK(hipEventSynchronize(M->ev_need[(s - 1) & 3]));
         const int need_c = M->h_need[2 * ((s - 1) & 3)], need_d = M->h_need[2 * ((s - 1) & 3) + 1];
         int capc = L.capc, capd = L.capd;
-        if (2 * need_c > capc) capc = std::min(M->maxseg, std::max(2 * capc, 2 * need_c + 64));
-        if (4 * need_d > capd) capd = std::max(2 * capd, 4 * need_d);
+        if (2 * need_c >= capc && need_c > 0) capc = std::min(M->maxseg, std::max(2 * capc, 4 * need_c + 64));
+        if (4 * need_d >= capd && need_d > 0) capd = std::max(2 * capd, 8 * need_d);
         if (capc != L.capc || capd != L.capd) {
             L = mir_layout(M, capc, capd);
             // slot tables in the new stride (h_need[8] is a pinned constant 1)

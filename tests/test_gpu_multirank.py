@@ -259,3 +259,37 @@ def test_contact_group_after_state_upload():
         e0 = loc.global_element_offset
         assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + loc.nElement])
         sv.close()
+
+
+def test_contact_mirror_capacity_grows_between_steps():
+    """Starting from a one-chunk block, the exposed-node capacity grows between steps from the
+    needs every rank computes identically (no overflow, results bit-identical to one context)."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(16, 16, 8), impactor=(4, 4, 4), v=-3e5, d_time=2e-8, n_steps=300)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+    assert len(gdel) > 0
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, 2, 8080)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        sv.set_tuning("contact_mirror_chunks", 1)
+        svs.append(sv)
+    b0 = svs[0].contact_stats()["mirror_block_bytes"]
+    step_group(svs, 1, glob.n_steps)
+    st0 = svs[0].contact_stats()
+    assert st0["mirror_chunks_sent"] > 1 and st0["mirror_block_bytes"] > b0
+    dels = []
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        dels += [tuple(x) for x in sv.deleted()]
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
+        sv.close()
+    assert sorted(dels) == gdel
