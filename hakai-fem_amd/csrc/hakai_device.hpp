@@ -56,6 +56,26 @@ __device__ __forceinline__ double allreduce8(double x) {
     return x;
 }
 
+// Reduce-scatter in RELATIVE slots: lane k holds v[j] for node s = j ^ k (s a node label in
+// 0..7), and partners are k^7 (half mirror), k^2, k^1. The partner's slot for the same node is
+// j ^ (partner mask), so every lane keeps slots with the mask bit clear and reads the partner's
+// slot j ^ mask: no per-lane selects. Lane k returns the sum over lanes for node s = k.
+// 21 double exchanges + 21 adds.
+__device__ __forceinline__ void reduce_scatter8_rel(const double (&v)[8][3], double (&out)[3]) {
+    double w[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) w[j][c] = v[j][c] + dpp<kDppHalfMir>(v[j ^ 7][c]);
+    double u[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) u[j][c] = w[j][c] + dpp<kDppXor2>(w[j ^ 2][c]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c] = u[0][c] + dpp<kDppXor1>(u[1][c]);
+}
+
 // Reduce-scatter of a per-lane [8 nodes][3] array over the 8 lanes: lane k returns the sum over
 // lanes of v[k][0..2]. 21 double exchanges instead of 72 for an all-reduce.
 __device__ __forceinline__ void reduce_scatter8(const double (&v)[8][3], double (&out)[3], int k) {

