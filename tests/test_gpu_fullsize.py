@@ -1,0 +1,109 @@
+"""Parity at BASELINE.json's full sizes (the bench's own configurations), not just small meshes.
+
+* C3, 2 M hex (the bench's workload, v_end = 5e5 mm/s): the GPU runs to just before the first ductile
+  deletion (step 7950, found by tools/diag_fullsize_deletion.py on MI355X). Its state goes into the
+  oracle and both run the window 7947-7953, which holds two deletion waves. The deletion lists must
+  be identical and the displacement within the north star's 1e-6.
+* C3: size-independent properties of one full step: every element's 8 nodal forces sum to zero
+  (sum_i dN_i/dx = 0, so B^T sigma has no net force), and the assembled Q obeys the same balance.
+* C5 family, the bench's N=2 weak-scaling case (100x100x400, 2 z-slabs of 2 M hex): the 2-rank
+  in-process group (same partition, pack / fix kernels and exchange protocol as the RCCL path) is
+  bit-identical to one context holding all 4 M elements.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from hakai import dist, mesh
+from hakai.solver import Solver, step_group
+from util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+C3_FIRST_DELETION = 7950          # MI355X, tools/diag_fullsize_deletion.py (v_end 5e5)
+WINDOW = (7947, 7953)             # both deletion waves (7950, 7953) inside
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "8"))
+
+
+@pytest.fixture(scope="module")
+def c3():
+    return mesh.config_c3(v_end=5e5)
+
+
+def test_c3_fullsize_deletion_window_vs_oracle(c3):
+    import oracle as O
+    m = c3
+    t0, t1 = WINDOW
+    with Solver(m) as sv:
+        sv.step(1, t0 - 1)
+        assert len(sv.deleted()) == 0, "no deletion may happen before the window"
+        g = sv.download()
+        o = O.Oracle(m, nthreads=_threads())
+        s = o.s
+        for k in ("disp", "disp_pre", "velo", "Q", "Qe", "integ_stress", "integ_strain", "integ_yield_stress",
+                  "integ_eq_plastic_strain", "integ_triax_stress", "element_flag"):
+            s[k][...] = getattr(g, k)
+        s["position"][...] = m.coordmat + g.disp.reshape(-1, 3)
+        del g
+        assert np.mean(s["integ_eq_plastic_strain"] > 0) > 0.9, "window must be elastoplastic"
+        n = t1 - t0 + 1
+        o.run(t0, n)
+        sv.step(t0, n)
+        gdel = [tuple(int(v) for v in x) for x in sv.deleted()]
+        g = sv.download()
+    assert len(o.deletions) > 0 and min(d[0] for d in o.deletions) == C3_FIRST_DELETION
+    assert gdel == sorted(tuple(int(v) for v in d) for d in o.deletions)
+    assert np.array_equal(g.element_flag, s["element_flag"])
+    assert rel_err(g.disp, s["disp"]) < 1e-6
+    assert rel_err(g.velo, s["velo"]) < 1e-6
+    assert rel_err(g.integ_stress, s["integ_stress"]) < 1e-6
+    assert rel_err(g.integ_eq_plastic_strain, s["integ_eq_plastic_strain"]) < 1e-6
+
+
+def test_c3_fullsize_force_balance(c3):
+    m = c3
+    with Solver(m) as sv:
+        sv.step(1, 400)          # the bench's preload: 96 % of Gauss points plastic
+        g = sv.download(Qe=True, Q=True)
+    fe = g.Qe.reshape(m.nElement, 8, 3)
+    scale = np.max(np.abs(fe), axis=(1, 2))
+    assert np.all(scale > 0)
+    net = np.max(np.abs(fe.sum(axis=1)), axis=1)
+    assert np.max(net / scale) < 1e-11
+    q = g.Q.reshape(-1, 3)
+    assert np.max(np.abs(q.sum(axis=0))) / np.abs(q).sum(axis=0).max() < 1e-12
+
+
+def test_c5_two_slabs_fullsize_bitexact():
+    world, layers, n_steps = 2, 400, 30
+    glob = mesh.config_c5(layers=layers)
+    with Solver(glob) as sv:
+        sv.step(1, n_steps)
+        g = sv.download(disp=True, disp_pre=True, integ_stress=True, element_flag=True)
+    assert np.any(g.disp != 0)
+    svs, parts = [], []
+    try:
+        for r in range(world):
+            loc, diag, iface = dist.slab_partition(glob, r, world, nx=100, ny=100)
+            sv = Solver(loc, diag_M=diag)
+            sv.set_element_offset(loc.global_element_offset)
+            sv.comm_init_local(r, world, 4242)
+            sv.set_interface(*iface)
+            svs.append(sv)
+            parts.append(loc)
+        step_group(svs, 1, n_steps)
+        for sv, loc in zip(svs, parts):
+            st = sv.download(disp=True, disp_pre=True, integ_stress=True, element_flag=True)
+            n0, nl = loc.global_node_offset, loc.nNode
+            e0, el = loc.global_element_offset, loc.nElement
+            assert np.array_equal(st.disp, g.disp[3 * n0:3 * (n0 + nl)])
+            assert np.array_equal(st.disp_pre, g.disp_pre[3 * n0:3 * (n0 + nl)])
+            assert np.array_equal(st.integ_stress, g.integ_stress[8 * e0:8 * (e0 + el)])
+            assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
+    finally:
+        for sv in svs:
+            sv.close()
