@@ -1,0 +1,88 @@
+"""Edge cases of the element / assembly path against the oracle, and loud failure on bad input.
+
+* Ragged incidence: every element of a bar duplicated in place (two coincident elements share all
+  8 nodes), so interior nodes have 16 incident elements. The padded [nN][8] gather cannot hold them
+  and the library switches to the CSR gather; the element-order sum is still the reference's
+  serial assembly (v2/HAKAI_j.jl:669-675).
+* Inverted elements: every element with its two node faces swapped has det J < 0 at every Gauss
+  point. The reference takes |det| in B-bar (`:1736-1742`, with a warning) but the signed det in
+  Bfinal, the force weight and the lumped mass (`:1436-1443`, `:1335`, `:194`); the device must do
+  the same and count the negative Jacobians. (A single inverted element in a right-handed mesh makes
+  the reference blow up to NaN within a few steps, so the whole mesh is mirrored.)
+* Out-of-range node or material indices: the reference raises BoundsError; the C ABI returns an
+  error (no partial upload, no silent clamp).
+"""
+import numpy as np
+import pytest
+
+from hakai.model import Model
+from hakai.solver import Solver
+import oracle as O
+from util import rel_err, small_bar
+
+pytestmark = pytest.mark.gpu
+
+
+def _clone(m, elementmat, element_material):
+    return Model(m.coordmat.copy(), elementmat, element_material, m.materials, bc=m.bc, ic_dofs=m.ic_dofs,
+                 ic_values=m.ic_values, d_time=m.d_time, end_time=m.end_time, name=m.name + "_edge")
+
+
+def _run_both(m, n):
+    o = O.Oracle(m)
+    o.run(1, n)
+    with Solver(m) as sv:
+        sv.step(1, n)
+        g = sv.download()
+        dels = [tuple(int(v) for v in x) for x in sv.deleted()]
+        nneg = sv.negative_jacobians()
+    return o, g, dels, nneg
+
+
+def test_duplicated_elements_ragged_incidence():
+    base = small_bar(3, 2, 6, v_end=2e5, n_steps=400)
+    em = np.repeat(base.elementmat, 2, axis=0)
+    mm = np.repeat(base.element_material, 2)
+    m = _clone(base, em, mm)
+    counts = np.bincount(m.elementmat.ravel())
+    assert counts.max() == 16
+    o, g, dels, _ = _run_both(m, 400)
+    assert dels == sorted(tuple(int(v) for v in d) for d in o.deletions)
+    assert np.array_equal(g.element_flag, o.s["element_flag"])
+    assert rel_err(g.disp, o.s["disp"]) < 1e-6
+    assert rel_err(g.integ_stress, o.s["integ_stress"]) < 1e-6
+    assert np.any(g.integ_eq_plastic_strain > 0)
+    # coincident twins see identical nodes and state: their Gauss-point stresses are equal
+    st = g.integ_stress.reshape(-1, 2, 8, 6)
+    assert rel_err(st[:, 0], st[:, 1]) < 1e-12
+
+
+def test_inverted_elements_parity():
+    base = small_bar(3, 2, 6, v_end=2e5, n_steps=300)
+    m = _clone(base, base.elementmat[:, [4, 5, 6, 7, 0, 1, 2, 3]].copy(), base.element_material.copy())
+    o, g, dels, nneg = _run_both(m, 300)
+    assert np.min(o.diag_M) < 0          # signed det in the lumped mass, as in the reference
+    assert nneg > 0
+    assert dels == sorted(tuple(int(v) for v in d) for d in o.deletions)
+    assert rel_err(g.disp, o.s["disp"]) < 1e-6
+    assert rel_err(g.integ_stress, o.s["integ_stress"]) < 1e-6
+    # the two sign flips (mass and force weight) cancel: same motion as the right-handed mesh
+    with Solver(base) as sv:
+        sv.step(1, 300)
+        g0 = sv.download(disp=True)
+    assert rel_err(g.disp, g0.disp) < 1e-10
+
+
+@pytest.mark.parametrize("what", ["node_zero", "node_past_end", "material"])
+def test_bad_indices_fail_loudly(what):
+    base = small_bar(2, 2, 3)
+    em, mm = base.elementmat.copy(), base.element_material.copy()
+    if what == "node_zero":
+        em[1, 3] = 0
+    elif what == "node_past_end":
+        em[2, 6] = base.nNode + 1
+    else:
+        mm[0] = 2
+    m = _clone(base, em, mm)
+    with pytest.raises(Exception, match="out of"):
+        Solver(m, diag_M=np.ones(3 * m.nNode))
