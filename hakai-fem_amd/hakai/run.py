@@ -47,6 +47,12 @@ class _Output:
         self.sv = Solver(replace(glob, contact_flag=0, contact_pairs=None), device=device, diag_M=gdiag)
         self.out_dir = out_dir
         os.makedirs(out_dir, exist_ok=True)
+        # files are formatted and written on the writer's threads while the ranks step on
+        self.writer = None
+        w = ctypes.c_void_p()
+        check(lib().hakai_vtk_writer_create(ctypes.byref(w), out_dir.encode(), glob.nNode, ptr(glob.coordmat),
+                                            glob.nElement, ptr(glob.elementmat, I64), 0))
+        self.writer = w
 
     def write(self, idx, parts):
         g = self.glob
@@ -68,12 +74,18 @@ class _Output:
         st.disp = disp
         self.sv.upload(st)
         avg = self.sv.node_stress_strain()
-        check(lib().hakai_write_vtk(self.out_dir.encode(), idx, nN, ptr(g.coordmat), nE, ptr(g.elementmat, I64),
-                                    ptr(st.element_flag, I64), ptr(disp), ptr(velo), ptr(avg["node_stress"]),
-                                    ptr(avg["node_strain"]), ptr(avg["node_eq_plastic_strain"]),
-                                    ptr(avg["node_mises_stress"]), ptr(avg["node_triax_stress"])))
+        check(lib().hakai_vtk_writer_submit(self.writer, idx, ptr(st.element_flag, I64), ptr(disp), ptr(velo),
+                                            ptr(avg["node_stress"]), ptr(avg["node_strain"]),
+                                            ptr(avg["node_eq_plastic_strain"]), ptr(avg["node_mises_stress"]),
+                                            ptr(avg["node_triax_stress"])))
 
     def close(self):
+        if self.writer:
+            try:
+                check(lib().hakai_vtk_writer_wait(self.writer))
+            finally:
+                lib().hakai_vtk_writer_destroy(self.writer)
+                self.writer = None
         self.sv.close()
 
 

@@ -740,9 +740,6 @@ void pusai_table(double P[8][3][8]) {  // cal_Pusai_hexa, v2/HAKAI_j.jl:1895-194
         }
 }
 
-// write_vtk's tiny-value flush (v2/HAKAI_j.jl:3530-3558)
-inline double flush16(double x) { return std::fabs(x) < 1E-16 ? 0.0 : x; }
-
 }  // namespace
 
 extern "C" {
@@ -811,64 +808,6 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
     return 0;
 }
 
-int hakai_write_vtk(const char* dir, int index, int64_t nNode, const double* coordmat, int64_t nElement,
-                    const int64_t* elementmat, const int64_t* element_flag, const double* disp, const double* velo,
-                    const double* node_stress, const double* node_strain, const double* node_eqps,
-                    const double* node_mises, const double* node_triax) {
-    if (!dir || !coordmat || !elementmat || !element_flag || !disp || !velo || !node_stress || !node_strain ||
-        !node_eqps || !node_mises || !node_triax)
-        return fail(HAKAI_ERR_ARG, "write_vtk: null array");
-    mkdir(dir, 0755);
-    char fname[4096];
-    std::snprintf(fname, sizeof fname, "%s/file%03d.vtk", dir, index);
-    FILE* f = std::fopen(fname, "w");
-    if (!f) return fail(HAKAI_ERR_IO, "cannot write %s", fname);
-    std::vector<char> buf(1 << 20);
-    setvbuf(f, buf.data(), _IOFBF, buf.size());
-    std::fprintf(f, "# vtk DataFile Version 2.0\nTest\nASCII\nDATASET UNSTRUCTURED_GRID\n");
-    std::fprintf(f, "POINTS %lld float\n", (long long)nNode);
-    for (int64_t i = 0; i < nNode; ++i)
-        std::fprintf(f, "%1.6e %1.6e %1.6e\n", coordmat[3 * i], coordmat[3 * i + 1], coordmat[3 * i + 2]);
-    long long draw = 0;
-    for (int64_t e = 0; e < nElement; ++e) draw += element_flag[e];
-    std::fprintf(f, "CELLS %lld %lld\n", draw, draw * (8 + 1));
-    for (int64_t e = 0; e < nElement; ++e)
-        if (element_flag[e] == 1) {
-            const int64_t* c = elementmat + 8 * e;
-            std::fprintf(f, "8 %lld %lld %lld %lld %lld %lld %lld %lld\n", (long long)c[0] - 1, (long long)c[1] - 1,
-                         (long long)c[2] - 1, (long long)c[3] - 1, (long long)c[4] - 1, (long long)c[5] - 1,
-                         (long long)c[6] - 1, (long long)c[7] - 1);
-        }
-    std::fprintf(f, "CELL_TYPES %lld\n", draw);
-    for (long long i = 0; i < draw; ++i) std::fprintf(f, "12\n");
-    std::fprintf(f, "POINT_DATA %lld\nVECTORS DISPLACEMENT float\n", (long long)nNode);
-    for (int64_t i = 0; i < nNode; ++i)
-        std::fprintf(f, "%1.6e %1.6e %1.6e\n", flush16(disp[3 * i]), flush16(disp[3 * i + 1]), flush16(disp[3 * i + 2]));
-    const char* vn[3] = {"Vx", "Vy", "Vz"};
-    for (int c = 0; c < 3; ++c) {
-        std::fprintf(f, "SCALARS %s float 1\nLOOKUP_TABLE default\n", vn[c]);
-        for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(velo[3 * i + c]));
-    }
-    const char* en[6] = {"E11", "E22", "E33", "E12", "E23", "E13"};
-    for (int c = 0; c < 6; ++c) {
-        std::fprintf(f, "SCALARS %s float 1\nLOOKUP_TABLE default\n", en[c]);
-        for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(node_strain[6 * i + c]));
-    }
-    std::fprintf(f, "SCALARS EQ_PSTRAIN float 1\nLOOKUP_TABLE default\n");
-    for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(node_eqps[i]));
-    const char* sn[6] = {"S11", "S22", "S33", "S12", "S23", "S13"};
-    for (int c = 0; c < 6; ++c) {
-        std::fprintf(f, "SCALARS %s float 1\nLOOKUP_TABLE default\n", sn[c]);
-        for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(node_stress[6 * i + c]));
-    }
-    std::fprintf(f, "SCALARS MISES_STRESS float 1\nLOOKUP_TABLE default\n");
-    for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(node_mises[i]));
-    std::fprintf(f, "SCALARS TRIAX_STRESS float 1\nLOOKUP_TABLE default\n");
-    for (int64_t i = 0; i < nNode; ++i) std::fprintf(f, "%1.6e\n", flush16(node_triax[i]));
-    std::fclose(f);
-    return 0;
-}
-
 int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbose) {
     hakai_inp_model_t* M = nullptr;
     int r = hakai_inp_read(fname, &M);
@@ -907,19 +846,28 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
     if ((r = hakai_reset_state(c, M->n_ic_dofs, M->ic_dofs, M->ic_values, d_time))) return r;
     const long long n_steps = time_num >= 1.0 ? (long long)std::floor(time_num) : 0;
     const long long d_out = (long long)std::floor(time_num / 100);  // output_num = 100 (:471-472)
-    std::vector<double> disp(3 * nN), velo(3 * nN), ns(6 * nN), nn(6 * nN), ne(nN), nm(nN), nt(nN);
-    std::vector<int64_t> flag(nE);
+    // VTK files are formatted and written by the writer's thread team while the device steps on;
+    // the arrays go straight from the device into the writer's fill buffers (zero-copy commit).
+    hakai_vtk_writer* w = nullptr;
+    if ((r = hakai_vtk_writer_create(&w, out_dir, nN, M->coordmat, nE, M->elementmat, 0))) return r;
+    struct FreeW {
+        hakai_vtk_writer* w;
+        ~FreeW() { hakai_vtk_writer_destroy(w); }
+    } fw{w};
     auto output = [&](int idx) -> int {
+        hakai_vtk_arrays_t a;
+        int q = hakai_vtk_writer_acquire(w, &a);
+        if (q) return q;
         hakai_state_t st;
         std::memset(&st, 0, sizeof st);
-        st.disp = disp.data();
-        st.velo = velo.data();
-        st.element_flag = flag.data();
-        int q = hakai_download_state(c, &st);
-        if (q) return q;
-        if ((q = hakai_node_stress_strain(c, ns.data(), nn.data(), ne.data(), nm.data(), nt.data()))) return q;
-        return hakai_write_vtk(out_dir, idx, nN, M->coordmat, nE, M->elementmat, flag.data(), disp.data(), velo.data(),
-                               ns.data(), nn.data(), ne.data(), nm.data(), nt.data());
+        st.disp = a.disp;
+        st.velo = a.velo;
+        st.element_flag = a.element_flag;
+        if ((q = hakai_download_state(c, &st))) return q;
+        if ((q = hakai_node_stress_strain(c, a.node_stress, a.node_strain, a.node_eq_plastic_strain,
+                                          a.node_mises_stress, a.node_triax_stress)))
+            return q;
+        return hakai_vtk_writer_commit(w, idx);
     };
     if ((r = output(0))) return r;
     int i_out = 1;
@@ -944,6 +892,7 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
         t0 = t1 + 1;
     }
     if ((r = hakai_sync(c))) return r;
+    if ((r = hakai_vtk_writer_wait(w))) return r;
     if (verbose) std::printf("\n");
     return 0;
 }

@@ -259,6 +259,38 @@ int hakai_write_vtk(const char* dir, int index, int64_t nNode, const double* coo
                     const double* node_eq_plastic_strain, const double* node_mises_stress,
                     const double* node_triax_stress);
 
+/* Asynchronous, multi-threaded VTK writer (same bytes as hakai_write_vtk). A writer holds the
+ * mesh (initial coordinates are formatted once, elementmat is copied) and writes one file at a
+ * time on a background thread, so the device keeps stepping while the previous output is
+ * formatted (the reference writes synchronously, v2/HAKAI_j.jl:932-942). n_threads <= 0: env
+ * HAKAI_VTK_THREADS, else OMP_NUM_THREADS, else all hardware threads (at most 64).
+ *   submit: copies the arrays, waits for the file in flight, starts <dir>/file%03d.vtk.
+ *   acquire/commit: zero-copy variant; acquire returns the writer's fill buffers (valid until
+ *   commit), commit waits for the file in flight and starts writing the filled buffers.
+ *   wait: blocks until the file in flight is written; returns its status (write errors of an
+ *   earlier file also surface at the next submit/commit). destroy waits, then frees. */
+typedef struct hakai_vtk_writer hakai_vtk_writer;
+typedef struct {
+    int64_t* element_flag;           /* nElement */
+    double* disp;                    /* 3 x nNode */
+    double* velo;                    /* 3 x nNode */
+    double* node_stress;             /* 6 x nNode */
+    double* node_strain;             /* 6 x nNode */
+    double* node_eq_plastic_strain;  /* nNode */
+    double* node_mises_stress;       /* nNode */
+    double* node_triax_stress;       /* nNode */
+} hakai_vtk_arrays_t;
+int hakai_vtk_writer_create(hakai_vtk_writer** w, const char* dir, int64_t nNode, const double* coordmat,
+                            int64_t nElement, const int64_t* elementmat, int n_threads);
+int hakai_vtk_writer_submit(hakai_vtk_writer* w, int index, const int64_t* element_flag, const double* disp,
+                            const double* velo, const double* node_stress, const double* node_strain,
+                            const double* node_eq_plastic_strain, const double* node_mises_stress,
+                            const double* node_triax_stress);
+int hakai_vtk_writer_acquire(hakai_vtk_writer* w, hakai_vtk_arrays_t* arrays);
+int hakai_vtk_writer_commit(hakai_vtk_writer* w, int index);
+int hakai_vtk_writer_wait(hakai_vtk_writer* w);
+void hakai_vtk_writer_destroy(hakai_vtk_writer* w);
+
 /* HAKAI(fname) (v2/HAKAI_j.jl:81-978): read, set up, run the whole step loop on `device`, write
  * out_dir/file000.vtk .. file100.vtk every floor(time_num/100) steps. verbose=1 prints the
  * reference's progress lines. Returns 0 or <0. */
