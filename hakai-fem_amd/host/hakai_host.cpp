@@ -848,6 +848,8 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
     const long long d_out = (long long)std::floor(time_num / 100);  // output_num = 100 (:471-472)
     // VTK files are formatted and written by the writer's thread team while the device steps on;
     // the arrays go straight from the device into the writer's fill buffers (zero-copy commit).
+    const char* se = std::getenv("HAKAI_VTK_SYNC");  // 1: wait for every file (A/B measurements)
+    const bool sync_out = se && se[0] == '1';
     hakai_vtk_writer* w = nullptr;
     if ((r = hakai_vtk_writer_create(&w, out_dir, nN, M->coordmat, nE, M->elementmat, 0))) return r;
     struct FreeW {
@@ -867,7 +869,8 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
         if ((q = hakai_node_stress_strain(c, a.node_stress, a.node_strain, a.node_eq_plastic_strain,
                                           a.node_mises_stress, a.node_triax_stress)))
             return q;
-        return hakai_vtk_writer_commit(w, idx);
+        if ((q = hakai_vtk_writer_commit(w, idx))) return q;
+        return sync_out ? hakai_vtk_writer_wait(w) : 0;
     };
     if ((r = output(0))) return r;
     int i_out = 1;

@@ -195,6 +195,26 @@ def test_hakai_driver_writes_vtk(tmp_path):
     assert cells == "CELLS 4 36"
 
 
+def test_hakai_driver_async_output_equals_sync(tmp_path, monkeypatch):
+    """The driver's asynchronous multi-threaded VTK output writes the same 101 files, byte for byte,
+    as a synchronous one-thread writer (the reference's order of work, v2/HAKAI_j.jl:932-942), on a
+    deck with a deletion mid-run (CELLS shrinks)."""
+    import os
+    from inp_writer import write_inp
+    deck = tmp_path / "Tensile5e.inp"
+    write_inp(str(deck), mesh.tensile5e_model())
+    hakai.hakai(str(deck), str(tmp_path / "a"), verbose=False)
+    monkeypatch.setenv("HAKAI_VTK_SYNC", "1")
+    monkeypatch.setenv("HAKAI_VTK_THREADS", "1")
+    hakai.hakai(str(deck), str(tmp_path / "s"), verbose=False)
+    fa, fs = sorted(os.listdir(tmp_path / "a")), sorted(os.listdir(tmp_path / "s"))
+    assert fa == fs and len(fa) == 101
+    for f in fa:
+        assert (tmp_path / "a" / f).read_bytes() == (tmp_path / "s" / f).read_bytes(), f
+    assert "\nCELLS 5 45\n" in (tmp_path / "a" / "file000.vtk").read_text()
+    assert "\nCELLS 4 36\n" in (tmp_path / "a" / "file100.vtk").read_text()
+
+
 @pytest.mark.parametrize("tuning", [{"fe_layout": 1}, {"elem_map": 1}, {"fe_layout": 1, "elem_map": 1},
                                     {"elem_pipe_blocks": 0, "fe_layout": 1}, {"elem_map": 0},
                                     {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1}])
