@@ -189,6 +189,19 @@ void prof_end(hakai_ctx* c, EventPair* p) {
     (void)hipEventRecord(p->b, c->stream);
     c->ev_pending.push_back(*p);
 }
+void graph_invalidate(hakai_ctx* c) {
+    c->epoch++;
+    c->tdev_next = -1;
+}
+static void graph_free(hakai_ctx* c) {
+    for (int g = 0; g < 2; ++g)
+        for (int p = 0; p < 2; ++p)
+            if (c->g_exec[g][p]) {
+                (void)hipGraphExecDestroy(c->g_exec[g][p]);
+                c->g_exec[g][p] = nullptr;
+                c->g_epoch[g][p] = -1;
+            }
+}
 }  // namespace hkc
 
 
@@ -342,6 +355,8 @@ int hakai_destroy(hakai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     prof_harvest(c);
+    hkc::graph_free(c);
+    dfree(c->d_tstep);
     hkc::comm_destroy(c);
     hkc::free_model(c);
     hkc::free_bc(c);
@@ -355,6 +370,7 @@ int hakai_destroy(hakai_ctx* c) {
 int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int64_t nElement,
                        const int64_t* elementmat, const int64_t* element_material, int32_t nMat,
                        const hakai_material_t* mats, const double* diag_M) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null ctx");
     if (nNode <= 0 || nElement < 0 || !coordmat || (nElement > 0 && (!elementmat || !element_material)) || nMat <= 0 ||
         !mats || !diag_M)
@@ -465,6 +481,7 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
 }
 
 int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !bc) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "set_bc before upload_model");
     HIPCHK(hipSetDevice(c->device));
@@ -523,6 +540,7 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
 }
 
 int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const double* ic_values, double d_time) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "reset_state before upload_model");
     HIPCHK(hipSetDevice(c->device));
@@ -558,6 +576,7 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
 }
 
 int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "upload_state before upload_model");
     HIPCHK(hipSetDevice(c->device));
@@ -700,6 +719,142 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
     return 0;
 }
 
+// One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take
+// the step number from the device counter and the element kernel advances it.
+static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
+    hipStream_t s = c->stream;
+    EventPair ep;
+    const int par = c->cur;  // graph mode: this step reads counter slot 1-par, writes slot par
+    // nodal update (:562-567), Q from the previous step's element forces (:668-675)
+    hk::NodalArgs na;
+    na.u = c->d_u[c->cur];
+    na.u_pre_out = c->d_u[1 - c->cur];
+    na.mass = c->d_mass;
+    na.inc_ptr = c->d_inc_ptr;
+    na.inc = c->d_inc;
+    na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
+    na.cstride = c->fe_layout == 1 ? c->nEp : 1;
+    na.early = c->nodal_early;
+    na.fe_nt = c->nodal_fe_nt;
+    na.reverse = c->nodal_reverse;
+    na.fe = c->d_fe;
+    na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
+    na.fext = nullptr;
+    na.nN = c->nN;
+    na.dt = d_time;
+    int rc = 0;
+    if (c->contact) {  // contact force into external_force (:500-560)
+        hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
+        rc = hkc::contact_step(c, t, d_time);
+        hkc::prof_end(c, &ep);
+        if (rc) return rc;
+        na.fext = c->d_fext;
+    }
+    rc = hkc::comm_pre_nodal(c);
+    if (rc) return rc;
+    hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
+    HIPCHK(hk::launch_nodal(na, s));
+    hkc::prof_end(c, &ep);
+    // multi-GPU: interface nodes are redone with the cross-rank assembled Q
+    rc = hkc::comm_post_nodal(c, d_time);
+    if (rc) return rc;
+    // boundary conditions (:585-617)
+    if (c->nbc > 0) {
+        hk::BCArgs ba;
+        ba.dof = c->d_bc_dof;
+        ba.grp = c->d_bc_grp;
+        ba.val = c->d_bc_val;
+        ba.n = c->nbc;
+        ba.amp_n = c->d_amp_n;
+        ba.amp_off = c->d_amp_off;
+        ba.amp_t = c->d_amp_t;
+        ba.amp_v = c->d_amp_v;
+        ba.out = c->d_u[1 - c->cur];
+        ba.ct = t * d_time;
+        ba.t_rd = c->g_trd;
+        ba.dt = d_time;
+        hkc::prof_begin(c, HAKAI_K_BC, &ep);
+        HIPCHK(hk::launch_bc(ba, s));
+        hkc::prof_end(c, &ep);
+    }
+    c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
+    c->q_from_buf = false;
+    // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
+    hk::ElemArgs ea = elem_args(c);
+    ea.step_i = (int)t;
+    if (c->g_trd) {
+        ea.t_rd = c->g_trd;
+        ea.t_wr = c->d_tstep + par;
+    }
+    hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
+    HIPCHK(hk::launch_element(ea, c->has_ductile, last, s));
+    hkc::prof_end(c, &ep);
+    rc = hkc::comm_post_element(c, (long long)t);
+    if (rc) return rc;
+    rc = hkc::contact_post_step(c);
+    if (rc) return rc;
+    c->steps_done++;
+    c->last_dt = d_time;
+    return 0;
+}
+
+// Steps t and t+1 can come from a graph: same launch sequence every step, nothing host-side that
+// depends on the step (no multi-GPU exchange, no profiling events, no uploaded Q), and contact in
+// its steady state. The step number comes from a device counter; every pointer argument is fixed
+// for a given starting parity (cur), so one graph per parity serves the whole run.
+static bool graph_eligible(const hakai_ctx* c, double t) {
+    return c->graph && !c->comm && !c->prof && !c->q_from_buf && c->nE > 0 && hkc::contact_graph_ok(c, t);
+}
+
+static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
+    hipStream_t s = c->stream;
+    const int p0 = c->cur;
+    const int gi = len == 2 ? 1 : 0;
+    hipGraphExec_t& ge = c->g_exec[gi][p0];
+    if (!c->d_tstep) HIPCHK(dalloc(&c->d_tstep, 2));
+    if (c->tdev_next != (long long)t) HIPCHK(hk::launch_set_step(c->d_tstep + (1 - p0), t - 1.0, s));
+    if (ge && (c->g_epoch[gi][p0] != c->epoch || c->g_dt[gi][p0] != d_time || c->g_len[gi][p0] != len)) {
+        HIPCHK(hipStreamSynchronize(s));
+        (void)hipGraphExecDestroy(ge);
+        ge = nullptr;
+    }
+    if (!ge) {
+        // capture the steps; their host-side state changes happen here, as in stream mode
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int rc = 0;
+        for (int k = 0; k < len && !rc; ++k) {
+            c->g_trd = c->d_tstep + (1 - c->cur);
+            rc = step_once(c, t + k, d_time, false);
+        }
+        c->g_trd = nullptr;
+        hipError_t e = hipStreamEndCapture(s, &g);
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        if (e != hipSuccess) return hip_fail(e, "hipStreamEndCapture (step graph)");
+        e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) {
+            ge = nullptr;
+            return hip_fail(e, "hipGraphInstantiate (step graph)");
+        }
+        c->g_epoch[gi][p0] = c->epoch;
+        c->g_dt[gi][p0] = d_time;
+        c->g_len[gi][p0] = len;
+    } else {  // replay the host-side state changes of the captured steps
+        hkc::contact_graph_advance(c, t + len - 1);
+        c->q_from_buf = false;
+        c->steps_done += len;
+        c->last_dt = d_time;
+    }
+    HIPCHK(hipGraphLaunch(ge, s));
+    c->tdev_next = (long long)t + len;
+    c->graph_steps += len;
+    return 0;
+}
+
 int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step before upload_model/reset_state");
@@ -707,76 +862,31 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (n_steps > 1 && hkc::comm_is_local(c))
         return fail(HAKAI_ERR_ARG, "step: an in-process group is stepped one step per call, rank by rank");
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    for (int64_t it = 0; it < n_steps; ++it) {
+    int64_t it = 0;
+    while (it < n_steps) {
         const double t = t_first + (double)it;
-        EventPair ep;
-        // nodal update (:562-567), Q from the previous step's element forces (:668-675)
-        hk::NodalArgs na;
-        na.u = c->d_u[c->cur];
-        na.u_pre_out = c->d_u[1 - c->cur];
-        na.mass = c->d_mass;
-        na.inc_ptr = c->d_inc_ptr;
-        na.inc = c->d_inc;
-        na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
-        na.cstride = c->fe_layout == 1 ? c->nEp : 1;
-        na.early = c->nodal_early;
-        na.fe_nt = c->nodal_fe_nt;
-        na.reverse = c->nodal_reverse;
-        na.fe = c->d_fe;
-        na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
-        na.fext = nullptr;
-        na.nN = c->nN;
-        na.dt = d_time;
-        int rc = 0;
-        if (c->contact) {  // contact force into external_force (:500-560)
-            hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
-            rc = hkc::contact_step(c, t, d_time);
-            hkc::prof_end(c, &ep);
-            if (rc) return rc;
-            na.fext = c->d_fext;
+        int rc;
+        // the call's last step stays in stream mode: it also stores triaxiality for downloads
+        // (eligibility of step t implies it for the steps after it: step t clears every one-off
+        // condition)
+        const int len = (c->graph > 2 && it + c->graph < n_steps) ? c->graph : 2;
+        if (c->graph && it + len < n_steps && graph_eligible(c, t)) {
+            rc = step_graph(c, t, d_time, len);
+            it += len;
+        } else {
+            rc = step_once(c, t, d_time, it == n_steps - 1);
+            c->tdev_next = -1;
+            ++it;
         }
-        rc = hkc::comm_pre_nodal(c);
         if (rc) return rc;
-        hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
-        HIPCHK(hk::launch_nodal(na, s));
-        hkc::prof_end(c, &ep);
-        // multi-GPU: interface nodes are redone with the cross-rank assembled Q
-        rc = hkc::comm_post_nodal(c, d_time);
-        if (rc) return rc;
-        // boundary conditions (:585-617)
-        if (c->nbc > 0) {
-            hk::BCArgs ba;
-            ba.dof = c->d_bc_dof;
-            ba.grp = c->d_bc_grp;
-            ba.val = c->d_bc_val;
-            ba.n = c->nbc;
-            ba.amp_n = c->d_amp_n;
-            ba.amp_off = c->d_amp_off;
-            ba.amp_t = c->d_amp_t;
-            ba.amp_v = c->d_amp_v;
-            ba.out = c->d_u[1 - c->cur];
-            ba.ct = t * d_time;
-            hkc::prof_begin(c, HAKAI_K_BC, &ep);
-            HIPCHK(hk::launch_bc(ba, s));
-            hkc::prof_end(c, &ep);
-        }
-        c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
-        c->q_from_buf = false;
-        // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
-        hk::ElemArgs ea = elem_args(c);
-        ea.step_i = (int)t;
-        hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
-        HIPCHK(hk::launch_element(ea, c->has_ductile, it == n_steps - 1, s));
-        hkc::prof_end(c, &ep);
-        rc = hkc::comm_post_element(c, (long long)t);
-        if (rc) return rc;
-        rc = hkc::contact_post_step(c);
-        if (rc) return rc;
-        c->steps_done++;
-        c->last_dt = d_time;
     }
     return hkc::contact_check(c);
+}
+
+int hakai_graph_steps(hakai_ctx* c, int64_t* n) {
+    if (!c || !n) return fail(HAKAI_ERR_ARG, "null");
+    *n = c->graph_steps;
+    return 0;
 }
 
 int hakai_sync(hakai_ctx* c) {
@@ -808,6 +918,7 @@ int hakai_deleted(hakai_ctx* c, int64_t* n_deleted, int64_t* log, int64_t cap) {
 }
 
 int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !key) return fail(HAKAI_ERR_ARG, "set_tuning: null");
     if (!std::strcmp(key, "elem_minw")) {
         if (value != 2 && value != 3 && value != 4) return fail(HAKAI_ERR_ARG, "elem_minw must be 2, 3 or 4");
@@ -856,6 +967,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         }
         return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
     }
+    if (!std::strcmp(key, "graph")) {
+        if (value < 0 || value > 1024 || (value & 1)) return fail(HAKAI_ERR_ARG, "graph must be 0 or an even step count <= 1024");
+        c->graph = (int)value;
+        return 0;
+    }
     if (!std::strncmp(key, "contact_", 8)) {
         HIPCHK(hipSetDevice(c->device));
         return hkc::contact_tuning(c, key, value);
@@ -864,6 +980,7 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
 }
 
 int hakai_set_element_offset(hakai_ctx* c, int64_t element_offset) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || element_offset < 0) return fail(HAKAI_ERR_ARG, "set_element_offset: bad args");
     c->elem_offset = element_offset;
     return 0;
@@ -914,6 +1031,7 @@ int hakai_node_stress_strain(hakai_ctx* c, double* node_stress, double* node_str
 int hakai_profile_enable(hakai_ctx* c, int on) { return hakai_profile_mask(c, on ? (1u << HAKAI_K_COUNT) - 1 : 0u); }
 
 int hakai_profile_mask(hakai_ctx* c, uint32_t mask) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!mask) prof_harvest(c);
     c->prof = mask != 0;

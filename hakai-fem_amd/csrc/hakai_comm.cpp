@@ -390,6 +390,7 @@ int hakai_comm_unique_id(uint8_t id[128]) {
 }
 
 int hakai_comm_init(hakai_ctx* c, int rank, int nranks, const uint8_t id[128]) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(HAKAI_ERR_ARG, "comm_init: bad args");
     HIPCHK(hipSetDevice(c->device));
     hkc::comm_destroy(c);
@@ -407,6 +408,7 @@ int hakai_comm_init(hakai_ctx* c, int rank, int nranks, const uint8_t id[128]) {
 }
 
 int hakai_comm_init_local(hakai_ctx* c, int rank, int nranks, int64_t group_key) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(HAKAI_ERR_ARG, "comm_init_local: bad args");
     HIPCHK(hipSetDevice(c->device));
     hkc::comm_destroy(c);
@@ -436,6 +438,7 @@ int hakai_comm_init_local(hakai_ctx* c, int rank, int nranks, int64_t group_key)
 
 int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_node, const int32_t* rank_lo,
                         const int32_t* rank_hi) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     hkc::Comm* m = c->comm;
     if (!m) return fail(HAKAI_ERR_STATE, "set_interface before comm_init");

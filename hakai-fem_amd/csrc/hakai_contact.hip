@@ -258,7 +258,9 @@ constexpr int kShardStride = 32;  // unsigned ints between shard counters
 // the contact forces of the previous step's touched nodes back to 0 (external_force is otherwise
 // never rewritten).
 __global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs, int force,
-                           const int* del_any, int t, const int* touched_prev, int tsel, double* fext) {
+                           const int* del_any, int t, const double* t_rd, const int* touched_prev, int tsel,
+                           double* fext) {
+    if (t_rd) t = (int)*t_rd + 1;  // graph mode: step number from the device counter
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < kEvShards) evs[i * kShardStride] = 0;
     if (i < 12 * npairs) bbox[i] = ((i % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
@@ -421,8 +423,9 @@ __global__ __launch_bounds__(kB) void k_ct_live_write(const unsigned int* ctl, L
 }
 
 // incremental update, part 1: the elements deleted in the previous step (int4 sweep of del_step)
-__global__ void k_ct_find_del(unsigned int* ctl, const int* del_step, int nE, int t, int* dlist) {
+__global__ void k_ct_find_del(unsigned int* ctl, const int* del_step, int nE, int t, const double* t_rd, int* dlist) {
     if (ctl[kDel] == 0) return;
+    if (t_rd) t = (int)*t_rd + 1;
     const int n4 = nE >> 2;
     const int4* d4 = reinterpret_cast<const int4*>(del_step);
     for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += gridDim.x * blockDim.x) {
@@ -460,9 +463,10 @@ struct AppendIn {
 
 // incremental update, part 2: one block per deleted element, one thread per entry its deletion
 // exposes (triangles, then i-node entries, then j-node entries)
-__global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t, int* reg,
-                            int* ni_live, int* nj_live, int* tri_live) {
+__global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t,
+                            const double* t_rd, int* reg, int* ni_live, int* nj_live, int* tri_live) {
     if (ctl[kDel] == 0) return;
+    if (t_rd) t = (int)*t_rd + 1;
     const int nd = (int)ctl[kNdel];
     for (int q = blockIdx.x; q < nd; q += gridDim.x) {
         const int e = dlist[q];
@@ -1596,7 +1600,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
     hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
-                       C->force_rebuild ? 1 : 0, del_any, in.t, C->d_touched[1 - tsel], tsel, fext);
+                       C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
     if (M)
         hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
                            M->d_g2l, c->d_fext);
@@ -1621,7 +1625,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         }
         // incremental update (steps after a deletion)
         hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
-                           C->d_dlist);
+                           c->g_trd, C->d_dlist);
         AppendIn A;
         A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
         A.el_ni_ptr = C->d_el_ni_ptr; A.el_ni = C->d_el_ni; A.el_nj_ptr = C->d_el_nj_ptr; A.el_nj = C->d_el_nj;
@@ -1630,7 +1634,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
         A.pair_reg = C->d_pair_reg;
         A.tri_reg = C->tri_reg;
         hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
-                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+                           c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
     }
     if (C->nseg > 0) {
         const Seg* sg = (const Seg*)C->d_seg;
@@ -1668,6 +1672,22 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
+}
+
+// Graph mode (hakai_step): a step may be captured when its contact work is the same launch sequence
+// every step -- no mirror (host-side capacity decisions), no full rebuild, no initial velocity,
+// consecutive step numbers. contact_step's host state then changes only by the tsel flip and
+// last_t, which contact_graph_advance replays for a cached graph's two steps.
+bool contact_graph_ok(const hakai_ctx* c, double t) {
+    const Contact* C = c->contact;
+    if (!C) return true;
+    return !C->mir && !C->force_rebuild && !C->always_rebuild && !C->use_velo0 && (long long)t == C->last_t + 1;
+}
+
+void contact_graph_advance(hakai_ctx* c, double t_last) {
+    Contact* C = c->contact;
+    if (!C) return;
+    C->last_t = (long long)t_last;  // two steps: tsel flipped twice
 }
 
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
@@ -2320,11 +2340,13 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
 extern "C" {
 
 int hakai_set_contact(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     return hakai_set_contact_cp(c, contact_flag, element_instance, 0, nullptr, nullptr, nullptr);
 }
 
 int hakai_set_contact_cp(hakai_ctx* c, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
                          const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
         return fail(HAKAI_ERR_ARG, "set_contact_cp: bad contact-pair arrays");
@@ -2344,6 +2366,7 @@ int hakai_set_contact_global(hakai_ctx* c, int32_t contact_flag, int64_t nNode, 
                              const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
                              const int64_t* rank_elem_off, int32_t n_cp, const int32_t* cp_instance,
                              const int64_t* cp_elem_off, const int64_t* cp_elems) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (n_cp < 0 || (n_cp > 0 && (!cp_instance || !cp_elem_off || !cp_elems)))
         return fail(HAKAI_ERR_ARG, "set_contact_global: bad contact-pair arrays");
@@ -2401,6 +2424,7 @@ int hakai_set_contact_global(hakai_ctx* c, int32_t contact_flag, int64_t nNode, 
 }
 
 int hakai_set_contact_params(hakai_ctx* c, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     hkc::Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "set_contact_params before set_contact");
@@ -2469,6 +2493,7 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
 }
 
 int hakai_contact_force(hakai_ctx* c, double t, double d_time, double* external_force) {
+    if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !external_force) return fail(HAKAI_ERR_ARG, "null");
     if (!c->contact) return fail(HAKAI_ERR_STATE, "contact_force before set_contact");
     if (!c->state_ok) return fail(HAKAI_ERR_STATE, "contact_force before reset/upload_state");

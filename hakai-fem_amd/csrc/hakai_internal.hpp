@@ -99,6 +99,19 @@ struct hakai_ctx {
     std::vector<EventPair> ev_pending;
     double k_ms[HAKAI_K_COUNT] = {0, 0, 0, 0};
     long long k_n[HAKAI_K_COUNT] = {0, 0, 0, 0};
+    // graph mode (hakai_step): `graph` steps (even) captured in one hipGraph per starting parity
+    // (cur), plus a 2-step graph for the tail; the step number is read from a device counter
+    // instead of kernel arguments. Slot [g][p]: g 0 = `graph` steps, 1 = 2 steps; p = parity.
+    double* d_tstep = nullptr;         // [2] counter slots (slot 1-cur: previous step's number)
+    const double* g_trd = nullptr;     // non-null while a step is captured: its counter slot
+    hipGraphExec_t g_exec[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    double g_dt[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    long long g_epoch[2][2] = {{-1, -1}, {-1, -1}};
+    int g_len[2][2] = {{0, 0}, {0, 0}};
+    long long epoch = 0;               // bumped by every call that may change buffers or settings
+    long long tdev_next = -1;          // the step the device counter is valid for (-1: unknown)
+    int graph = 16;                    // tuning "graph": steps per graph (even), 0 = no capture
+    long long graph_steps = 0;         // steps run from graphs (tests, stats)
     // multi-GPU
     hkc::Comm* comm = nullptr;
 };
@@ -127,5 +140,8 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host);
 int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
 int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack the mirror block of the next step
 int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
+void graph_invalidate(hakai_ctx* c);                      // drop captured step graphs (hakai_step)
+bool contact_graph_ok(const hakai_ctx* c, double t);       // step t's contact work can be captured
+void contact_graph_advance(hakai_ctx* c, double t_last);   // host state after a cached graph's steps
 int contact_tuning(hakai_ctx* c, const char* key, long long value);  // "contact_*" tuning keys
 }  // namespace hkc

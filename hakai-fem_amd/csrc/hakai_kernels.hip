@@ -329,10 +329,23 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     }
 }
 
+// Graph mode (hipGraph of two steps, hakai_step): the step number is not a kernel argument but a
+// device counter. Every kernel of a step reads slot 1-p (the previous step's number) and adds 1;
+// the element kernel, the last of the step, stores that number into slot p, which the next step
+// reads. A divergent lane stores it, so it is an ordinary vector store.
+__device__ __forceinline__ void graph_step(ElemArgs& a) {
+    if (a.t_rd) {
+        const double tp = *a.t_rd;
+        a.step_i = (int)tp + 1;
+        if (a.t_wr && blockIdx.x == 0 && threadIdx.x == 0) *a.t_wr = tp + 1.0;
+    }
+}
+
 // One batch of 32 elements per block (simple form; used by the literal drop-in and for A/B).
 template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
+    graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
     const long long e = (long long)xcd_remap(blockIdx.x, gridDim.x) * kEPB + grp;
@@ -350,6 +363,7 @@ template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
+    graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
     if (LDS_MATS) {
@@ -653,6 +667,7 @@ __global__ __launch_bounds__(kBlock) void k_bc(BCArgs a) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.n) return;
     const int g = a.grp[i];
+    const double ct = a.t_rd ? (*a.t_rd + 1.0) * a.dt : a.ct;  // t * d_time, as on the host
     double amp = 1.0;
     const int na = a.amp_n[g];
     if (na > 0) {
@@ -660,11 +675,11 @@ __global__ __launch_bounds__(kBlock) void k_bc(BCArgs a) {
         const double* av = a.amp_v + a.amp_off[g];
         int ti = 0;
         for (int j = 0; j < na - 1; ++j)
-            if (a.ct >= at[j] && a.ct <= at[j + 1]) {
+            if (ct >= at[j] && ct <= at[j + 1]) {
                 ti = j;
                 break;
             }
-        amp = av[ti] + (av[ti + 1] - av[ti]) * (a.ct - at[ti]) / (at[ti + 1] - at[ti]);
+        amp = av[ti] + (av[ti + 1] - av[ti]) * (ct - at[ti]) / (at[ti + 1] - at[ti]);
     }
     a.out[a.dof[i]] = a.val[i] * amp;
 }
@@ -672,6 +687,15 @@ __global__ __launch_bounds__(kBlock) void k_bc(BCArgs a) {
 hipError_t launch_bc(const BCArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_bc, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+__global__ void k_set_step(double* slot, double t_prev) {
+    if (threadIdx.x == 0) *slot = t_prev;
+}
+
+hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_step, dim3(1), dim3(64), 0, s, slot, t_prev);
     return hipGetLastError();
 }
 

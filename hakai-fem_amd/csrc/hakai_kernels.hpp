@@ -28,6 +28,8 @@ struct ElemArgs {
     long long ld;          // Gauss-point stride of the SoA arrays (8 nEp)
     int* del_step;         // [nEp+1] step at which each element was deleted (0 = never); [nEp] = dump
     int step_i;            // current step number
+    const double* t_rd;    // graph mode: step number = *t_rd + 1 (read on device), else step_i
+    double* t_wr;          // graph mode: block 0 stores *t_rd + 1 here (the next step's t_rd)
     int any_plastic;       // some material has a *Plastic table (eqps/yield are live)
     int variant;           // occupancy variant of the simple kernel: min waves per SIMD (2, 3, 4)
     int pipe_blocks;        // > 0: persistent pipelined kernel with this many blocks
@@ -65,12 +67,16 @@ struct BCArgs {
     const double* amp_v;
     double* out;           // disp_new
     double ct;             // current time t*d_time
+    const double* t_rd;    // graph mode: ct = (*t_rd + 1) * dt (read on device), else ct
+    double dt;
 };
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
 hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s);
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s);
 hipError_t launch_bc(const BCArgs& a, hipStream_t s);
+// graph mode: the step counter slot read by the first step of a captured graph
+hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s);
 
 // Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
 hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, long long cstride, double* Q,

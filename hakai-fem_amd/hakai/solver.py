@@ -190,6 +190,12 @@ class Solver:
     def set_tuning(self, key: str, value: int):
         check(self.L.hakai_set_tuning(self.ctx, key.encode(), int(value)))
 
+    def graph_steps(self) -> int:
+        """Steps run from captured hipGraphs so far (hakai_graph_steps)."""
+        n = I64(0)
+        check(self.L.hakai_graph_steps(self.ctx, ctypes.byref(n)))
+        return n.value
+
     # -- multi-GPU ---------------------------------------------------------------------------------
     def comm_init(self, rank: int, nranks: int, uid: bytes):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)

@@ -112,6 +112,12 @@ int hakai_download_state(hakai_ctx* ctx, hakai_state_t* st);
  * t = t_first .. t_first+n_steps-1 (t is Float64 like `for t = 1:time_num`). Asynchronous with
  * respect to the host until hakai_sync / a download. */
 int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
+/* Launch-bound step loops run from hipGraphs: hakai_step captures two steps per graph (one graph
+ * per starting parity, reused for the whole run) whenever the step is the same launch sequence
+ * every time -- no multi-GPU exchange, no profiling, contact in its steady state -- and keeps the
+ * call's last step in stream mode. Results are bit-identical to stream mode
+ * (hakai_set_tuning(ctx, "graph", 0) turns capture off). Returns the steps run from graphs. */
+int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
 int hakai_deleted(hakai_ctx* ctx, int64_t* n_deleted, int64_t* log, int64_t cap);
