@@ -108,7 +108,7 @@ int hakai_reset_state(hakai_ctx* ctx, int64_t n_ic, const int64_t* ic_dofs, cons
 int hakai_upload_state(hakai_ctx* ctx, const hakai_state_t* st);
 int hakai_download_state(hakai_ctx* ctx, hakai_state_t* st);
 
-/* n_steps iterations of the time-loop body v2/HAKAI_j.jl:497-764 (contact-free decks) for
+/* n_steps iterations of the time-loop body v2/HAKAI_j.jl:497-764 (with contact if enabled) for
  * t = t_first .. t_first+n_steps-1 (t is Float64 like `for t = 1:time_num`). Asynchronous with
  * respect to the host until hakai_sync / a download. */
 int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
