@@ -125,6 +125,9 @@ def main():
     if a.preload >= 0:
         preload = a.preload
     sv = Solver(model, device=local_rank if multi else 0, diag_M=diag)
+    # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region is
+    # stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
+    sv.set_tuning("graph", 0)
     if multi:
         uid = comm_unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")

@@ -337,6 +337,13 @@ int hakai_create(hakai_ctx** out, int device) {
     c->device = device;
     if (const char* v = std::getenv("HAKAI_ELEM_MINW")) c->elem_variant = std::atoi(v);
     if (const char* v = std::getenv("HAKAI_PIPE_BLOCKS")) c->pipe_blocks = std::atoi(v);
+    // HAKAI_GRAPH=n: steps per captured graph (0 = stream mode). rocprofv3 --kernel-trace crashes
+    // the host process on any hipGraph launch with this ROCm (tools/graph_probe.hip alone
+    // reproduces it), so the profiling scripts run with HAKAI_GRAPH=0.
+    if (const char* v = std::getenv("HAKAI_GRAPH")) {
+        const int g = std::atoi(v);
+        c->graph = (g >= 0 && g <= 1024 && !(g & 1)) ? g : 0;
+    }
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

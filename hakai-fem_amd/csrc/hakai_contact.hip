@@ -148,6 +148,9 @@ struct Contact {
     bool force_rebuild = true;
     bool always_rebuild = false;    // tuning/testing: full rebuild every step (no incremental update)
     long long last_t = -1;
+    // launch grids sized at setup from the contact model (small decks: few blocks, so the ~20
+    // per-step kernels are not dominated by dispatching idle workgroups); every loop is grid-stride
+    int g_seg = 256, g_ev = 1024, g_tri = 4096, g_node = 256, g_del = 1024, g_reset = 64;
     // hash grid over i-nodes
     int htot = 0;
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
@@ -506,15 +509,15 @@ __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsig
 
 __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                 const int* nj_live, const int* ni_node, const int* nj_node,
-                                                unsigned long long* bbox) {
-    const Seg sg = segs[blockIdx.x / kSegBlocks];
-    const int sub = blockIdx.x % kSegBlocks;
+                                                unsigned long long* bbox, int sb) {
+    const Seg sg = segs[blockIdx.x / sb];
+    const int sub = blockIdx.x % sb;
     const bool side_i = sg.side == 0;
     const int* node = side_i ? ni_node : nj_node;
     const int* lst = (side_i ? ni_live : nj_live) + reg[2 * sg.region];
     const int cnt = reg[2 * sg.region + 1];
     unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
-    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += kSegBlocks * kB) {
+    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += sb * kB) {
         double p[3];
         pos(s, node[lst[q]], p);
         for (int d = 0; d < 3; ++d) {
@@ -550,16 +553,16 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
 }
 
 // cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts.
-// kSegBlocks blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
+// sb blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
 __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                const int* ni_pair, const int* ni_node, const PairParam* par,
                                                const unsigned long long* bbox, int* qbucket, long long* ni_map,
-                                               int* bcnt) {
+                                               int* bcnt, int sb) {
 #pragma clang fp contract(off)
-    const Seg sg = segs[blockIdx.x / kSegBlocks];
+    const Seg sg = segs[blockIdx.x / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
-    for (int q = (blockIdx.x % kSegBlocks) * kB + (int)threadIdx.x; q < n; q += kSegBlocks * kB) {
+    for (int q = (blockIdx.x % sb) * kB + (int)threadIdx.x; q < n; q += sb * kB) {
         const int k = ni_live[base + q];
         const int pr = ni_pair[k];
         const Range r = pair_range(bbox + 12 * pr);
@@ -583,11 +586,11 @@ __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const 
 }
 
 __global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* qbucket, const int* boff, int* bcnt, int* blist) {
-    const Seg sg = segs[blockIdx.x / kSegBlocks];
+                                                const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
+    const Seg sg = segs[blockIdx.x / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
-    for (int q = (blockIdx.x % kSegBlocks) * kB + (int)threadIdx.x; q < n; q += kSegBlocks * kB) {
+    for (int q = (blockIdx.x % sb) * kB + (int)threadIdx.x; q < n; q += sb * kB) {
         const int b = qbucket[base + q];
         if (b < 0) continue;
         const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
@@ -1599,7 +1602,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
-    hipLaunchKernelGGL(k_ct_reset, dim3(64), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
+    hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
                        C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
     if (M)
         hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
@@ -1624,7 +1627,7 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
                                C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
         }
         // incremental update (steps after a deletion)
-        hipLaunchKernelGGL(k_ct_find_del, dim3(1024), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
+        hipLaunchKernelGGL(k_ct_find_del, dim3(C->g_del), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
                            c->g_trd, C->d_dlist);
         AppendIn A;
         A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
@@ -1638,33 +1641,34 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     }
     if (C->nseg > 0) {
         const Seg* sg = (const Seg*)C->d_seg;
-        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox);
-        hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                           C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt);
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_seg);
+        hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
+                           C->g_seg);
     }
     size_t tb = C->tmp_bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
     if (C->nseg > 0)
-        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * kSegBlocks), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
-                           C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist);
+        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
+                           C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
     if (C->n_tri > 0) {
         hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, 2048))),
                            dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
                            C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ctl, (TriRec*)C->d_cand,
                            C->cand_cap);
-        hipLaunchKernelGGL(k_ct_tri, dim3(4096), dim3(128), 0, s, in, C->d_ctl, (const TriRec*)C->d_cand, C->cand_cap,
+        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, (const TriRec*)C->d_cand, C->cand_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
     }
-    const unsigned ge = (unsigned)std::min<long long>((4 * C->cap + kB - 1) / kB, 1024);
+    const unsigned ge = (unsigned)C->g_ev;
     hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel);
-    hipLaunchKernelGGL(k_ct_alloc, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
+    hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
-    hipLaunchKernelGGL(k_ct_sum, dim3(256), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
+    hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
                        C->d_terms, fext);
     if (M)
         hipLaunchKernelGGL(k_mir_fext_copy, dim3(64), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], M->d_g2l,
@@ -2027,6 +2031,22 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         C->cap = (C->cap + kEvShards - 1) / kEvShards * kEvShards;
     }
     C->tcap = std::min<long long>(H.nN, 4 * C->cap);
+    {  // launch grids (see Contact::g_*): large models keep the full grids
+        auto clampi = [](long long v, long long lo, long long hi) { return (int)std::max(lo, std::min(hi, v)); };
+        long long ci0 = 0, ct0 = 0, maxseg = 1;
+        for (int p = 0; p < C->npairs; ++p) {
+            ci0 += C->pair_counts[3 * p];
+            ct0 += C->pair_counts[3 * p + 1];
+        }
+        for (int q = 0; q < C->nseg; ++q) maxseg = std::max<long long>(maxseg, seg[8 * q + 1] - seg[8 * q]);
+        C->g_seg = clampi((maxseg + kB - 1) / kB, 1, kSegBlocks);
+        C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
+        C->g_tri = clampi((32 * ct0 / 4 + 127) / 128, 32, 4096);  // >= 64 waves: every event shard
+        C->g_node = clampi((2 * ci0 + kB - 1) / kB, 4, 256);
+        C->g_del = clampi((C->nE / 4 + kB - 1) / kB, 1, 1024);
+        C->g_reset = clampi((std::max<long long>(std::max<long long>(kEvShards, 12LL * C->npairs), 2 * ci0) + kB - 1) / kB,
+                            1, 64);
+    }
     // live-list regions: i-node segments, j-node segments, then the triangle list; tiles of
     // kTile entries inside one region each (full rebuild)
     std::vector<Tile> tiles;

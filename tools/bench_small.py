@@ -15,6 +15,8 @@ sys.path[:0] = [os.path.join(ROOT, "hakai-fem_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--only", default="", help="run the cases whose name contains this")
+    ap.add_argument("--graphs", default="0,2,16,64", help="graph tuning values to compare")
     a = ap.parse_args()
     from hakai import mesh
     from hakai.solver import Solver
@@ -26,7 +28,9 @@ def main():
                                                                                 impactor=(12, 12, 12))),
     ]
     for name, m in cases:
-        for graph in (0, 2, 16, 64):
+        if a.only not in name:
+            continue
+        for graph in (int(g) for g in a.graphs.split(",")):
             with Solver(m, device=0) as sv:
                 sv.set_tuning("graph", graph)
                 sv.step(1, 50)

@@ -3,6 +3,7 @@
 # Env switches (pass inline in the gpurun command): SWEEP="variants", PROF=1, NOTEST=1.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+export HAKAI_GRAPH=0  # rocprofv3 cannot trace hipGraph launches
 mkdir -p gpurun_out
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ -z "$NOTEST" ]; then
