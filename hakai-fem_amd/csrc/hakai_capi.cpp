@@ -805,10 +805,11 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     return 0;
 }
 
-// Steps t and t+1 can come from a graph: same launch sequence every step, nothing host-side that
-// depends on the step (no multi-GPU exchange, no profiling events, no uploaded Q), and contact in
-// its steady state. The step number comes from a device counter; every pointer argument is fixed
-// for a given starting parity (cur), so one graph per parity serves the whole run.
+// A run of steps starting at t can come from a graph: same launch sequence every step, nothing
+// host-side that depends on the step (no multi-GPU exchange, no profiling events, no uploaded Q),
+// and contact in its steady state. The step number comes from a device counter; every pointer
+// argument is fixed for a given starting parity (cur), so one graph per parity serves the whole
+// run. A failed capture leaves the context's host state advanced: the call returns the error.
 static bool graph_eligible(const hakai_ctx* c, double t) {
     return c->graph && !c->comm && !c->prof && !c->q_from_buf && c->nE > 0 && hkc::contact_graph_ok(c, t);
 }
