@@ -230,7 +230,8 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.step_i = 0;
     ea.any_plastic = c->any_plastic ? 1 : 0;
     ea.variant = c->elem_variant;
-    ea.pipe_blocks = c->pipe_blocks;
+    // nEp / 32 = batches of 32 elements (kEPB); small meshes take the one-batch-per-block kernel
+    ea.pipe_blocks = (c->nEp / 32 >= (long long)c->pipe_min * c->pipe_blocks) ? c->pipe_blocks : 0;
     ea.pipe_map = c->pipe_map;
     ea.gp_nt = c->gp_nt;
     ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
@@ -961,6 +962,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "elem_gp_nt")) {
         if (value < 0 || value > 3) return fail(HAKAI_ERR_ARG, "elem_gp_nt must be 0..3 (bit 0 loads, bit 1 stores)");
         c->gp_nt = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "elem_pipe_min")) {
+        if (value < 0 || value > 1024) return fail(HAKAI_ERR_ARG, "elem_pipe_min out of range");
+        c->pipe_min = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_map")) {

@@ -57,6 +57,8 @@ struct hakai_ctx {
     int elem_variant = 2;        // k_element occupancy variant (HAKAI_ELEM_MINW)
     int pipe_blocks = 512;       // persistent pipelined element kernel grid (0 = simple kernel)
     int pipe_map = 1;            // batch schedule of the persistent kernel (0 per block, 1 per XCD)
+    int pipe_min = 2;            // persistent kernel only with >= pipe_min batches per block (small
+                                 // meshes: one batch per block, the pipeline only adds latency)
     int nodal_early = 1;         // nodal kernel loads its node operands before the gather
     int gp_nt = 3;               // element kernel: Gauss-point state nontemporal (bit 0 loads, bit 1 stores)
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally

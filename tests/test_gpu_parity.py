@@ -217,17 +217,20 @@ def test_hakai_driver_async_output_equals_sync(tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("tuning", [{"fe_layout": 1}, {"elem_map": 1}, {"fe_layout": 1, "elem_map": 1},
                                     {"elem_pipe_blocks": 0, "fe_layout": 1}, {"elem_map": 0},
-                                    {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1}])
+                                    {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1},
+                                    {"elem_pipe_min": 2}])
 def test_tuning_variants_bitexact(tuning):
     """Force layouts (AoS rows / component SoA) and batch schedules change only where bytes
     live and which block computes what: the trajectory is bit-identical to the default."""
     m = fast_deletion_bar(3, 3, 10)
     n = 1200
     with Solver(m) as sv:
+        sv.set_tuning("elem_pipe_min", 0)  # the persistent kernel even on this small mesh
         sv.step(1, n)
         ref = sv.download()
         rdel = [tuple(x) for x in sv.deleted()]
     with Solver(m) as sv:
+        sv.set_tuning("elem_pipe_min", 0)
         for k, v in tuning.items():
             sv.set_tuning(k, v)
         sv.step(1, 500)

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--only", default="", help="run the cases whose name contains this")
     ap.add_argument("--graphs", default="0,2,16,64", help="graph tuning values to compare")
+    ap.add_argument("--tuning", default="", help="extra tuning key=value[,key=value] for every context")
     a = ap.parse_args()
     from hakai import mesh
     from hakai.solver import Solver
@@ -33,6 +34,9 @@ def main():
         for graph in (int(g) for g in a.graphs.split(",")):
             with Solver(m, device=0) as sv:
                 sv.set_tuning("graph", graph)
+                for kv in filter(None, a.tuning.split(",")):
+                    k, v = kv.split("=")
+                    sv.set_tuning(k, int(v))
                 sv.step(1, 50)
                 sv.sync()
                 g0 = sv.graph_steps()
@@ -43,6 +47,7 @@ def main():
                 t2 = time.perf_counter()
                 gs = sv.graph_steps() - g0
             print(json.dumps({"case": name, "elements": m.nElement, "steps": a.steps, "graph": graph,
+                              "tuning": a.tuning,
                               "graph_steps": gs, "us_per_step": round((t2 - t0) / a.steps * 1e6, 2),
                               "host_enqueue_us_per_step": round((t1 - t0) / a.steps * 1e6, 2),
                               "contact": bool(getattr(m, "contact_flag", 0))}), flush=True)
