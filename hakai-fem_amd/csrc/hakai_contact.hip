@@ -585,6 +585,25 @@ __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const 
     }
 }
 
+// Exclusive scan of the bucket counts for small bucket tables (n <= kSmallScan): one block of
+// 1024 threads, each scanning a contiguous run. It replaces the two-kernel device-wide scan, whose
+// launches dominate the contact step of small decks ("Launch-bound step loops").
+constexpr int kSmallScan = 32768;
+__global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) {
+    __shared__ int s_w[16];
+    const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int a = (int)threadIdx.x * per, b = min(n, a + per);
+    int sum = 0;
+    for (int i = a; i < b; ++i) sum += in[i];
+    int total;
+    int run = block_excl_scan(sum, s_w, total);
+    for (int i = a; i < b; ++i) {
+        const int v = in[i];
+        out[i] = run;
+        run += v;
+    }
+}
+
 __global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
                                                 const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
     const Seg sg = segs[blockIdx.x / sb];
@@ -1647,8 +1666,12 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
                            C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
                            C->g_seg);
     }
-    size_t tb = C->tmp_bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
+    if (C->htot + 1 <= kSmallScan) {
+        hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, s, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
+    } else {
+        size_t tb = C->tmp_bytes;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
+    }
     if (C->nseg > 0)
         hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
                            C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
