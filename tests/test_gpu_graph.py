@@ -81,3 +81,29 @@ def test_graph_contact_with_deletion_bitexact(flag, per):
         for k in ("disp", "integ_stress", "element_flag"):
             assert np.array_equal(getattr(a, k), getattr(b, k)), k
         assert sv1.graph_steps() > 150
+
+
+def test_graph_settings(monkeypatch):
+    """Odd step counts are refused; HAKAI_GRAPH sets the default of new contexts; profiling events
+    keep the loop in stream mode."""
+    import hakai
+    m = mesh.tensile5e_model()
+    with Solver(m, device=0) as sv:
+        with pytest.raises(hakai.HakaiError):
+            sv.set_tuning("graph", 3)
+        sv.step(1, 100)
+        assert sv.graph_steps() > 0  # default on
+        n0 = sv.graph_steps()
+        sv.profile(True)
+        sv.step(101, 100)
+        sv.profile(False)
+        assert sv.graph_steps() == n0
+    monkeypatch.setenv("HAKAI_GRAPH", "0")
+    with Solver(m, device=0) as sv:
+        sv.step(1, 100)
+        assert sv.graph_steps() == 0
+    monkeypatch.setenv("HAKAI_GRAPH", "4")
+    with Solver(m, device=0) as sv:
+        sv.step(1, 100)
+        # 24 graphs of 4 steps, one 2-step tail graph, then the call's last 2 steps in stream mode
+        assert sv.graph_steps() == 98
