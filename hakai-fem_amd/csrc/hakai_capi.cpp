@@ -95,6 +95,7 @@ static void free_model(hakai_ctx* c) {
 }
 
 static void free_bc(hakai_ctx* c) {
+    dfree(c->d_bc_of_dof);
     dfree(c->d_bc_dof);
     dfree(c->d_bc_grp);
     dfree(c->d_bc_val);
@@ -543,6 +544,15 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
         HIPCHK(hipMemcpyAsync(c->d_amp_t, bc->amp_time, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_amp_v, bc->amp_value, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
     }
+    // small meshes: per-dof entry table, so the nodal kernel applies the BCs itself (hakai_step)
+    if (!dof.empty() && c->nN <= kFuseBcMaxNodes) {
+        std::vector<int> of(3 * (size_t)c->nN, -1);
+        for (size_t i = 0; i < dof.size(); ++i)
+            if (dof[i] >= 0 && (size_t)dof[i] < of.size()) of[(size_t)dof[i]] = (int)i;
+        HIPCHK(dalloc(&c->d_bc_of_dof, of.size()));
+        HIPCHK(hipMemcpyAsync(c->d_bc_of_dof, of.data(), of.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
@@ -750,6 +760,27 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     na.fext = nullptr;
     na.nN = c->nN;
     na.dt = d_time;
+    na.bc_of_dof = nullptr;
+    hk::BCArgs ba;
+    ba.dof = c->d_bc_dof;
+    ba.grp = c->d_bc_grp;
+    ba.val = c->d_bc_val;
+    ba.n = c->nbc;
+    ba.amp_n = c->d_amp_n;
+    ba.amp_off = c->d_amp_off;
+    ba.amp_t = c->d_amp_t;
+    ba.amp_v = c->d_amp_v;
+    ba.out = c->d_u[1 - c->cur];
+    ba.ct = t * d_time;
+    ba.t_rd = c->g_trd;
+    ba.dt = d_time;
+    // one GPU, small mesh: the nodal kernel applies the BCs (multi-GPU redoes interface nodes
+    // after the nodal kernel, so the BCs must come after that)
+    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_dof && c->fuse_bc && !c->comm;
+    if (fuse_bc) {
+        na.bc_of_dof = c->d_bc_of_dof;
+        na.bc = ba;
+    }
     int rc = 0;
     if (c->contact) {  // contact force into external_force (:500-560)
         hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
@@ -767,20 +798,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     rc = hkc::comm_post_nodal(c, d_time);
     if (rc) return rc;
     // boundary conditions (:585-617)
-    if (c->nbc > 0) {
-        hk::BCArgs ba;
-        ba.dof = c->d_bc_dof;
-        ba.grp = c->d_bc_grp;
-        ba.val = c->d_bc_val;
-        ba.n = c->nbc;
-        ba.amp_n = c->d_amp_n;
-        ba.amp_off = c->d_amp_off;
-        ba.amp_t = c->d_amp_t;
-        ba.amp_v = c->d_amp_v;
-        ba.out = c->d_u[1 - c->cur];
-        ba.ct = t * d_time;
-        ba.t_rd = c->g_trd;
-        ba.dt = d_time;
+    if (c->nbc > 0 && !fuse_bc) {
         hkc::prof_begin(c, HAKAI_K_BC, &ep);
         HIPCHK(hk::launch_bc(ba, s));
         hkc::prof_end(c, &ep);
@@ -962,6 +980,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "elem_gp_nt")) {
         if (value < 0 || value > 3) return fail(HAKAI_ERR_ARG, "elem_gp_nt must be 0..3 (bit 0 loads, bit 1 stores)");
         c->gp_nt = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "fuse_bc")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fuse_bc must be 0 or 1");
+        c->fuse_bc = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_pipe_min")) {

@@ -20,6 +20,8 @@ struct EventPair {
     int kernel;
 };
 
+constexpr long long kFuseBcMaxNodes = 1 << 18;  // BCs fused into k_nodal up to this many nodes
+
 struct hakai_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -74,6 +76,8 @@ struct hakai_ctx {
     int* d_amp_off = nullptr;
     double* d_amp_t = nullptr;
     double* d_amp_v = nullptr;
+    int* d_bc_of_dof = nullptr;  // [3nN] resolved BC entry per dof (-1 none); small meshes only
+    int fuse_bc = 1;             // tuning "fuse_bc": the nodal kernel applies the BCs (one GPU)
     // state extras
     double* d_qbuf = nullptr;
     bool q_from_buf = false;

@@ -540,6 +540,28 @@ hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream
 // The node's own operands are loaded FIRST, so they are in flight together with the incidence
 // indices; loaded after the gather they add a third dependent memory round trip (measured with
 // tools/nodal_probe.hip: 0.174 -> 0.141 ms on the C3 node count).
+// Prescribed value of resolved BC entry i at the step's time (v2/HAKAI_j.jl:585-617): the entry's
+// value times its group's piecewise-linear amplitude, first segment extrapolated.
+__device__ __forceinline__ double bc_value(const BCArgs& a, int i) {
+#pragma clang fp contract(off)
+    const int g = a.grp[i];
+    const double ct = a.t_rd ? (*a.t_rd + 1.0) * a.dt : a.ct;  // t * d_time, as on the host
+    double amp = 1.0;
+    const int na = a.amp_n[g];
+    if (na > 0) {
+        const double* at = a.amp_t + a.amp_off[g];
+        const double* av = a.amp_v + a.amp_off[g];
+        int ti = 0;
+        for (int j = 0; j < na - 1; ++j)
+            if (ct >= at[j] && ct <= at[j + 1]) {
+                ti = j;
+                break;
+            }
+        amp = av[ti] + (av[ti + 1] - av[ti]) * (ct - at[ti]) / (at[ti + 1] - at[ti]);
+    }
+    return a.val[i] * amp;
+}
+
 struct NodeIn {
     double m, uc[3], up[3], f[3];
 };
@@ -555,6 +577,7 @@ __device__ __forceinline__ void nodal_load(const NodalArgs& a, long long n, Node
     }
 }
 
+template <bool BCF>
 __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, const NodeIn& in, double Q0, double Q1,
                                              double Q2) {
 #pragma clang fp contract(off)
@@ -567,14 +590,19 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double up = in.up[c];
-        a.u_pre_out[3 * n + c] = inv * (in.f[c] - Q[c] + mdt2 * (2.0 * in.uc[c] - up) + dC / 2.0 / dt * up);
+        double v = inv * (in.f[c] - Q[c] + mdt2 * (2.0 * in.uc[c] - up) + dC / 2.0 / dt * up);
+        if (BCF) {  // what k_bc would overwrite afterwards
+            const int bi = a.bc_of_dof[3 * n + c];
+            if (bi >= 0) v = bc_value(a.bc, bi);
+        }
+        a.u_pre_out[3 * n + c] = v;
     }
 }
 
 // MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer. Compile-time modes keep the
 // kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
 // which serialises the early node loads with the gather again.
-template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false>
+template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false, bool BCF = false>
 __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
     const unsigned lb = a.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
@@ -616,44 +644,51 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
         }
     }
     if (!EARLY) nodal_load<FEXT>(a, n, in);
-    nodal_update(a, n, in, Q0, Q1, Q2);
+    nodal_update<BCF>(a, n, in, Q0, Q1, Q2);
 }
 
-template <bool FEXT, bool AOS, bool EARLY>
+template <bool FEXT, bool AOS, bool EARLY, bool BCF>
 static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.qbuf)
-        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8 && a.fe_nt)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
-template <bool FEXT, bool AOS>
+template <bool FEXT, bool AOS, bool BCF>
 static void launch_nodal_f(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.early)
-        launch_nodal_e<FEXT, AOS, true>(a, grid, s);
+        launch_nodal_e<FEXT, AOS, true, BCF>(a, grid, s);
     else
-        launch_nodal_e<FEXT, AOS, false>(a, grid, s);
+        launch_nodal_e<FEXT, AOS, false, BCF>(a, grid, s);
 }
 
-template <bool FEXT>
+template <bool FEXT, bool BCF>
 static void launch_nodal_a(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.cstride == 1)
-        launch_nodal_f<FEXT, true>(a, grid, s);
+        launch_nodal_f<FEXT, true, BCF>(a, grid, s);
     else
-        launch_nodal_f<FEXT, false>(a, grid, s);
+        launch_nodal_f<FEXT, false, BCF>(a, grid, s);
 }
 
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
     if (a.nN <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((a.nN + kBlock - 1) / kBlock);
-    if (a.fext)
-        launch_nodal_a<true>(a, grid, s);
-    else
-        launch_nodal_a<false>(a, grid, s);
+    if (a.bc_of_dof) {
+        if (a.fext)
+            launch_nodal_a<true, true>(a, grid, s);
+        else
+            launch_nodal_a<false, true>(a, grid, s);
+    } else {
+        if (a.fext)
+            launch_nodal_a<true, false>(a, grid, s);
+        else
+            launch_nodal_a<false, false>(a, grid, s);
+    }
     return hipGetLastError();
 }
 
@@ -663,25 +698,9 @@ hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
 // in-order overwrite leaves behind.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_bc(BCArgs a) {
-#pragma clang fp contract(off)
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.n) return;
-    const int g = a.grp[i];
-    const double ct = a.t_rd ? (*a.t_rd + 1.0) * a.dt : a.ct;  // t * d_time, as on the host
-    double amp = 1.0;
-    const int na = a.amp_n[g];
-    if (na > 0) {
-        const double* at = a.amp_t + a.amp_off[g];
-        const double* av = a.amp_v + a.amp_off[g];
-        int ti = 0;
-        for (int j = 0; j < na - 1; ++j)
-            if (ct >= at[j] && ct <= at[j + 1]) {
-                ti = j;
-                break;
-            }
-        amp = av[ti] + (av[ti + 1] - av[ti]) * (ct - at[ti]) / (at[ti + 1] - at[ti]);
-    }
-    a.out[a.dof[i]] = a.val[i] * amp;
+    a.out[a.dof[i]] = bc_value(a, i);
 }
 
 hipError_t launch_bc(const BCArgs& a, hipStream_t s) {

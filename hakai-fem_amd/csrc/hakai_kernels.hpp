@@ -38,6 +38,21 @@ struct ElemArgs {
     int gp_nt;              // 1: Gauss-point state streamed with nontemporal loads/stores
 };
 
+struct BCArgs {
+    const int* dof;        // 0-based dof
+    const int* grp;
+    const double* val;
+    int n;
+    const int* amp_n;
+    const int* amp_off;
+    const double* amp_t;
+    const double* amp_v;
+    double* out;           // disp_new
+    double ct;             // current time t*d_time
+    const double* t_rd;    // graph mode: ct = (*t_rd + 1) * dt (read on device), else ct
+    double dt;
+};
+
 struct NodalArgs {
     const double* u;       // disp
     double* u_pre_out;     // in: disp_pre, out: disp_new (ping-pong buffers, no copies)
@@ -54,22 +69,10 @@ struct NodalArgs {
     int reverse;           // 1: each XCD walks its node chunk from the end (xcd_remap_rev)
     long long nN;
     double dt;
+    const int* bc_of_dof;  // small meshes, one GPU: [3nN] entry of `bc` per dof (-1 none); the
+    BCArgs bc;             // nodal kernel then applies the BCs itself (no k_bc launch)
 };
 
-struct BCArgs {
-    const int* dof;        // 0-based dof
-    const int* grp;
-    const double* val;
-    int n;
-    const int* amp_n;
-    const int* amp_off;
-    const double* amp_t;
-    const double* amp_v;
-    double* out;           // disp_new
-    double ct;             // current time t*d_time
-    const double* t_rd;    // graph mode: ct = (*t_rd + 1) * dt (read on device), else ct
-    double dt;
-};
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
 hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s);

@@ -218,7 +218,7 @@ def test_hakai_driver_async_output_equals_sync(tmp_path, monkeypatch):
 @pytest.mark.parametrize("tuning", [{"fe_layout": 1}, {"elem_map": 1}, {"fe_layout": 1, "elem_map": 1},
                                     {"elem_pipe_blocks": 0, "fe_layout": 1}, {"elem_map": 0},
                                     {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1},
-                                    {"elem_pipe_min": 2}])
+                                    {"elem_pipe_min": 2}, {"fuse_bc": 0}])
 def test_tuning_variants_bitexact(tuning):
     """Force layouts (AoS rows / component SoA) and batch schedules change only where bytes
     live and which block computes what: the trajectory is bit-identical to the default."""
