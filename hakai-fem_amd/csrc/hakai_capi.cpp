@@ -139,6 +139,22 @@ int build_devmat(const hakai_material_t& in, DevMat& o) {
     return 0;
 }
 
+// cal_Pusai_hexa (v2/HAKAI_j.jl:1895-1943): dN_i/dxi at the 8 Gauss points, out[24k + 8r + i],
+// with the reference's expression order (this file is compiled without contraction).
+void pusai_table(double out[192]) {
+    static const double delta[8][3] = {{-1.0, -1.0, -1.0}, {1.0, -1.0, -1.0}, {1.0, 1.0, -1.0}, {-1.0, 1.0, -1.0},
+                                       {-1.0, -1.0, 1.0},  {1.0, -1.0, 1.0},  {1.0, 1.0, 1.0},  {-1.0, 1.0, 1.0}};
+    const double g = 1.0 / std::sqrt(3.0);
+    for (int k = 0; k < 8; ++k) {  // gc order :1913-1920: k bits = (xi, eta, zeta) signs
+        const double gzai = (k & 4) ? g : -g, eta = (k & 2) ? g : -g, tueta = (k & 1) ? g : -g;
+        for (int i = 0; i < 8; ++i) {
+            out[24 * k + i] = 1.0 / 8.0 * delta[i][0] * (1.0 + eta * delta[i][1]) * (1.0 + tueta * delta[i][2]);
+            out[24 * k + 8 + i] = 1.0 / 8.0 * delta[i][1] * (1.0 + gzai * delta[i][0]) * (1.0 + tueta * delta[i][2]);
+            out[24 * k + 16 + i] = 1.0 / 8.0 * delta[i][2] * (1.0 + gzai * delta[i][0]) * (1.0 + eta * delta[i][1]);
+        }
+    }
+}
+
 hipStream_t ctx_stream(hakai_ctx* c) { return c->stream; }
 int ctx_device(hakai_ctx* c) { return c->device; }
 
@@ -237,6 +253,8 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.gp_nt = c->gp_nt;
     ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
     ea.nmat = c->nmat;
+    ea.exact = c->elem_exact;
+    ea.pusai = c->d_pusai;
     return ea;
 }
 
@@ -351,10 +369,23 @@ int hakai_create(hakai_ctx** out, int device) {
         delete c;
         return hip_fail(e, "hipStreamCreate");
     }
-    if (dalloc(&c->d_negjac, 1) != hipSuccess) {
+    if (dalloc(&c->d_negjac, 1) != hipSuccess || dalloc(&c->d_pusai, 192) != hipSuccess) {
+        dfree(c->d_negjac);
         delete c;
         return fail(HAKAI_ERR_DEVICE, "hipMalloc for context bookkeeping failed");
     }
+    {
+        double pus[192];
+        hkc::pusai_table(pus);
+        e = hipMemcpy(c->d_pusai, pus, sizeof pus, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            dfree(c->d_negjac);
+            dfree(c->d_pusai);
+            delete c;
+            return hip_fail(e, "hipMemcpy (Pusai table)");
+        }
+    }
+    if (const char* v = std::getenv("HAKAI_ELEM_EXACT")) c->elem_exact = std::atoi(v) ? 1 : 0;
     *out = c;
     return 0;
 }
@@ -370,6 +401,7 @@ int hakai_destroy(hakai_ctx* c) {
     hkc::free_model(c);
     hkc::free_bc(c);
     dfree(c->d_negjac);
+    dfree(c->d_pusai);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -990,6 +1022,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "elem_pipe_min")) {
         if (value < 0 || value > 1024) return fail(HAKAI_ERR_ARG, "elem_pipe_min out of range");
         c->pipe_min = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "elem_exact")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact must be 0 or 1");
+        c->elem_exact = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_map")) {

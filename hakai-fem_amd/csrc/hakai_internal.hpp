@@ -65,6 +65,8 @@ struct hakai_ctx {
     int gp_nt = 3;               // element kernel: Gauss-point state nontemporal (bit 0 loads, bit 1 stores)
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
     int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
+    int elem_exact = 0;          // tuning "elem_exact": reference-order element arithmetic
+    double* d_pusai = nullptr;   // cal_Pusai_hexa table for the exact element kernel (192 doubles)
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
     // bc

@@ -55,11 +55,14 @@ struct ElemIn {
 // behave like deleted elements), so every load and store below is unconditional: the compiler can
 // then count outstanding memory operations exactly and keep prefetches in flight across the
 // stores of the previous batch (a conditional store makes its vmcnt accounting fall back to 0).
+// EXACT: lane k stores the force of local node k (elem_step_exact); otherwise that of node
+// ref_of_sign(k) (elem_step's relative slots).
+template <bool EXACT = false>
 __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int k, ElemIn& in) {
     in.fl = a.flag[e];
     in.n = a.conn[8 * e + k];
     in.mt = a.mat[e];
-    const int kn = ref_of_sign(k);  // the node whose force lane k ends up with (elem_step)
+    const int kn = EXACT ? k : ref_of_sign(k);  // the node whose force lane k ends up with
     in.fb = a.cstride == 1 ? (int)(24 * e + 3 * kn) : (int)(3 * kn * a.nEp + e);
 }
 
@@ -100,6 +103,52 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
     }
 }
 
+// Unconditional write-back of one lane (selects, no branches): its node's force fk, its Gauss
+// point's state, the element flag and the deletion log.
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT>
+__device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, int k, const ElemIn& in, bool active,
+                                               bool kill, const double (&fk)[3], const double (&fin)[6],
+                                               const double (&eps)[6], double eqp, double ys, double tri) {
+    const long long gp = 8 * e + k, ld = a.ld;
+    double* fo = a.fe + in.fb;
+    fo[0] = active ? fk[0] : 0.0;
+    fo[a.cstride] = active ? fk[1] : 0.0;
+    fo[2 * a.cstride] = active ? fk[2] : 0.0;
+    // deletion zeroes stress/strain (:742-756); inactive elements keep their state
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        gp_st<NT>(a.stress + c * ld + gp, kill ? 0.0 : (active ? fin[c] : in.sig[c]));
+        gp_st<NT>(a.strain + c * ld + gp, kill ? 0.0 : (active ? eps[c] : in.eps[c]));
+    }
+    if (ANY_PLASTIC) {
+        gp_st<NT>(a.eqps + gp, active ? eqp : in.eqp);
+        gp_st<NT>(a.yield + gp, active ? ys : in.ys);
+    }
+    if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
+    if (DO_DELETE) {
+        a.flag[e] = kill ? 2 : (in.fl == 2 ? 0 : in.fl);        // 8 lanes, same value
+        // lane 0: the element's deletion step; lanes 1-7 of a killed element: slot nEp+1, "last step
+        // with a deletion" (contact rebuilds its live surface lists from it); others: dump slot nEp
+        int* ds = kill ? a.del_step + (k == 0 ? e : a.nEp + 1) : a.del_step + a.nEp;
+        *ds = a.step_i;
+    }
+}
+
+// Ductile table (:720-733): fracture strain at element triaxiality t_e (t_e >= 0), last row
+// outside the bracketing rows.
+__device__ __forceinline__ double ductile_fr(const DevMat* M, int nd, double t_e) {
+#pragma clang fp contract(off)
+    double fr = M->du_eps[nd - 1];
+    for (int j = 0; j + 1 < nd; ++j) {
+        if (t_e >= M->du_tri[j] && t_e < M->du_tri[j + 1]) {
+            fr = M->du_eps[j] + (M->du_eps[j + 1] - M->du_eps[j]) / (M->du_tri[j + 1] - M->du_tri[j]) *
+                                    (t_e - M->du_tri[j]);
+            break;
+        }
+    }
+    return fr;
+}
+
 // One element step for the 8 lanes of a group (every group runs it; the element flag selects what
 // is stored):  flag 1 -> full update;  flag 2 (deleted in the previous step) -> Qe and triaxiality
 // become 0 and the flag 0 (the reference skips deleted elements, :1116, and their stress is zero);
@@ -109,8 +158,6 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
                                           double* nd8, const ElemIn& in) {
     const DevMat* M = mats + in.mt;
     const bool active = in.fl == 1;
-    const long long gp = 8 * e + k;
-    const long long ld = a.ld;
     const int npp = M->npp;
     const int nd = DO_DELETE ? M->nd : 0;
     double eqp = in.eqp, ys = in.ys;
@@ -272,17 +319,7 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     if (DO_DELETE && nd > 0) {
         const double v_e = allreduce8(eqp) * 0.125;
         const double t_e = allreduce8(tri) * 0.125;
-        if (!(t_e < 0.0)) {  // ductile table (:720-733)
-            double fr = M->du_eps[nd - 1];
-            for (int j = 0; j + 1 < nd; ++j) {
-                if (t_e >= M->du_tri[j] && t_e < M->du_tri[j + 1]) {
-                    fr = M->du_eps[j] + (M->du_eps[j + 1] - M->du_eps[j]) / (M->du_tri[j + 1] - M->du_tri[j]) *
-                                            (t_e - M->du_tri[j]);
-                    break;
-                }
-            }
-            kill = active && v_e >= fr;
-        }
+        if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);  // ductile table (:720-733)
     }
 
     // ---- internal force (Qe[:,e] += detJ * Bfinal' * sigma, :1330-1340), reduce-scattered so
@@ -302,31 +339,296 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
         reduce_scatter8_rel(v, fk);
     }
     const double S = allreduce8(det * (3.0 * mean));
-
-    // ---- unconditional write-back (selects, no branches)
-    double* fo = a.fe + in.fb;
-    fo[0] = active ? fk[0] + S * bb0 : 0.0;
-    fo[a.cstride] = active ? fk[1] + S * bb1 : 0.0;
-    fo[2 * a.cstride] = active ? fk[2] + S * bb2 : 0.0;
+    fk[0] += S * bb0;
+    fk[1] += S * bb1;
+    fk[2] += S * bb2;
     if (WITH_VOL) a.vol[e] = V;
-    // deletion zeroes stress/strain (:742-756); inactive elements keep their state
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Reference-order element update (tuning key "elem_exact"): cal_stress_hexa's own arithmetic,
+// operation for operation (the oracle's restatement: oracle/hakai_oracle.c cal_BVbar_hexa,
+// cal_Bfinal, stress_one_element), so the element forces and the Gauss-point state are the
+// reference's bits -- and, with the bit-exact nodal update and contact, whole trajectories are.
+// Same mapping as elem_step (lane k = Gauss point k); no contraction, fma exactly where the
+// reference's StaticArrays products use muladd:
+//   * Jacobian of GP k summed in node order 1..8 (:1424-1434) from the Pusai table (cal_Pusai_hexa,
+//     built on the host with the reference's expression), cofactor det/inverse (:1436-1455);
+//   * BVbar[:, 3i+c] = (sum over k in GP order of (P2_k/3)*|det_k|) / V with V = sum |det_k|
+//     (:1729-1780): each lane writes its 8 node terms to LDS, lane i sums node i's column over
+//     the 8 lanes in GP order -- (P2/3)*|det| equals (P_signed/3)*det_signed exactly;
+//   * Bfinal (:1472-1490) is never stored: its entries are Pix, Piy, Piz, BVbar - P/3 and the
+//     explicit zeros, fed to the 6x24 * 24 chain (:1204) column by column in the reference's order;
+//   * D * de as the full 6x6 muladd chain (:1205); radial return with the reference's divisions
+//     (:1251-1282); Qe[:, e] += detJ * Bfinal' sigma (:1330-1340) summed over GPs in order via LDS;
+//   * deletion averages (:701-712) summed in GP order; triaxiality in invariant form (the
+//     reference's eigvals agree to rounding; it only enters the deletion test and the output).
+// ---------------------------------------------------------------------------------------------
+constexpr int kXbStride = 104;  // doubles of LDS per element: w[64] + av[8] + bv[24] + pad
+
+// x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
+// q = RN(x*y) with y = RN(1/3), then one exact-remainder correction q + (x - 3q)*y. The exact
+// quotient x/3 (a multiple of 1/3 of the last place) is never within 1/6 ulp of a rounding
+// boundary, and the corrected value is within |x - 3q| * |y - 1/3| < 2^-52 ulp of it, so both round
+// the same way (tests/test_div3.py checks the identity against IEEE division on the CPU). x == 0
+// keeps its sign.
+__device__ __forceinline__ double div3(double x) {
+    constexpr double y = 1.0 / 3.0;
+    const double q = x * y;
+    const double r = __builtin_fma(-q, 3.0, x);
+    const double q1 = __builtin_fma(r, y, q);
+    return x == 0.0 ? x : q1;
+}
+
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0>
+__device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat* __restrict__ mats, long long e,
+                                                int k, double* nd8, double* xb, const double* pus,
+                                                const ElemIn& in) {
+#pragma clang fp contract(off)
+    const DevMat* M = mats + in.mt;
+    const bool active = in.fl == 1;
+    const int npp = M->npp;
+    const int nd = DO_DELETE ? M->nd : 0;
+    double eqp = in.eqp, ys = in.ys;
+    double* w = xb;        // [node i][lane kk] exchange of one component
+    double* av = xb + 64;  // one scalar per lane
+    double* bv = xb + 72;  // BVbar row (24)
+
+    nd8[6 * k + 0] = in.x[0];
+    nd8[6 * k + 1] = in.x[1];
+    nd8[6 * k + 2] = in.x[2];
+    nd8[6 * k + 3] = in.du[0];
+    nd8[6 * k + 4] = in.du[1];
+    nd8[6 * k + 5] = in.du[2];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- Jacobian at GP k in node order, det and inverse (cal_Bfinal :1424-1455; cal_BVbar_hexa
+    // computes the same J and det at :1716-1740)
+    const double* P0 = pus + 24 * k;  // Pusai_mat[k][r][i] = pus[24k + 8r + i]
+    const double* P1 = P0 + 8;
+    const double* P2 = P0 + 16;
+    double J11 = 0.0, J12 = 0.0, J13 = 0.0, J21 = 0.0, J22 = 0.0, J23 = 0.0, J31 = 0.0, J32 = 0.0, J33 = 0.0;
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        gp_st<NT>(a.stress + c * ld + gp, kill ? 0.0 : (active ? fin[c] : in.sig[c]));
-        gp_st<NT>(a.strain + c * ld + gp, kill ? 0.0 : (active ? eps[c] : in.eps[c]));
+    for (int i = 0; i < 8; ++i) {
+        const double X0 = nd8[6 * i + 0], X1 = nd8[6 * i + 1], X2 = nd8[6 * i + 2];
+        J11 += P0[i] * X0;
+        J12 += P0[i] * X1;
+        J13 += P0[i] * X2;
+        J21 += P1[i] * X0;
+        J22 += P1[i] * X1;
+        J23 += P1[i] * X2;
+        J31 += P2[i] * X0;
+        J32 += P2[i] * X1;
+        J33 += P2[i] * X2;
     }
-    if (ANY_PLASTIC) {
-        gp_st<NT>(a.eqps + gp, active ? eqp : in.eqp);
-        gp_st<NT>(a.yield + gp, active ? ys : in.ys);
+    const double v = J11 * J22 * J33 + J12 * J23 * J31 + J13 * J21 * J32 - J11 * J23 * J32 - J12 * J21 * J33 -
+                     J13 * J22 * J31;
+    const double div_v = 1.0 / v;
+    double pd[8][3];  // P2 = dN_i/dx at GP k (:1457-1470)
+    {
+        const double iJ11 = (J22 * J33 - J23 * J32) * div_v;
+        const double iJ21 = (J23 * J31 - J21 * J33) * div_v;
+        const double iJ31 = (J21 * J32 - J22 * J31) * div_v;
+        const double iJ12 = (J13 * J32 - J12 * J33) * div_v;
+        const double iJ22 = (J11 * J33 - J13 * J31) * div_v;
+        const double iJ32 = (J12 * J31 - J11 * J32) * div_v;
+        const double iJ13 = (J12 * J23 - J13 * J22) * div_v;
+        const double iJ23 = (J13 * J21 - J11 * J23) * div_v;
+        const double iJ33 = (J11 * J22 - J12 * J21) * div_v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            pd[i][0] = iJ11 * P0[i] + iJ12 * P1[i] + iJ13 * P2[i];
+            pd[i][1] = iJ21 * P0[i] + iJ22 * P1[i] + iJ23 * P2[i];
+            pd[i][2] = iJ31 * P0[i] + iJ32 * P1[i] + iJ33 * P2[i];
+        }
     }
-    if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
-    if (DO_DELETE) {
-        a.flag[e] = kill ? 2 : (in.fl == 2 ? 0 : in.fl);        // 8 lanes, same value
-        // lane 0: the element's deletion step; lanes 1-7 of a killed element: slot nEp+1, "last step
-        // with a deletion" (contact rebuilds its live surface lists from it); others: dump slot nEp
-        int* ds = kill ? a.del_step + (k == 0 ? e : a.nEp + 1) : a.del_step + a.nEp;
-        *ds = a.step_i;
+
+    // ---- V and BVbar (:1729-1780), summed over the 8 GPs in order by the lane of each node.
+    // (P2_abs/3)*|det| of the reference equals (P2/3)*det with the signed det, bit for bit.
+    av[k] = fabs(v);
+    double bvk[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[8 * i + k] = div3(pd[i][c]) * v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double s = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) s += w[8 * k + kk];
+        bvk[c] = s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    double V = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) V += av[kk];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bv[3 * k + c] = bvk[c] / V;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // Bfinal rows 1-3 carry -P2/3 + BVbar (:1482-1490)
+    auto tq = [&](int i, int c) { return -div3(pd[i][c]) + bv[3 * i + c]; };
+
+    // ---- de = Bfinal * d_u (:1204): per row, the chain over columns j = 3i+c in order.
+    // Bfinal column (i,c) by rows: c=0: (Pix+t0, t0, t0, Piy, 0, Piz); c=1: (t1, Piy+t1, t1, Pix,
+    // Piz, 0); c=2: (t2, t2, Piz+t2, 0, Piy, Pix).
+    double de[6];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double* D = nd8 + 6 * i + 3;
+        const double u0 = D[0], u1 = D[1], u2 = D[2];
+        const double t0 = tq(i, 0), t1 = tq(i, 1), t2 = tq(i, 2);
+        if (i == 0) {
+            de[0] = (pd[0][0] + t0) * u0;
+            de[1] = t0 * u0;
+            de[2] = t0 * u0;
+            de[3] = pd[0][1] * u0;
+            de[4] = 0.0 * u0;
+            de[5] = pd[0][2] * u0;
+        } else {
+            de[0] = __builtin_fma(pd[i][0] + t0, u0, de[0]);
+            de[1] = __builtin_fma(t0, u0, de[1]);
+            de[2] = __builtin_fma(t0, u0, de[2]);
+            de[3] = __builtin_fma(pd[i][1], u0, de[3]);
+            de[4] = __builtin_fma(0.0, u0, de[4]);
+            de[5] = __builtin_fma(pd[i][2], u0, de[5]);
+        }
+        de[0] = __builtin_fma(t1, u1, de[0]);
+        de[1] = __builtin_fma(pd[i][1] + t1, u1, de[1]);
+        de[2] = __builtin_fma(t1, u1, de[2]);
+        de[3] = __builtin_fma(pd[i][0], u1, de[3]);
+        de[4] = __builtin_fma(pd[i][2], u1, de[4]);
+        de[5] = __builtin_fma(0.0, u1, de[5]);
+        de[0] = __builtin_fma(t2, u2, de[0]);
+        de[1] = __builtin_fma(t2, u2, de[1]);
+        de[2] = __builtin_fma(pd[i][2] + t2, u2, de[2]);
+        de[3] = __builtin_fma(0.0, u2, de[3]);
+        de[4] = __builtin_fma(pd[i][1], u2, de[4]);
+        de[5] = __builtin_fma(pd[i][0], u2, de[5]);
+    }
+
+    // ---- d_o = Dmat * de (:1205), the full 6x6 chain (Dmat[r][j] = c*M[r][j], zeros included)
+    const double Dn = M->Dn, Do = M->Do, Ds = M->Ds, Z = 0.0;
+    const double Dm[6][6] = {{Dn, Do, Do, Z, Z, Z}, {Do, Dn, Do, Z, Z, Z}, {Do, Do, Dn, Z, Z, Z},
+                             {Z, Z, Z, Ds, Z, Z},   {Z, Z, Z, Z, Ds, Z},   {Z, Z, Z, Z, Z, Ds}};
+    double fin[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        double acc = Dm[r][0] * de[0];
+#pragma unroll
+        for (int j = 1; j < 6; ++j) acc = __builtin_fma(Dm[r][j], de[j], acc);
+        fin[r] = in.sig[r] + acc;
+    }
+    // ---- J2 radial return (:1227-1289)
+    if (ANY_PLASTIC && npp > 0) {
+        const double mean = div3(fin[0] + fin[1] + fin[2]);
+        const double dev[6] = {fin[0] - mean, fin[1] - mean, fin[2] - mean, fin[3], fin[4], fin[5]};
+        const double q = sqrt(1.5 * (dev[0] * dev[0] + dev[1] * dev[1] + dev[2] * dev[2] + 2.0 * (dev[3] * dev[3]) +
+                                     2.0 * (dev[4] * dev[4]) + 2.0 * (dev[5] * dev[5])));
+        if (q > ys) {
+            int p = npp - 2;  // segment search (:1255-1264), 0-based p = p_index-1
+            for (int j = 1; j < npp; ++j) {
+                if (eqp <= M->pl_eps[j]) {
+                    p = j - 1;
+                    break;
+                }
+            }
+            const double H = M->Hd[p];
+            const double dep = (q - ys) / (3.0 * M->G + H);
+            const double s = ys + H * dep;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) fin[r] = dev[r] * s / q + mean;
+#pragma unroll
+            for (int r = 3; r < 6; ++r) fin[r] = dev[r] * s / q + 0.0;
+            eqp = eqp + dep;
+            ys = ys + H * dep;
+        }
+    }
+    double eps[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) eps[c] = in.eps[c] + de[c];
+
+    // ---- triaxiality of the final stress (invariant form of :995-1018)
+    double tri;
+    {
+        const double mean = div3(fin[0] + fin[1] + fin[2]);
+        const double a01 = fin[0] - fin[1], a12 = fin[1] - fin[2], a20 = fin[2] - fin[0];
+        const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) +
+                                3.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5]));
+        tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
+    }
+    bool kill = false;
+    if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
+        av[k] = eqp;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double v_e = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) v_e += av[kk];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        av[k] = tri;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double t_e = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) t_e += av[kk];
+        v_e = v_e * 0.125;  // /8, exact
+        t_e = t_e * 0.125;
+        if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
+    }
+
+    // ---- Qe[:, e] += detJ * Bfinal' * sigma (:1330-1340), GP contributions summed in GP order
+    double fk[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double t = tq(i, c);
+            double acc;
+            if (c == 0) {
+                acc = (pd[i][0] + t) * fin[0];
+                acc = __builtin_fma(t, fin[1], acc);
+                acc = __builtin_fma(t, fin[2], acc);
+                acc = __builtin_fma(pd[i][1], fin[3], acc);
+                acc = __builtin_fma(0.0, fin[4], acc);
+                acc = __builtin_fma(pd[i][2], fin[5], acc);
+            } else if (c == 1) {
+                acc = t * fin[0];
+                acc = __builtin_fma(pd[i][1] + t, fin[1], acc);
+                acc = __builtin_fma(t, fin[2], acc);
+                acc = __builtin_fma(pd[i][0], fin[3], acc);
+                acc = __builtin_fma(pd[i][2], fin[4], acc);
+                acc = __builtin_fma(0.0, fin[5], acc);
+            } else {
+                acc = t * fin[0];
+                acc = __builtin_fma(t, fin[1], acc);
+                acc = __builtin_fma(pd[i][2] + t, fin[2], acc);
+                acc = __builtin_fma(0.0, fin[3], acc);
+                acc = __builtin_fma(pd[i][1], fin[4], acc);
+                acc = __builtin_fma(pd[i][0], fin[5], acc);
+            }
+            w[8 * i + k] = v * acc;  // W*W*W*detJ*acc with W = 1
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double s = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) s += w[8 * k + kk];
+        fk[c] = s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (WITH_VOL) a.vol[e] = V;
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
+}
+
+// Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.
+__device__ __forceinline__ void stage_pusai(const ElemArgs& a, double* s_pus) {
+    for (int w = threadIdx.x; w < 192; w += blockDim.x) s_pus[w] = a.pusai[w];
 }
 
 // Graph mode (hipGraph of two steps, hakai_step): the step number is not a kernel argument but a
@@ -341,28 +643,40 @@ __device__ __forceinline__ void graph_step(ElemArgs& a) {
     }
 }
 
-// One batch of 32 elements per block (simple form; used by the literal drop-in and for A/B).
-template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW>
+// One batch of 32 elements per block (simple form; small meshes, the literal drop-in, A/B).
+template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW, bool EXACT>
 __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
+    __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
+    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
     graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
+    if (EXACT) {
+        stage_pusai(a, s_pus);
+        __syncthreads();
+    }
     const long long e = (long long)xcd_remap(blockIdx.x, gridDim.x) * kEPB + grp;
     ElemIn in;
-    load_stage_a(a, e, k, in);
+    load_stage_a<EXACT>(a, e, k, in);
     load_stage_b<true>(a, e, k, in);
-    elem_step<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride, in);
+    if (EXACT)
+        elem_step_exact<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride,
+                                                                s_xb + grp * kXbStride, s_pus, in);
+    else
+        elem_step<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride, in);
 }
 
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT = 0>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
+    __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
+    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
     graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
@@ -371,10 +685,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         const double* src = reinterpret_cast<const double*>(a.mats);
         double* dst = reinterpret_cast<double*>(s_mats);
         for (int w = threadIdx.x; w < words; w += kBlock) dst[w] = src[w];
-        __syncthreads();
     }
+    if (EXACT) stage_pusai(a, s_pus);
+    if (LDS_MATS || EXACT) __syncthreads();
     const DevMat* mats = LDS_MATS ? s_mats : a.mats;
     double* nd8 = s_nd + grp * kLdsStride;
+    double* xb = s_xb + (EXACT ? grp * kXbStride : 0);
     const long long nb = a.nEp / kEPB;
     // Batch schedule, as (first, stride, count):
     //  map 0: each block walks a contiguous run of batches;
@@ -399,77 +715,84 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     auto elem_of = [&](long long i) { return (first + (i < count ? i : count - 1) * stride) * kEPB + grp; };
 
     ElemIn cur, nxt;
-    load_stage_a(a, elem_of(0), k, cur);
-    load_stage_a(a, elem_of(1), k, nxt);
+    load_stage_a<EXACT>(a, elem_of(0), k, cur);
+    load_stage_a<EXACT>(a, elem_of(1), k, nxt);
     load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
-        load_stage_a(a, elem_of(i + 2), k, nn);
+        load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
         load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
-        elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, cur);
+        if (EXACT)
+            elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, xb, s_pus,
+                                                                            cur);
+        else
+            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, cur);
         cur = nxt;
         nxt = nn;
     }
 }
 
-template <int MINW>
+// Runtime flags -> template instantiations.
+template <int MINW, bool EXACT>
 static void launch_element_w(const ElemArgs& a, bool do_delete, bool store_triax, bool with_vol, unsigned grid,
                              hipStream_t s) {
     if (with_vol) {
-        hipLaunchKernelGGL((k_element<false, false, true, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_element<false, false, true, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     } else if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<true, true, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, true, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<true, false, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, false, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<false, true, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, true, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<false, false, false, MINW>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, false, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     }
 }
 
-template <int NT>
-static void launch_pipe_nt(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+template <bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT>
+static void launch_pipe(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
     if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid), dim3(kBlock),
+                               0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<true, false, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<false, false, true, true, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
     }
 }
 
 template <bool ANY_PLASTIC, bool LDS_MATS>
 static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (a.exact) {  // reference-order kernel: Gauss-point state nontemporal when any is requested
+        if (a.gp_nt)
+            launch_pipe<ANY_PLASTIC, LDS_MATS, 3, true>(a, do_delete, store_triax, grid, s);
+        else
+            launch_pipe<ANY_PLASTIC, LDS_MATS, 0, true>(a, do_delete, store_triax, grid, s);
+        return;
+    }
     if (ANY_PLASTIC && LDS_MATS && a.gp_nt) {
         switch (a.gp_nt) {
-            case 1: launch_pipe_nt<1>(a, do_delete, store_triax, grid, s); break;
-            case 2: launch_pipe_nt<2>(a, do_delete, store_triax, grid, s); break;
-            default: launch_pipe_nt<3>(a, do_delete, store_triax, grid, s); break;
+            case 1: launch_pipe<true, true, 1, false>(a, do_delete, store_triax, grid, s); break;
+            case 2: launch_pipe<true, true, 2, false>(a, do_delete, store_triax, grid, s); break;
+            default: launch_pipe<true, true, 3, false>(a, do_delete, store_triax, grid, s); break;
         }
         return;
     }
-    if (do_delete) {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
-    } else {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS>), dim3(grid), dim3(kBlock), 0, s, a);
-    }
+    launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false>(a, do_delete, store_triax, grid, s);
 }
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
     if (a.nE <= 0) return hipSuccess;
+    if (a.exact && !a.pusai) return hipErrorInvalidValue;
     const long long nb = a.nEp / kEPB;
     if (a.pipe_blocks > 0 && !a.vol) {
         const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
@@ -484,10 +807,14 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
         return hipGetLastError();
     }
     const unsigned grid = (unsigned)nb;
+    if (a.exact) {
+        launch_element_w<2, true>(a, do_delete, store_triax, a.vol != nullptr, grid, s);
+        return hipGetLastError();
+    }
     switch (a.variant) {
-        case 3: launch_element_w<3>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        case 4: launch_element_w<4>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        default: launch_element_w<2>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        case 3: launch_element_w<3, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        case 4: launch_element_w<4, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        default: launch_element_w<2, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
     }
     return hipGetLastError();
 }

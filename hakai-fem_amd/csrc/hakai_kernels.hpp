@@ -36,6 +36,9 @@ struct ElemArgs {
     int pipe_map;           // batch schedule: 0 contiguous per block, 1 contiguous per XCD, strided
     int nmat;               // materials (staged in LDS when <= kMaxLdsMats)
     int gp_nt;              // 1: Gauss-point state streamed with nontemporal loads/stores
+    int exact;              // 1: reference-order arithmetic (elem_step_exact), bit-identical to
+                            //    cal_stress_hexa; 0: fused single-pass form (elem_step)
+    const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
 };
 
 struct BCArgs {

@@ -92,6 +92,8 @@ class _Output:
 def _setup_rank(glob, gdiag, rank, world, device, comm):
     loc, diag, iface, l2g, off = _dist.range_partition(glob, rank, world, gdiag)
     sv = Solver(loc, device=device, diag_M=diag)
+    # the driver's element arithmetic is the reference's, operation for operation (as hakai_run_inp)
+    sv.set_tuning("elem_exact", 0 if os.environ.get("HAKAI_ELEM_EXACT") == "0" else 1)
     sv.set_element_offset(loc.global_element_offset)
     comm(sv)
     sv.set_interface(*iface)

@@ -836,6 +836,11 @@ int hakai_run_inp(const char* fname, const char* out_dir, int device, int verbos
         hakai_ctx* c;
         ~FreeC() { hakai_destroy(c); }
     } fc{c};
+    // The driver reproduces the reference's element arithmetic operation for operation
+    // (elem_exact), so its output is the reference's bits; HAKAI_ELEM_EXACT=0 selects the fused
+    // single-pass kernel (same physics, rounding-level differences).
+    const char* ex = std::getenv("HAKAI_ELEM_EXACT");
+    if ((r = hakai_set_tuning(c, "elem_exact", (ex && ex[0] == '0') ? 0 : 1))) return r;
     if ((r = hakai_upload_model(c, nN, M->coordmat, nE, M->elementmat, M->element_material, M->nMat, M->materials,
                                 diag_M.data())))
         return r;

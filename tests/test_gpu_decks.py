@@ -28,8 +28,28 @@ def _deck(name):
     return z, model_from_arrays(z, name)
 
 
+@pytest.mark.parametrize("name", ["Charpy_test", "bullet_impact", "crash_tube_80_350_solid"])
+def test_reference_deck_bitexact(name):
+    """The driver's mode (elem_exact: cal_stress_hexa's own arithmetic, tests/test_gpu_exact.py):
+    the whole trajectory is the oracle's, bit for bit -- including the self-contact crash tube,
+    whose contact decisions depend on the last bit of a position."""
+    z, m = _deck(name)
+    steps = int(z["steps"])
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", 1)
+        sv.step(1, steps // 2)
+        sv.step(1 + steps // 2, steps - steps // 2)
+        g = sv.download()
+        dels = [tuple(int(v) for v in x) for x in sv.deleted()]
+    assert dels == [tuple(int(v) for v in x) for x in z["deletions"]]
+    assert np.array_equal(g.element_flag, z["element_flag"])
+    assert np.array_equal(g.disp, z["disp"]), f"disp max rel diff {rel_err(g.disp, z['disp']):.3e}"
+    assert np.array_equal(g.disp_pre, z["disp_pre"])
+
+
 @pytest.mark.parametrize("name", ["Charpy_test", "bullet_impact"])
 def test_reference_deck_parity(name):
+    """The fused kernel (default for hakai_step): rounding-level element differences, 1e-6."""
     z, m = _deck(name)
     steps = int(z["steps"])
     with Solver(m) as sv:
@@ -53,7 +73,8 @@ def _oracle_from_gpu(o, g, m):
 
 
 def test_self_contact_deck_stepwise_parity():
-    """crash-tube-80-350-solid (HAKAIoption=self-contact): the tube stands on the plate with nodes
+    """crash-tube-80-350-solid (HAKAIoption=self-contact) with the FUSED element kernel (exact mode
+    is bit-exact on the whole run, test_reference_deck_bitexact): the tube stands on the plate with nodes
     exactly on mesh edges and planes, so which triangles catch a node changes with the last bit of
     its position. Two FP64 implementations that differ in rounding (the element kernel sums in a
     lane-dependent node order) part after the first such flip, by ~1e-3 relative within 100 steps
