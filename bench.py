@@ -3,18 +3,25 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W
+        --master-port P bench.py --gpus N --steps K --warmup W [--strong]
+    python bench.py --local-ranks R          # rehearsal of the N-rank path on one GPU
 
 A "step" is one full pass of the reference time-loop body (v2/HAKAI_j.jl:497-764): nodal central
 difference with element-order force assembly, prescribed BCs, fused hex8 B-bar + J2 return +
 internal force + triaxiality + ductile-deletion check for every active element (and, for N > 1, the
-RCCL interface exchange). Inputs are resident in HBM before timing starts.
+interface exchange). Inputs are resident in HBM before timing starts.
 
-Workload (BASELINE.json): N = 1 -> C3, the 2 M-hex elastoplastic tensile bar 20x20x5000
-(Tensile5e steel_Ductile, ENCASTRE at z=0, linear v_z field). N > 1 -> weak scaling, each rank owns a
-2 M-hex z-slab of the C5 family bar 100x100x(200N) (uniform v_z = -1e5 mm/s into the clamped face);
-N = 8 is C5 (16 M hex). Before warm-up an untimed preload advances the bar into its plastic regime
-(the share of yielding Gauss points is reported).
+Workloads (BASELINE.json):
+  N = 1 (default)  C3, the 2 M-hex elastoplastic tensile bar 20x20x5000 (Tensile5e steel_Ductile,
+                   ENCASTRE at z=0, linear v_z field) -- the configuration the north star is quoted on.
+  N > 1 (weak)     each rank owns a 2 M-hex z-slab of the C5 bar 100x100x(200N) (uniform
+                   v_z = -1e5 mm/s into the clamped face); N = 8 is C5 (16 M hex). The line carries
+                   `single_gpu_same_slab`: the same run's rate of one rank's slab on its GPU alone
+                   (no exchange), so value / (N x that) is the weak-scaling efficiency on ONE workload.
+  --strong         the whole C5 bar 100x100x1600 (16 M hex) split over N (N = 1 holds all 16 M),
+                   so value_N / value_1 is the strong-scaling speed-up ("scaling": "strong").
+Before warm-up an untimed preload advances the bar into its plastic regime (the share of yielding
+Gauss points is reported).
 
 Rank 0 prints ONE JSON line. `roofline` is for the dominant (element) kernel, from HIP events on the
 library's stream; `cpu_baseline` is the oracle (CPU restatement of v0.0.2, OpenMP element loop)
@@ -39,6 +46,7 @@ B_E_PLASTIC = 1832             # compulsory bytes per elastopl
 B_E_ELASTIC = 1576
 B_N = 224                      # compulsory bytes per node per step (whole step)
 B_N_ELEMENT_SIDE = 72          # coord, u, u_pre read by the element kernel, once per node
+C5_LAYERS = 1600               # C5: 100x100x1600
 
 
 def parse():
@@ -48,6 +56,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--preload", type=int, default=-1, help="untimed steps before warm-up (-1: config default)")
     ap.add_argument("--layers", type=int, default=0, help="override z layers (tests / quick runs)")
+    ap.add_argument("--strong", action="store_true", help="strong scaling: C5 16 M hex split over the ranks")
+    ap.add_argument("--local-ranks", type=int, default=0,
+                    help="rehearsal: the N-rank path as an in-process group of R contexts on one GPU")
+    ap.add_argument("--same-slab-ref", type=int, default=1,
+                    help="N > 1 weak: also time one rank's slab alone (single_gpu_same_slab)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -56,10 +69,22 @@ def parse():
     return ap.parse_args()
 
 
-def build_rank_model(rank, world, layers_override=0, dist_path=False):
-    """Returns (local Model, local diag_M, interface arrays or None, config dict)."""
+def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=False):
+    """Returns (local Model, local diag_M, interface arrays or None, config dict, preload)."""
     from hakai import mesh
     from hakai.dist import slab_partition
+    if strong:
+        layers = layers_override or C5_LAYERS
+        glob = mesh.config_c5(layers=layers)
+        cfg = {"workload": "C5 100x100x%d elastoplastic impact bar (%d hex), split into %d z-slab(s) (strong scaling)"
+               % (layers, glob.nElement, world), "elements": glob.nElement, "nodes": glob.nNode,
+               "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"
+               if world > 1 else "single GPU"}
+        if world == 1:
+            diag, _ = glob.lumped_mass()
+            return glob, diag, None, cfg, 20
+        local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
+        return local, diag, iface, cfg, 20
     if world == 1 and not dist_path:
         nz = layers_override or 5000
         m = mesh.config_c3(v_end=5e5) if nz == 5000 else mesh.bar_model(
@@ -100,6 +125,23 @@ def cpu_baseline(seconds, threads):
                       f"{n} steps in {dt:.1f} s, {threads} OpenMP threads"}
 
 
+def same_slab_rate(model, diag, t, preload, warmup, steps):
+    """One rank's slab alone on its GPU (no communicator, no interface): wall time of `steps`."""
+    import torch
+    from hakai.solver import Solver
+    sv = Solver(model, device=torch.cuda.current_device(), diag_M=diag)
+    sv.set_tuning("graph", 0)
+    sv.step(1, preload + warmup)
+    sv.sync()
+    t0 = time.perf_counter()
+    sv.step(1 + preload + warmup, steps)
+    sv.sync()
+    el = time.perf_counter() - t0
+    n_act = int(sv.download(element_flag=True).element_flag.sum())
+    sv.close()
+    return el, n_act
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -110,9 +152,12 @@ def main():
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     import torch
     import torch.distributed as dist
-    import hakai
     from hakai._abi import K_ELEMENT, K_EXCHANGE, K_NODAL, K_BC
-    from hakai.solver import Solver, comm_unique_id
+    from hakai.solver import Solver, comm_unique_id, step_group
+    R = a.local_ranks if a.local_ranks > 1 else 0
+    if R and world > 1:
+        raise SystemExit("--local-ranks is a one-process rehearsal")
+    nparts = R or world                      # subdomains of the workload
     multi = world > 1 or a.dist_path
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -121,94 +166,142 @@ def main():
         os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    model, diag, iface, cfg, preload = build_rank_model(rank, world, a.layers, a.dist_path)
-    if a.preload >= 0:
-        preload = a.preload
-    sv = Solver(model, device=local_rank if multi else 0, diag_M=diag)
-    # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region is
-    # stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
-    sv.set_tuning("graph", 0)
-    if multi:
-        uid = comm_unique_id() if rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
-        dist.broadcast(t, 0)
-        sv.comm_init(rank, world, bytes(t.cpu().tolist()))
-        sv.set_interface(*iface)
+    # this process's subdomains: one per rank, or R in-process ranks on one device
+    ids = list(range(R)) if R else [rank]
+    built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong) for r in ids]
+    cfg = built[0][3]
+    preload = built[0][4] if a.preload < 0 else a.preload
+    svs = []
+    for r, (model, diag, iface, _, _) in zip(ids, built):
+        sv = Solver(model, device=local_rank if multi else 0, diag_M=diag)
+        # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region is
+        # stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
+        sv.set_tuning("graph", 0)
+        if iface is not None:
+            sv.set_element_offset(model.global_element_offset)
+            if R:
+                sv.comm_init_local(r, R, 7117)
+            else:
+                uid = comm_unique_id() if rank == 0 else bytes(128)
+                tu = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
+                dist.broadcast(tu, 0)
+                sv.comm_init(rank, world, bytes(tu.cpu().tolist()))
+            sv.set_interface(*iface)
+        svs.append(sv)
+
+    def run(t_first, n):
+        if R:
+            step_group(svs, t_first, n)
+        else:
+            svs[0].step(t_first, n)
+
     t = 1
     if preload:
-        sv.step(t, preload)
+        run(t, preload)
         t += preload
     if a.warmup:
-        sv.step(t, a.warmup)
+        run(t, a.warmup)
         t += a.warmup
-    sv.sync()
+    for sv in svs:
+        sv.sync()
 
     def barrier():
         if multi:
             dist.barrier()
         torch.cuda.synchronize()
 
-    n_active = model.nElement
     # timed region: HIP events around the element kernel only (the roofline figure), so the step
     # loop is not slowed by events around every launch
-    sv.profile(True, kernels=[K_ELEMENT])
+    for sv in svs:
+        sv.profile(True, kernels=[K_ELEMENT])
     barrier()
     t0 = time.perf_counter()
-    sv.step(t, a.steps)
-    sv.sync()
+    run(t, a.steps)
+    for sv in svs:
+        sv.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if multi:
         dist.barrier()
     elapsed = t1 - t0
     t += a.steps
-    el_timed = sv.profile_read(K_ELEMENT)
+    el_timed = [sv.profile_read(K_ELEMENT) for sv in svs]
     # per-kernel breakdown from a short extra pass after the timed region (reported, not timed)
-    sv.profile(True)
+    for sv in svs:
+        sv.profile(True)
     nb = min(20, max(a.steps, 1))
-    sv.step(t, nb)
-    sv.sync()
-    k_ms = {name: sv.profile_read(k) for k, name in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
-                                                        (K_EXCHANGE, "exchange"))}
-    sv.profile(False)
-    st = sv.download(integ_eq_plastic_strain=True, element_flag=True)
-    plastic_frac = float(np.mean(st.integ_eq_plastic_strain > 0))
-    n_active = int(st.element_flag.sum())
-    n_deleted = model.nElement - n_active
+    run(t, nb)
+    t += nb
+    k_tot = {}
+    for sv in svs:
+        sv.sync()
+        for k, name in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"), (K_EXCHANGE, "exchange")):
+            ms, n = sv.profile_read(k)
+            if n:
+                p = k_tot.setdefault(name, [0.0, 0])
+                p[0] += ms
+                p[1] += n
+        sv.profile(False)
+    n_active, plastic = 0, []
+    for sv in svs:
+        st = sv.download(integ_eq_plastic_strain=True, element_flag=True)
+        plastic.append(float(np.mean(st.integ_eq_plastic_strain > 0)))
+        n_active += int(st.element_flag.sum())
+    plastic_frac = float(np.mean(plastic))
+    n_elem_local = sum(b[0].nElement for b in built)
+    n_node_local = sum(b[0].nNode for b in built)
     if multi:
-        v = torch.tensor([elapsed, float(n_active)], dtype=torch.float64, device="cuda")
+        v = torch.tensor([elapsed, float(n_active), plastic_frac], dtype=torch.float64, device="cuda")
         mx = v.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = v.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
         n_active_total = sm[1].item()
-        g = torch.tensor([plastic_frac], dtype=torch.float64, device="cuda")
-        dist.all_reduce(g)
-        plastic_frac = g.item() / world
+        plastic_frac = sm[2].item() / world
     else:
         n_active_total = n_active
+    n_deleted = cfg["elements"] - n_active_total
     # element updates: active elements x steps (metric definition)
     updates = n_active_total * a.steps
     value = updates / elapsed / 1e6
     ms_step = elapsed / a.steps * 1e3
-    # roofline of the dominant kernel, from HIP events on the library's stream (rank 0)
-    el_ms, el_n = el_timed
-    el_avg_s = el_ms / max(el_n, 1) / 1e3
-    nE_loc, nN_loc = model.nElement, model.nNode
-    alg_bytes = B_E_PLASTIC * n_active + B_N_ELEMENT_SIDE * nN_loc
+    # roofline of the dominant kernel, from HIP events on the library's stream (this process)
+    el_ms = sum(x[0] for x in el_timed)
+    el_n = max(el_timed[0][1], 1)
+    el_avg_s = el_ms / el_n / 1e3 / len(svs)   # per subdomain launch
+    alg_bytes = (B_E_PLASTIC * n_active + B_N_ELEMENT_SIDE * n_node_local) / len(svs)
     achieved = alg_bytes / el_avg_s / 1e9
-    whole_bytes = B_E_PLASTIC * n_active + B_N * nN_loc
+    whole_bytes = B_E_PLASTIC * n_active + B_N * n_node_local
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "element_pmc.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and not R:
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("elements") == nE_loc:
+            if pm.get("elements") == n_elem_local:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in k_tot.items()}
+    extra = {}
+    if nparts > 1:
+        extra["exchange_ms_per_step"] = k_ms.get("exchange")
+    if world > 1 and not a.strong and a.same_slab_ref:
+        # the same slab alone on each GPU, concurrently; the slowest rank, like the timed run
+        for sv in svs:
+            sv.close()
+        svs = []
+        model, diag = built[0][0], built[0][1]
+        e_ref, n_ref = same_slab_rate(model, diag, 1, preload, a.warmup, a.steps)
+        v = torch.tensor([e_ref], dtype=torch.float64, device="cuda")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        e_ref = float(v.item())
+        extra["single_gpu_same_slab"] = {
+            "value": round(n_ref * a.steps / e_ref / 1e6, 3), "unit": "M element-updates/s",
+            "ms_per_step": round(e_ref / a.steps * 1e3, 4),
+            "what": "one rank's slab alone on its GPU (no exchange), same preload/warmup/steps, slowest rank; "
+                    "weak-scaling efficiency = value / (n_gpus x this)"}
     out = {
         "metric": "M element-updates/sec (hex8, 8 Gauss pts) at 1/2/4/8 MI355X; % HBM roofline",
         "value": round(value, 3),
@@ -218,24 +311,30 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (structured hex bar, 1% node perturbation, seed 0; no reference checkpoint needed)",
         "config": dict(cfg, preload_steps=preload, plastic_gp_frac=round(plastic_frac, 4),
                        deleted_elements=int(n_deleted),
                        whole_step_roofline_frac=round(whole_bytes * a.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)
-                       if world == 1 else None,
-                       kernel_ms_per_step={k: round(v[0] / max(v[1], 1), 4) for k, v in k_ms.items() if v[1]},
-                       parallelism=f"dp{world}" if world > 1 else "single"),
+                       if nparts == 1 else None,
+                       kernel_ms_per_step=k_ms, **extra,
+                       parallelism=(f"dp{world}" if world > 1 else
+                                    (f"rehearsal: {R} in-process ranks on one GPU (device-copy exchange)"
+                                     if R else "single"))),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": ("static: rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this kernel and "
+                                        "workload, calibrated (profiles/element_pmc.json); not measured in this run")
+                     if traffic else None,
                      "kernel": "k_element", "alg_bytes_per_launch": int(alg_bytes),
                      "avg_launch_ms": round(el_avg_s * 1e3, 4), "measured_peak_GBs": HBM_MEASURED_GBS},
         "cpu_baseline": None,
     }
-    sv.close()
-    if rank == 0 and world == 1 and a.cpu_baseline:
+    for sv in svs:
+        sv.close()
+    if rank == 0 and world == 1 and not R and not a.strong and a.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_threads)
         except Exception as e:  # reported, never fatal for the GPU number

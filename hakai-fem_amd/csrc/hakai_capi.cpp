@@ -421,6 +421,9 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     HIPCHK(hipSetDevice(c->device));
     (void)hipStreamSynchronize(c->stream);
     hkc::free_model(c);
+    // BC tables are sized for the previous mesh (the fused-BC per-dof table has 3nN entries): a new
+    // model starts without BCs until hakai_set_bc runs again
+    hkc::free_bc(c);
     const long long nN = nNode, nE = nElement;
     const long long nEp = ((nE + 31) / 32) * 32;  // whole 32-element batches; padding behaves as deleted
     // host-side conversions
@@ -584,7 +587,6 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
         HIPCHK(dalloc(&c->d_bc_of_dof, of.size()));
         HIPCHK(hipMemcpyAsync(c->d_bc_of_dof, of.data(), of.size() * sizeof(int), hipMemcpyHostToDevice, s));
     }
-    HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
 }

@@ -591,13 +591,30 @@ __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const 
 constexpr int kSmallScan = 32768;
 __global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) {
     __shared__ int s_w[16];
-    const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
+    // each thread scans a run of `per` entries (a multiple of 4, so the run is whole 16-B vectors:
+    // a quarter of the load/store instructions of an element-wise loop)
+    const int per = (((n + (int)blockDim.x - 1) / (int)blockDim.x) + 3) & ~3;
     const int a = (int)threadIdx.x * per, b = min(n, a + per);
+    const int bv = a + ((max(b - a, 0)) & ~3);  // end of the whole vectors
     int sum = 0;
-    for (int i = a; i < b; ++i) sum += in[i];
+    for (int i = a; i < bv; i += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(in + i);
+        sum += v.x + v.y + v.z + v.w;
+    }
+    for (int i = bv; i < b; ++i) sum += in[i];
     int total;
     int run = block_excl_scan(sum, s_w, total);
-    for (int i = a; i < b; ++i) {
+    for (int i = a; i < bv; i += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(in + i);
+        int4 o;
+        o.x = run;
+        o.y = o.x + v.x;
+        o.z = o.y + v.y;
+        o.w = o.z + v.z;
+        run = o.w + v.w;
+        *reinterpret_cast<int4*>(out + i) = o;
+    }
+    for (int i = bv; i < b; ++i) {
         const int v = in[i];
         out[i] = run;
         run += v;
@@ -2532,6 +2549,7 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
         stats[7] = sent;
         if (cap > 8) stats[8] = bytes;
     }
+    if (cap > 9) stats[9] = C->htot;  // hash-grid buckets over all pairs (> kSmallScan: device-wide scan)
     return 0;
 }
 

@@ -153,10 +153,10 @@ class Solver:
     # -- contact ----------------------------------------------------------------------------------
     def contact_stats(self) -> dict:
         """Counters of the last contact step (hakai_contact_stats)."""
-        st = np.zeros(9, np.int64)
-        check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 9))
+        st = np.zeros(10, np.int64)
+        check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 10))
         keys = ("events", "max_events", "candidate_triangles", "touched_nodes", "live_triangles", "live_nodes_i",
-                "live_nodes_j", "mirror_chunks_sent", "mirror_block_bytes")
+                "live_nodes_j", "mirror_chunks_sent", "mirror_block_bytes", "hash_buckets")
         return {k: int(v) for k, v in zip(keys, st)}
 
     def contact_info(self):

@@ -40,7 +40,13 @@ inline double flush16(double x) { return std::fabs(x) < 1E-16 ? 0.0 : x; }
 // "%1.6e": at most "-1.234567e-308" = 14 chars
 constexpr int kMaxNum = 16;
 
+// Julia's @printf prints non-finite values as "NaN", "Inf" and "-Inf" (C's printf: "nan", "inf")
 inline char* put_e(char* p, double x) {
+    if (!std::isfinite(x)) {
+        const char* t = std::isnan(x) ? "NaN" : (x > 0 ? "Inf" : "-Inf");
+        while (*t) *p++ = *t++;
+        return p;
+    }
     return std::to_chars(p, p + kMaxNum, x, std::chars_format::scientific, 6).ptr;
 }
 

@@ -112,11 +112,12 @@ int hakai_download_state(hakai_ctx* ctx, hakai_state_t* st);
  * t = t_first .. t_first+n_steps-1 (t is Float64 like `for t = 1:time_num`). Asynchronous with
  * respect to the host until hakai_sync / a download. */
 int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
-/* Launch-bound step loops run from hipGraphs: hakai_step captures two steps per graph (one graph
- * per starting parity, reused for the whole run) whenever the step is the same launch sequence
- * every time -- no multi-GPU exchange, no profiling, contact in its steady state -- and keeps the
- * call's last step in stream mode. Results are bit-identical to stream mode
- * (hakai_set_tuning(ctx, "graph", 0) turns capture off). Returns the steps run from graphs. */
+/* Launch-bound step loops run from hipGraphs: hakai_step captures `graph` steps per graph
+ * (default 16, an even count; tuning key "graph" or env HAKAI_GRAPH, 0 = no capture), one graph per
+ * starting parity, reused for the whole run, plus 2-step graphs for a run's tail. A step is captured
+ * whenever it is the same launch sequence every time -- no multi-GPU exchange, no profiling, no
+ * uploaded Q, contact in its steady state -- and the call's last step always runs in stream mode.
+ * Results are bit-identical to stream mode. hakai_graph_steps returns the steps run from graphs. */
 int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
@@ -158,9 +159,27 @@ int hakai_profile_enable(hakai_ctx* ctx, int on);  /* all kernels on / off; rese
 /* Time only the kernels whose bit (1 << HAKAI_K_*) is set (fewer events in a timed loop). */
 int hakai_profile_mask(hakai_ctx* ctx, uint32_t mask);
 int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
-/* Tuning knobs for A/B measurements: "elem_pipe_blocks" (>0: persistent software-pipelined
- * element kernel on that many blocks, default 512; 0: one-batch-per-block kernel), "elem_minw"
- * (2|3|4: occupancy variant of the one-batch kernel), "nodal_padded" (0: CSR gather). */
+/* Tuning knobs (results are bit-identical across every setting except elem_exact, which selects
+ * the arithmetic):
+ *   "elem_exact"        1: reference-order element arithmetic (cal_stress_hexa op for op; GPU
+ *                       trajectories bit-identical to the reference's expression order; the mode
+ *                       hakai_run_inp uses), 0 (default for hakai_step): fused single-pass element
+ *                       kernel (rounding-level differences); env HAKAI_ELEM_EXACT sets the default;
+ *   "elem_pipe_blocks"  >0: persistent software-pipelined element kernel on that many blocks
+ *                       (default 512); 0: one batch of 32 elements per block;
+ *   "elem_pipe_min"     persistent kernel only with >= this many batches per block (default 2);
+ *   "elem_map"          batch schedule: 1 (default) contiguous per XCD, 0 contiguous per block;
+ *   "elem_minw"         2|3|4: occupancy variant of the one-batch kernel;
+ *   "elem_gp_nt"        0..3: Gauss-point state with nontemporal loads (bit 0) / stores (bit 1);
+ *   "fe_layout"         element-force layout: 0 (default) Qe rows, 1 component SoA;
+ *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
+ *   "nodal_early"       1 (default): node operands loaded before the force gather;
+ *   "nodal_reverse"     1 (default): each XCD walks its node chunk from its end;
+ *   "nodal_fe_nt"       1: element forces gathered with nontemporal loads;
+ *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
+ *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
+ *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
+ *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy. */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
 
 /* ---- contact: all-exterior instance-vs-instance penalty contact --------- */
@@ -204,7 +223,8 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
  * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
  * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
  * [7] chunks of deletion-exposed contact nodes all ranks sent in the last step, [8] bytes of one
- * rank's per-step block (hakai_set_contact_global). */
+ * rank's per-step block (hakai_set_contact_global); [9] hash-grid buckets of all pairs (tables of
+ * more than 32 768 entries take the device-wide scan). */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);

@@ -120,6 +120,10 @@ hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, cons
 hko_contact* hko_contact_create_cp(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
                                    const double* mat_young, int32_t n_cp, const int32_t* cp_instance,
                                    const int64_t* cp_off, const int64_t* cp_elems);
+/* Same, indexed = 1: identical results through sorted face keys / cell index (large models). */
+hko_contact* hko_contact_create_ex(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
+                                   const double* mat_young, int32_t n_cp, const int32_t* cp_instance,
+                                   const int64_t* cp_off, const int64_t* cp_elems, int indexed);
 void hko_contact_destroy(hko_contact* c);
 /* The constants of cal_contact_force (v2/HAKAI_j.jl:2255-2259); defaults 0.25, 1, 1, 0, 0. */
 void hko_contact_set_params(hko_contact* c, double myu, double kc_o, double kc_s, double Cr_o, double Cr_s);

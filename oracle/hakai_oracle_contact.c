@@ -11,6 +11,7 @@
  * Node ids are global (the reference works on part-local ids plus instance node offsets, the
  * same numbers). The face-orientation test uses the model's (instance) coordinates.
  */
+#define _GNU_SOURCE /* qsort_r */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -52,12 +53,14 @@ typedef struct {
     int64_t* faces;          /* [6nE][4] global node ids, oriented */
     int64_t* sorted;         /* [6nE][4] */
     int64_t* face_ele;       /* [6nE] global element id (1-based) */
+    int64_t* order;          /* indexed mode: face indices sorted by (sorted key, index) */
     double young;
 } inst_t;
 
 typedef struct {
     int i_inst, j_inst;      /* 0-based */
     ivec nodes_i, nodes_j, tri, tri_ele;   /* tri: 3 per triangle */
+    char *in_i, *in_j;       /* indexed mode: membership of nodes_i / nodes_j (node id -> 0/1) */
     double young;
 } ct_t;
 
@@ -70,6 +73,12 @@ struct hko_contact {
     ct_t* ct;
     double elementMinSize, elementMaxSize;
     double myu, kc_o, kc_s, Cr_o, Cr_s;
+    /* Indexed mode (a checker for models too large for the literal loops, e.g. BASELINE C4 at
+     * 4 M hex): the same face matches, lists, candidate node sets and event order as the literal
+     * restatement, found through sorted face keys, membership tables and a cell index instead of
+     * the reference's O(F^2) face scan, O(n^2) unique! and O(T x N) node loop. Every result is
+     * identical by construction; tests/test_contact_oracle.py checks it against the literal mode. */
+    int indexed;
 };
 
 static double my3norm(double a, double b, double c) { return sqrt(a * a + b * b + c * c); }
@@ -116,6 +125,55 @@ static int same4(const int64_t* a, const int64_t* b) {
     return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
 }
 
+static int cmp_key4(const int64_t* a, const int64_t* b) {
+    for (int q = 0; q < 4; ++q)
+        if (a[q] != b[q]) return a[q] < b[q] ? -1 : 1;
+    return 0;
+}
+
+static int cmp_face_r(const void* x, const void* y, void* arg) {
+    const int64_t* sorted = (const int64_t*)arg;
+    const int64_t a = *(const int64_t*)x, b = *(const int64_t*)y;
+    const int c = cmp_key4(sorted + 4 * a, sorted + 4 * b);
+    return c ? c : (a < b ? -1 : a > b);
+}
+
+/* indexed mode: faces ordered by (key, index) */
+static void face_order(inst_t* I) {
+    const int64_t F = 6 * I->nE;
+    I->order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(F > 0 ? F : 1));
+    for (int64_t j = 0; j < F; ++j) I->order[j] = j;
+    qsort_r(I->order, (size_t)F, sizeof(int64_t), cmp_face_r, I->sorted);
+}
+
+/* first position in I->order whose face key is >= key */
+static int64_t order_lower(const inst_t* I, const int64_t* key) {
+    int64_t lo = 0, hi = 6 * I->nE;
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (cmp_key4(I->sorted + 4 * I->order[mid], key) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* The exterior-face marks of the literal scan below (j = 1:6nE-1, first later match of j marks
+ * that match as seen): within a run of equal keys in index order, faces pair up two by two and an
+ * odd run keeps its last face, unless that face is the instance's last (never visited as j). */
+static void exterior_marks_indexed(const inst_t* I, char* keep) {
+    const int64_t F = 6 * I->nE;
+    int64_t a = 0;
+    while (a < F) {
+        int64_t b = a + 1;
+        while (b < F && same4(I->sorted + 4 * I->order[a], I->sorted + 4 * I->order[b])) ++b;
+        if ((b - a) & 1) {
+            const int64_t last = I->order[b - 1];
+            if (last < F - 1) keep[last] = 1;
+        }
+        a = b;
+    }
+}
+
 /* get_surface_triangle, v2/HAKAI_j.jl:1996-2164. contact: instance-local 1-based element list of a
  * *Contact Pair surface (n_contact < 0: all elements); like the reference the exterior faces are
  * filtered only when the list length differs from the instance's element count (:2087). */
@@ -125,15 +183,24 @@ static void surface_triangles_of(const inst_t* I, ivec* tri, ivec* tri_ele, ivec
                                  int64_t n_contact) {
     const int64_t F = 6 * I->nE;
     char* dp = (char*)calloc((size_t)F + 1, 1);
+    char* keep = NULL;
+    if (I->order) {
+        keep = (char*)calloc((size_t)F + 1, 1);
+        exterior_marks_indexed(I, keep);
+    }
     for (int64_t j = 0; j < F - 1; ++j) { /* j = 1 : nE*6-1 */
         if (dp[j]) continue;
         int u = 1;
-        for (int64_t k = j + 1; k < F; ++k)
-            if (same4(I->sorted + 4 * j, I->sorted + 4 * k)) {
-                u = 0;
-                dp[k] = 1;
-                break;
-            }
+        if (keep) {
+            u = keep[j];
+        } else {
+            for (int64_t k = j + 1; k < F; ++k)
+                if (same4(I->sorted + 4 * j, I->sorted + 4 * k)) {
+                    u = 0;
+                    dp[k] = 1;
+                    break;
+                }
+        }
         if (u && n_contact >= 0 && n_contact != I->nE) { /* "pick up only contact element" */
             const int64_t local = I->face_ele[j] - I->e0;  /* 1-based instance-local */
             int in = 0;
@@ -149,6 +216,7 @@ static void surface_triangles_of(const inst_t* I, ivec* tri, ivec* tri_ele, ivec
         }
     }
     free(dp);
+    free(keep);
     /* sort!(unique!(c_nodes)) */
     const int64_t n0 = nodes->n;
     for (int64_t i = 0; i < tri->n; ++i) iv_push(nodes, tri->v[i]);
@@ -167,8 +235,16 @@ hko_contact* hko_contact_create(const hko_model_view* mv, int contact_flag, cons
 hko_contact* hko_contact_create_cp(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
                                    const double* mat_young, int32_t n_cp, const int32_t* cp_instance,
                                    const int64_t* cp_off, const int64_t* cp_elems) {
+    return hko_contact_create_ex(mv, contact_flag, element_instance, mat_young, n_cp, cp_instance, cp_off, cp_elems,
+                                 0);
+}
+
+hko_contact* hko_contact_create_ex(const hko_model_view* mv, int contact_flag, const int64_t* element_instance,
+                                   const double* mat_young, int32_t n_cp, const int32_t* cp_instance,
+                                   const int64_t* cp_off, const int64_t* cp_elems, int indexed) {
     if (contact_flag < 1) return NULL;
     hko_contact* C = (hko_contact*)calloc(1, sizeof(hko_contact));
+    C->indexed = indexed;
     C->view = *mv;
     C->mv = &C->view;
     mv = C->mv;
@@ -187,7 +263,10 @@ hko_contact* hko_contact_create_cp(const hko_model_view* mv, int contact_flag, c
         }
         I->nE++;
     }
-    for (int i = 0; i < n_inst; ++i) element_faces(mv, &C->inst[i]);
+    for (int i = 0; i < n_inst; ++i) {
+        element_faces(mv, &C->inst[i]);
+        if (indexed) face_order(&C->inst[i]);
+    }
     /* pairs, :273-311 (all exterior) or the *Contact Pair list (:1063-1102) */
     int np = 0;
     int (*pi)[2] = (int (*)[2])malloc(sizeof(int[2]) * (size_t)(n_inst * (n_inst + 1) / 2 + 1 + n_cp));
@@ -225,6 +304,12 @@ hko_contact* hko_contact_create_cp(const hko_model_view* mv, int contact_flag, c
             free(tri.v); free(te.v);
             surface_triangles_of(&C->inst[T->j_inst], &T->tri, &T->tri_ele, &T->nodes_j, lj, nj);
             T->young = C->inst[T->j_inst].young;  /* :367 */
+            if (indexed) {
+                T->in_i = (char*)calloc((size_t)mv->nN + 1, 1);
+                T->in_j = (char*)calloc((size_t)mv->nN + 1, 1);
+                for (int64_t q = 0; q < T->nodes_i.n; ++q) T->in_i[T->nodes_i.v[q]] = 1;
+                for (int64_t q = 0; q < T->nodes_j.n; ++q) T->in_j[T->nodes_j.v[q]] = 1;
+            }
         }
     }
     free(pi);
@@ -253,10 +338,11 @@ void hko_contact_set_params(hko_contact* C, double myu, double kc_o, double kc_s
 void hko_contact_destroy(hko_contact* C) {
     if (!C) return;
     for (int i = 0; i < C->n_inst; ++i) {
-        free(C->inst[i].faces); free(C->inst[i].sorted); free(C->inst[i].face_ele);
+        free(C->inst[i].faces); free(C->inst[i].sorted); free(C->inst[i].face_ele); free(C->inst[i].order);
     }
     for (int c = 0; c < C->n_ct; ++c) {
         free(C->ct[c].nodes_i.v); free(C->ct[c].nodes_j.v); free(C->ct[c].tri.v); free(C->ct[c].tri_ele.v);
+        free(C->ct[c].in_i); free(C->ct[c].in_j);
     }
     free(C->inst);
     free(C->ct);
@@ -273,6 +359,19 @@ void hko_contact_element_deleted(hko_contact* C, const int64_t* element_instance
     const int64_t j0 = (e1 - 1 - I->e0) * 6;
     for (int j = 0; j < 6; ++j) {
         const int64_t* sj = I->sorted + 4 * (j0 + j);
+        if (I->order) { /* indexed: the first face (index order) with this key, not of ele */
+            for (int64_t q = order_lower(I, sj); q < F && same4(sj, I->sorted + 4 * I->order[q]); ++q) {
+                const int64_t k = I->order[q];
+                if (I->face_ele[k] == ele) continue;
+                const int64_t* f = I->faces + 4 * k;
+                iv_push(&add_tri, f[0]); iv_push(&add_tri, f[1]); iv_push(&add_tri, f[2]);
+                iv_push(&add_tri, f[2]); iv_push(&add_tri, f[3]); iv_push(&add_tri, f[0]);
+                iv_push(&add_ele, I->face_ele[k]);
+                iv_push(&add_ele, I->face_ele[k]);
+                break;
+            }
+            continue;
+        }
         for (int64_t k = 0; k < F; ++k) {
             if (I->face_ele[k] == ele) continue;
             if (same4(sj, I->sorted + 4 * k)) {
@@ -291,11 +390,27 @@ void hko_contact_element_deleted(hko_contact* C, const int64_t* element_instance
     for (int c = 0; c < C->n_ct; ++c) {
         ct_t* T = &C->ct[c];
         if (T->i_inst == ii) {
-            for (int64_t i = 0; i < add_nodes.n; ++i) iv_push(&T->nodes_i, add_nodes.v[i]);
-            iv_unique_inplace(&T->nodes_i);
+            if (T->in_i) { /* unique! keeps first occurrences: append the nodes not yet listed */
+                for (int64_t i = 0; i < add_nodes.n; ++i)
+                    if (!T->in_i[add_nodes.v[i]]) {
+                        T->in_i[add_nodes.v[i]] = 1;
+                        iv_push(&T->nodes_i, add_nodes.v[i]);
+                    }
+            } else {
+                for (int64_t i = 0; i < add_nodes.n; ++i) iv_push(&T->nodes_i, add_nodes.v[i]);
+                iv_unique_inplace(&T->nodes_i);
+            }
         } else if (T->j_inst == ii) {
-            for (int64_t i = 0; i < add_nodes.n; ++i) iv_push(&T->nodes_j, add_nodes.v[i]);
-            iv_unique_inplace(&T->nodes_j);
+            if (T->in_j) {
+                for (int64_t i = 0; i < add_nodes.n; ++i)
+                    if (!T->in_j[add_nodes.v[i]]) {
+                        T->in_j[add_nodes.v[i]] = 1;
+                        iv_push(&T->nodes_j, add_nodes.v[i]);
+                    }
+            } else {
+                for (int64_t i = 0; i < add_nodes.n; ++i) iv_push(&T->nodes_j, add_nodes.v[i]);
+                iv_unique_inplace(&T->nodes_j);
+            }
             for (int64_t i = 0; i < add_ele.n; ++i) iv_push(&T->tri_ele, add_ele.v[i]);
             for (int64_t i = 0; i < add_tri.n; ++i) iv_push(&T->tri, add_tri.v[i]);
         }
@@ -304,6 +419,26 @@ void hko_contact_element_deleted(hko_contact* C, const int64_t* element_instance
 }
 
 static int64_t map_of(double p, double mn, double ddiv) { return (int64_t)ceil((p - mn) / ddiv); }
+
+typedef struct {
+    int64_t key, k;
+} cellk_t;
+
+static int cmp_cellk(const void* x, const void* y) {
+    const cellk_t *a = (const cellk_t*)x, *b = (const cellk_t*)y;
+    if (a->key != b->key) return a->key < b->key ? -1 : 1;
+    return a->k < b->k ? -1 : a->k > b->k;
+}
+
+static int64_t cell_lower(const cellk_t* c, int64_t n, int64_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (c[mid].key < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 /* cal_contact_force, v2/HAKAI_j.jl:2248-2706 (one thread => c_force3[:,1]), then
  * external_force[i] += c_force3[i] (:536-538): one rounding of the Float128 sum to Float64. */
@@ -345,6 +480,24 @@ int64_t hko_contact_force(const hko_contact* C, const double* position, const do
         for (int64_t k = 0; k < nn_i; ++k)
             for (int d = 0; d < 3; ++d) mapi[3 * k + d] = map_of(position[3 * (T->nodes_i.v[k] - 1) + d], amn[d], ddiv);
         const double kc = self ? C->kc_s : C->kc_o, Cr = self ? C->Cr_s : C->Cr_o;
+        /* indexed mode: i-nodes by cell, (cell key, k) ascending */
+        cellk_t* cells = NULL;
+        int64_t M1 = 0, M2 = 0, M0 = 0;
+        int64_t* cand = NULL;
+        if (C->indexed) {
+            for (int64_t k = 0; k < nn_i; ++k) {
+                if (mapi[3 * k] > M0) M0 = mapi[3 * k];
+                if (mapi[3 * k + 1] > M1) M1 = mapi[3 * k + 1];
+                if (mapi[3 * k + 2] > M2) M2 = mapi[3 * k + 2];
+            }
+            cells = (cellk_t*)malloc(sizeof(cellk_t) * (size_t)nn_i);
+            for (int64_t k = 0; k < nn_i; ++k) {
+                cells[k].key = (mapi[3 * k] * (M1 + 1) + mapi[3 * k + 1]) * (M2 + 1) + mapi[3 * k + 2];
+                cells[k].k = k;
+            }
+            qsort(cells, (size_t)nn_i, sizeof(cellk_t), cmp_cellk);
+            cand = (int64_t*)malloc(sizeof(int64_t) * (size_t)nn_i);
+        }
         const int64_t ntri = T->tri_ele.n;
         for (int64_t j = 0; j < ntri; ++j) {
             const int64_t eleid = T->tri_ele.v[j];
@@ -380,7 +533,22 @@ int64_t hko_contact_force(const hko_contact* C, const double* position, const do
             const double A13 = -nx, A23 = -ny, A33 = -nz;
             const int64_t mj0[3] = {map_of(q0x, amn[0], ddiv), map_of(q0y, amn[1], ddiv), map_of(q0z, amn[2], ddiv)};
             const int64_t* el = mv->elementmat + 8 * (eleid - 1);
-            for (int64_t k = 0; k < nn_i; ++k) {
+            int64_t ncand = nn_i;
+            if (C->indexed) { /* the nodes of the 27 cells around mj0, in ascending k like the loop */
+                ncand = 0;
+                for (int64_t dx = -1; dx <= 1; ++dx)
+                    for (int64_t dy = -1; dy <= 1; ++dy)
+                        for (int64_t dz = -1; dz <= 1; ++dz) {
+                            const int64_t x = mj0[0] + dx, y = mj0[1] + dy, z = mj0[2] + dz;
+                            if (x < 0 || y < 0 || z < 0 || x > M0 || y > M1 || z > M2) continue;
+                            const int64_t key = (x * (M1 + 1) + y) * (M2 + 1) + z;
+                            for (int64_t q = cell_lower(cells, nn_i, key); q < nn_i && cells[q].key == key; ++q)
+                                cand[ncand++] = cells[q].k;
+                        }
+                qsort(cand, (size_t)ncand, sizeof(int64_t), cmp_i64);
+            }
+            for (int64_t kq = 0; kq < ncand; ++kq) {
+                const int64_t k = C->indexed ? cand[kq] : kq;
                 if (llabs(mj0[0] - mapi[3 * k]) > 1 || llabs(mj0[1] - mapi[3 * k + 1]) > 1 ||
                     llabs(mj0[2] - mapi[3 * k + 2]) > 1)
                     continue;
@@ -436,6 +604,8 @@ int64_t hko_contact_force(const hko_contact* C, const double* position, const do
             }
         }
         free(mapi);
+        free(cells);
+        free(cand);
     }
     for (int64_t i = 0; i < fn; ++i) external_force[i] = (double)((__float128)external_force[i] + acc[i]);
     free(acc);

@@ -63,6 +63,9 @@ def lib():
         L.hko_contact_create.argtypes = [POINTER(View), c_int, PI64, PD]
         L.hko_contact_create_cp.restype = c_void_p
         L.hko_contact_create_cp.argtypes = [POINTER(View), c_int, PI64, PD, c_int32, POINTER(c_int32), PI64, PI64]
+        L.hko_contact_create_ex.restype = c_void_p
+        L.hko_contact_create_ex.argtypes = [POINTER(View), c_int, PI64, PD, c_int32, POINTER(c_int32), PI64, PI64,
+                                            c_int]
         L.hko_contact_destroy.argtypes = [c_void_p]
         L.hko_contact_set_params.argtypes = [c_void_p, c_double, c_double, c_double, c_double, c_double]
         L.hko_contact_force.restype = c_int64
@@ -90,7 +93,9 @@ def _p(a, t=c_double):
 class Oracle:
     """CPU restatement of the reference time loop for one Model (hakai.model.Model)."""
 
-    def __init__(self, model, nthreads: int = 1):
+    def __init__(self, model, nthreads: int = 1, contact_indexed: bool = False):
+        """contact_indexed: the contact setup/search through sorted face keys and a cell index
+        (identical results, tests/test_contact_oracle.py; needed at BASELINE C4's 4 M hex)."""
         self.L = lib()
         self.m = model
         self.nthreads = nthreads
@@ -138,9 +143,9 @@ class Oracle:
                               _p(model.element_material, c_int64))
             ncp, cpi, cpo, cpe = model.c_contact_pairs()
             self._cp = (cpi, cpo, cpe)
-            self.ct = self.L.hko_contact_create_cp(ctypes.byref(self._view), int(model.contact_flag),
+            self.ct = self.L.hko_contact_create_ex(ctypes.byref(self._view), int(model.contact_flag),
                                                    _p(self._inst, c_int64), _p(self._young), ncp, _p(cpi, c_int32),
-                                                   _p(cpo, c_int64), _p(cpe, c_int64))
+                                                   _p(cpo, c_int64), _p(cpe, c_int64), int(contact_indexed))
             cp = getattr(model, "contact_params", None)
             if cp is not None:
                 self.L.hko_contact_set_params(self.ct, *[float(x) for x in cp])

@@ -117,3 +117,36 @@ def test_reference_charpy_contact_pairs():
         f, n = o.contact_force()
         fr, nr = _ref_force(ref, o)
         assert n == nr and np.array_equal(f, fr)
+
+
+@pytest.mark.parametrize("case", ["deletion", "self", "pair_surfaces", "charpy_deck"])
+def test_indexed_oracle_equals_literal(case):
+    """The oracle's indexed contact mode (sorted face keys, membership tables, cell index; the
+    checker for BASELINE C4 at 4 M hex) reproduces the literal restatement bit for bit: pair lists,
+    surface updates after deletions, contact events and the whole trajectory."""
+    if case == "deletion":
+        m, n = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400), 400
+    elif case == "self":
+        m, n = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 3), v=-1e5, perturb=0.02, seed=1,
+                                   contact_flag=2), 300
+    elif case == "pair_surfaces":
+        m, n = mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 2), v=-1e5, perturb=0.02, seed=1,
+                                   surfaces=True), 300
+    else:
+        import os
+        from deck_fixtures import model_from_arrays
+        z = np.load(os.path.join(os.path.dirname(__file__), "golden", "deck_Charpy_test.npz"))
+        m, n = model_from_arrays(z, "Charpy_test"), 1500
+    a, b = O.Oracle(m), O.Oracle(m, contact_indexed=True)
+    assert a.contact_pairs() == b.contact_pairs()
+    a.run(1, n)
+    b.run(1, n)
+    assert a.deletions == b.deletions
+    for k in ("disp", "disp_pre", "integ_stress", "element_flag"):
+        assert np.array_equal(a.s[k], b.s[k]), k
+    assert a.contact_pairs() == b.contact_pairs()
+    fa, na = a.contact_force()
+    fb, nb = b.contact_force()
+    assert na == nb and np.array_equal(fa, fb)
+    if case == "deletion":
+        assert len(a.deletions) >= 4

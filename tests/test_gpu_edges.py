@@ -86,3 +86,50 @@ def test_bad_indices_fail_loudly(what):
     m = _clone(base, em, mm)
     with pytest.raises(Exception, match="out of"):
         Solver(m, diag_M=np.ones(3 * m.nNode))
+
+
+@pytest.mark.parametrize("case", ["ragged", "inverted"])
+def test_edge_meshes_exact_mode_bitexact(case):
+    """The reference-order kernel (elem_exact) on the ragged (CSR gather) and the inverted mesh
+    (negative det: |det| in BVbar, signed det in Bfinal and the force weight): bit-identical."""
+    base = small_bar(3, 2, 6, v_end=2e5, n_steps=300)
+    if case == "ragged":
+        m = _clone(base, np.repeat(base.elementmat, 2, axis=0), np.repeat(base.element_material, 2))
+    else:
+        m = _clone(base, base.elementmat[:, [4, 5, 6, 7, 0, 1, 2, 3]].copy(), base.element_material.copy())
+    o = O.Oracle(m)
+    o.run(1, 300)
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", 1)
+        sv.step(1, 300)
+        g = sv.download()
+    for k in ("disp", "disp_pre", "integ_stress", "integ_strain", "integ_eq_plastic_strain", "Q"):
+        assert np.array_equal(getattr(g, k), o.s[k]), k
+
+
+def test_reupload_larger_model_without_bc():
+    """hakai_upload_model drops the BC tables sized for the previous mesh (the fused-BC per-dof
+    table would be read past its end): a larger model uploaded into a context that had BCs steps
+    like a fresh context without BCs."""
+    import ctypes
+    from hakai._abi import check, ptr
+    small = small_bar(2, 2, 3, n_steps=50)
+    big = small_bar(3, 3, 12, n_steps=50)
+    I64 = ctypes.c_int64
+    diag, _ = big.lumped_mass()
+    with Solver(small) as sv:
+        sv.step(1, 5)
+        mats, keep = big.c_materials()
+        check(sv.L.hakai_upload_model(sv.ctx, big.nNode, ptr(big.coordmat), big.nElement, ptr(big.elementmat, I64),
+                                      ptr(big.element_material, I64), len(big.materials), mats, ptr(diag)))
+        del keep
+        sv.model = big
+        sv.reset()
+        sv.step(1, 50)
+        g = sv.download(disp=True)
+    nobc = _clone(big, big.elementmat.copy(), big.element_material.copy())
+    nobc.bc = []
+    with Solver(nobc) as sv:
+        sv.step(1, 50)
+        r = sv.download(disp=True)
+    assert np.array_equal(g.disp, r.disp)

@@ -20,7 +20,9 @@ def serial_vtk(coordmat, elementmat, flag, disp, velo, ns, nn, ne, nm, nt):
     def f16(x):
         return 0.0 if abs(x) < 1e-16 else x
 
-    def e(x):
+    def e(x):  # Julia's @printf spells non-finite values NaN / Inf / -Inf
+        if not np.isfinite(x):
+            return "NaN" if np.isnan(x) else ("Inf" if x > 0 else "-Inf")
         return "%1.6e" % x
 
     nN, nE = coordmat.size // 3, flag.size
@@ -88,6 +90,22 @@ def test_write_vtk_matches_serial_printf(tmp_path, nN, nE):
     want = serial_vtk(d["coordmat"], d["elementmat"], d["flag"], d["disp"], d["velo"], d["ns"], d["nn"], d["ne"],
                       d["nm"], d["nt"])
     assert got == want
+
+
+def test_write_vtk_non_finite_values_as_julia(tmp_path):
+    """A diverged state: NaN and +-Inf print as Julia's @printf does ("NaN", "Inf", "-Inf")."""
+    d = random_fields(37, 11, seed=5)
+    d["disp"][::7] = np.nan
+    d["velo"][1::5] = np.inf
+    d["ns"][2::3] = -np.inf
+    d["nm"][0] = -np.nan
+    check(hakai.lib().hakai_write_vtk(str(tmp_path).encode(), 1, 37, ptr(d["coordmat"]), 11,
+                                      ptr(d["elementmat"], I64), *field_ptrs(d)))
+    got = (tmp_path / "file001.vtk").read_bytes()
+    want = serial_vtk(d["coordmat"], d["elementmat"], d["flag"], d["disp"], d["velo"], d["ns"], d["nn"], d["ne"],
+                      d["nm"], d["nt"])
+    assert got == want
+    assert b"NaN" in got and b"\nInf\n" in got and b"-Inf" in got and b"nan" not in got and b"inf" not in got
 
 
 @pytest.mark.parametrize("threads", [1, 3, 16])
