@@ -95,7 +95,7 @@ static void free_model(hakai_ctx* c) {
 }
 
 static void free_bc(hakai_ctx* c) {
-    dfree(c->d_bc_of_dof);
+    dfree(c->d_bc_of_node);
     dfree(c->d_bc_dof);
     dfree(c->d_bc_grp);
     dfree(c->d_bc_val);
@@ -255,6 +255,7 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.nmat = c->nmat;
     ea.exact = c->elem_exact;
     ea.pusai = c->d_pusai;
+    ea.fe_mask = c->diag_no_assembly ? 0 : -1;
     return ea;
 }
 
@@ -579,13 +580,14 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
         HIPCHK(hipMemcpyAsync(c->d_amp_t, bc->amp_time, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(c->d_amp_v, bc->amp_value, n_amp * sizeof(double), hipMemcpyHostToDevice, s));
     }
-    // small meshes: per-dof entry table, so the nodal kernel applies the BCs itself (hakai_step)
+    // per-node table: the first resolved entry of each node (entries are sorted by dof, a node's
+    // up-to-3 entries are consecutive) or -1, so the nodal kernel applies the BCs itself
+    // (hakai_step; 4 B per node)
     if (!dof.empty() && c->nN <= kFuseBcMaxNodes) {
-        std::vector<int> of(3 * (size_t)c->nN, -1);
-        for (size_t i = 0; i < dof.size(); ++i)
-            if (dof[i] >= 0 && (size_t)dof[i] < of.size()) of[(size_t)dof[i]] = (int)i;
-        HIPCHK(dalloc(&c->d_bc_of_dof, of.size()));
-        HIPCHK(hipMemcpyAsync(c->d_bc_of_dof, of.data(), of.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        std::vector<int> of((size_t)c->nN, -1);
+        for (size_t i = dof.size(); i-- > 0;) of[(size_t)dof[i] / 3] = (int)i;
+        HIPCHK(dalloc(&c->d_bc_of_node, of.size()));
+        HIPCHK(hipMemcpyAsync(c->d_bc_of_node, of.data(), of.size() * sizeof(int), hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     return 0;
@@ -790,11 +792,11 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     na.fe_nt = c->nodal_fe_nt;
     na.reverse = c->nodal_reverse;
     na.fe = c->d_fe;
-    na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
+    na.qbuf = (c->q_from_buf || c->diag_no_assembly) ? c->d_qbuf : nullptr;
     na.fext = nullptr;
     na.nN = c->nN;
     na.dt = d_time;
-    na.bc_of_dof = nullptr;
+    na.bc_of_node = nullptr;
     hk::BCArgs ba;
     ba.dof = c->d_bc_dof;
     ba.grp = c->d_bc_grp;
@@ -810,9 +812,9 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     ba.dt = d_time;
     // one GPU, small mesh: the nodal kernel applies the BCs (multi-GPU redoes interface nodes
     // after the nodal kernel, so the BCs must come after that)
-    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_dof && c->fuse_bc && !c->comm;
+    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm;
     if (fuse_bc) {
-        na.bc_of_dof = c->d_bc_of_dof;
+        na.bc_of_node = c->d_bc_of_node;
         na.bc = ba;
     }
     int rc = 0;
@@ -1029,6 +1031,12 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "elem_exact")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact must be 0 or 1");
         c->elem_exact = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "diag_no_assembly")) {  // timing diagnostic only: results are invalid
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "diag_no_assembly must be 0 or 1");
+        if (value && c->model_ok) HIPCHK(hipMemset(c->d_qbuf, 0, 3 * (size_t)c->nN * sizeof(double)));
+        c->diag_no_assembly = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_map")) {

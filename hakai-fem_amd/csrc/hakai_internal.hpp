@@ -20,7 +20,11 @@ struct EventPair {
     int kernel;
 };
 
-constexpr long long kFuseBcMaxNodes = 1 << 18;  // BCs fused into k_nodal up to this many nodes
+
+// BCs fused into k_nodal up to this many nodes: the per-node lookup (4 B/node, one dependent load)
+// costs more than the k_bc launch it saves on large meshes (C3: nodal 0.165 -> 0.180 ms, measured
+// profiles/r02_assembly_bound_sweep.log), and wins on launch-bound small decks.
+constexpr long long kFuseBcMaxNodes = 1 << 18;
 
 struct hakai_ctx {
     int device = 0;
@@ -66,6 +70,9 @@ struct hakai_ctx {
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
     int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
     int elem_exact = 0;          // tuning "elem_exact": reference-order element arithmetic
+    int diag_no_assembly = 0;    // tuning "diag_no_assembly": TIMING DIAGNOSTIC, results invalid --
+                                 // no element-force traffic (rows to one dummy row, Q read from a
+                                 // zero buffer): the step's cost without any force assembly
     double* d_pusai = nullptr;   // cal_Pusai_hexa table for the exact element kernel (192 doubles)
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
@@ -78,7 +85,7 @@ struct hakai_ctx {
     int* d_amp_off = nullptr;
     double* d_amp_t = nullptr;
     double* d_amp_v = nullptr;
-    int* d_bc_of_dof = nullptr;  // [3nN] resolved BC entry per dof (-1 none); small meshes only
+    int* d_bc_of_node = nullptr; // [nN] first resolved BC entry of each node (-1 none)
     int fuse_bc = 1;             // tuning "fuse_bc": the nodal kernel applies the BCs (one GPU)
     // state extras
     double* d_qbuf = nullptr;

@@ -110,7 +110,7 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
                                                bool kill, const double (&fk)[3], const double (&fin)[6],
                                                const double (&eps)[6], double eqp, double ys, double tri) {
     const long long gp = 8 * e + k, ld = a.ld;
-    double* fo = a.fe + in.fb;
+    double* fo = a.fe + (in.fb & a.fe_mask);
     fo[0] = active ? fk[0] : 0.0;
     fo[a.cstride] = active ? fk[1] : 0.0;
     fo[2 * a.cstride] = active ? fk[2] : 0.0;
@@ -914,13 +914,15 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
     const double mdt2 = m / (dt * dt);
     const double inv = 1.0 / (mdt2 + dC / 2.0 / dt);
     const double Q[3] = {Q0, Q1, Q2};
+    const int b0 = BCF ? a.bc_of_node[n] : -1;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double up = in.up[c];
         double v = inv * (in.f[c] - Q[c] + mdt2 * (2.0 * in.uc[c] - up) + dC / 2.0 / dt * up);
-        if (BCF) {  // what k_bc would overwrite afterwards
-            const int bi = a.bc_of_dof[3 * n + c];
-            if (bi >= 0) v = bc_value(a.bc, bi);
+        if (BCF) {  // what k_bc would overwrite afterwards: the node's entries are consecutive
+            const long long dc = 3 * n + c;
+            for (int j = b0; j >= 0 && j < a.bc.n && a.bc.dof[j] <= dc; ++j)
+                if (a.bc.dof[j] == dc) v = bc_value(a.bc, j);
         }
         a.u_pre_out[3 * n + c] = v;
     }
@@ -1005,7 +1007,7 @@ static void launch_nodal_a(const NodalArgs& a, unsigned grid, hipStream_t s) {
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
     if (a.nN <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((a.nN + kBlock - 1) / kBlock);
-    if (a.bc_of_dof) {
+    if (a.bc_of_node) {
         if (a.fext)
             launch_nodal_a<true, true>(a, grid, s);
         else

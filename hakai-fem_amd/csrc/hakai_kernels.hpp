@@ -39,6 +39,8 @@ struct ElemArgs {
     int exact;              // 1: reference-order arithmetic (elem_step_exact), bit-identical to
                             //    cal_stress_hexa; 0: fused single-pass form (elem_step)
     const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
+    long long fe_mask;      // -1; 0 only in the timing diagnostic "diag_no_assembly" (all force
+                            // rows land on one dummy row: no fe traffic, results invalid)
 };
 
 struct BCArgs {
@@ -72,8 +74,8 @@ struct NodalArgs {
     int reverse;           // 1: each XCD walks its node chunk from the end (xcd_remap_rev)
     long long nN;
     double dt;
-    const int* bc_of_dof;  // small meshes, one GPU: [3nN] entry of `bc` per dof (-1 none); the
-    BCArgs bc;             // nodal kernel then applies the BCs itself (no k_bc launch)
+    const int* bc_of_node; // one GPU: [nN] first entry of `bc` of each node (-1 none); the nodal
+    BCArgs bc;             // kernel then applies the BCs itself (no k_bc launch)
 };
 
 

@@ -22,18 +22,24 @@ import oracle as O  # noqa: E402
 from deck_fixtures import model_to_arrays  # noqa: E402
 
 REF = "/root/reference"
-DECKS = [  # (deck, steps): contact with deletion, self-contact, a projectile with deletion
-    ("HAKAI-v0.0.0/input/Charpy-test.inp", 6200),
-    ("HAKAI-v0.0.1/input/crash-tube-80-350-solid.inp", 2000),
-    ("HAKAI-v0.0.0/input/bullet-impact.inp", 12000),
+DECKS = [  # (deck, steps, indexed oracle contact)
+    ("HAKAI-v0.0.0/input/Charpy-test.inp", 6200, False),               # contact + deletion
+    ("HAKAI-v0.0.1/input/crash-tube-80-350-solid.inp", 2000, False),   # self-contact option
+    ("HAKAI-v0.0.0/input/bullet-impact.inp", 12000, False),            # projectile + deletion
+    ("HAKAI-v0.0.2/input/car-crash-N2k.inp", 0, False),                # v0.0.2, whole run
+    ("HAKAI-v0.0.2/input/car-wall-N2k.inp", 0, True),                  # v0.0.2 self-contact, whole run
 ]
 
 
 def main():
     out = os.path.join(ROOT, "tests", "golden")
-    for deck, steps in DECKS:
+    sel = sys.argv[1:]
+    for deck, steps, indexed in DECKS:
+        if sel and not any(x in deck for x in sel):
+            continue
         m = hakai.read_inp(os.path.join(REF, deck))
-        o = O.Oracle(m)
+        steps = steps or m.n_steps
+        o = O.Oracle(m, nthreads=int(os.environ.get("OMP_NUM_THREADS", "4")), contact_indexed=indexed)
         t0 = time.time()
         o.run(1, steps)
         f, nev = o.contact_force()
