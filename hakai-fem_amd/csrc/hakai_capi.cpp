@@ -256,6 +256,7 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.exact = c->elem_exact;
     ea.pusai = c->d_pusai;
     ea.fe_mask = c->diag_no_assembly ? 0 : -1;
+    ea.poison = c->d_poison;
     return ea;
 }
 
@@ -370,8 +371,11 @@ int hakai_create(hakai_ctx** out, int device) {
         delete c;
         return hip_fail(e, "hipStreamCreate");
     }
-    if (dalloc(&c->d_negjac, 1) != hipSuccess || dalloc(&c->d_pusai, 192) != hipSuccess) {
+    if (dalloc(&c->d_negjac, 1) != hipSuccess || dalloc(&c->d_pusai, 192) != hipSuccess ||
+        dalloc(&c->d_poison, 2) != hipSuccess || hipMemset(c->d_poison, 0, 2 * sizeof(int)) != hipSuccess) {
         dfree(c->d_negjac);
+        dfree(c->d_pusai);
+        dfree(c->d_poison);
         delete c;
         return fail(HAKAI_ERR_DEVICE, "hipMalloc for context bookkeeping failed");
     }
@@ -382,6 +386,7 @@ int hakai_create(hakai_ctx** out, int device) {
         if (e != hipSuccess) {
             dfree(c->d_negjac);
             dfree(c->d_pusai);
+            dfree(c->d_poison);
             delete c;
             return hip_fail(e, "hipMemcpy (Pusai table)");
         }
@@ -403,6 +408,7 @@ int hakai_destroy(hakai_ctx* c) {
     hkc::free_bc(c);
     dfree(c->d_negjac);
     dfree(c->d_pusai);
+    dfree(c->d_poison);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -610,6 +616,8 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     c->h_velo0.assign(fn, 0.0);
     c->q_from_buf = false;
     c->steps_done = 0;
+    c->poison_halt = false;
+    HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), s));
     hkc::comm_reset(c);
     if (n_ic > 0) {
         if (!ic_dofs || !ic_values) return fail(HAKAI_ERR_ARG, "reset_state: null IC arrays");
@@ -691,8 +699,10 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
         int r = fe_upload_qe(c, st->Qe);
         if (r) return r;
     }
+    HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), s));
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
+    c->poison_halt = false;
     hkc::comm_reset(c);
     c->state_ok = true;
     if (c->contact) {
@@ -810,6 +820,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
     ba.ct = t * d_time;
     ba.t_rd = c->g_trd;
     ba.dt = d_time;
+    ba.poison = c->d_poison;
+    na.poison = c->d_poison;
     // one GPU, small mesh: the nodal kernel applies the BCs (multi-GPU redoes interface nodes
     // after the nodal kernel, so the BCs must come after that)
     const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm;
@@ -924,7 +936,12 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step: n_steps=%lld d_time=%g", (long long)n_steps, d_time);
     if (n_steps > 1 && hkc::comm_is_local(c))
         return fail(HAKAI_ERR_ARG, "step: an in-process group is stepped one step per call, rank by rank");
+    if (c->poison_halt)
+        return fail(HAKAI_ERR_STATE, "step: a multi-GPU contact buffer overflowed; the state is that of the last good "
+                    "step -- raise the capacity and hakai_upload_state / hakai_reset_state on every rank");
     HIPCHK(hipSetDevice(c->device));
+    const int cur0 = c->cur;
+    const long long done0 = c->steps_done;
     int64_t it = 0;
     while (it < n_steps) {
         const double t = t_first + (double)it;
@@ -943,7 +960,27 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         }
         if (rc) return rc;
     }
-    return hkc::contact_check(c);
+    const int rc = hkc::contact_check(c);
+    if (rc && c->contact) {
+        // An overflow poisoned step p: the device state-writing kernels of steps p.. were no-ops, so
+        // the device holds the state after step p-1. Bring the host's view back to that step.
+        int pz[2] = {0, 0};
+        HIPCHK(hipMemcpy(pz, c->d_poison, sizeof pz, hipMemcpyDeviceToHost));
+        if (pz[0]) {
+            const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
+            if (good >= 0 && good <= n_steps) {
+                c->cur = (good & 1) ? 1 - cur0 : cur0;
+                c->steps_done = done0 + good;
+            }
+            hkc::graph_invalidate(c);
+            hkc::contact_after_overflow(c, c->steps_done);
+            HIPCHK(hipMemset(c->d_poison, 0, 2 * sizeof(int)));
+            const std::string msg = hakai_last_error();
+            return fail(rc, "%s; step %d was not applied: the state is that after step %d", msg.c_str(), pz[1],
+                        pz[1] - 1);
+        }
+    }
+    return rc;
 }
 
 int hakai_graph_steps(hakai_ctx* c, int64_t* n) {

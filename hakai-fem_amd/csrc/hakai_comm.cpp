@@ -130,8 +130,9 @@ __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const i
 __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
                       const double* fe, long long cs, int nslot, const double* up_sendP, const double* up_recvC,
                       const double* dn_recvP, const double* saved, const double* u, double* out, const double* mass,
-                      const double* fext, double dt) {
+                      const double* fext, double dt, const int* poison) {
 #pragma clang fp contract(off)
+    if (*poison) return;  // contact overflow earlier in the call: the state stays the last good step's
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_up + n_dn) return;
     double Q[3];
@@ -341,7 +342,7 @@ int comm_post_nodal(hakai_ctx* c, double d_time) {
         hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
                            c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
                            m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, c->contact ? c->d_fext : nullptr,
-                           d_time);
+                           d_time, c->d_poison);
         HIPCHK(hipGetLastError());
     }
     prof_end(c, &ep);

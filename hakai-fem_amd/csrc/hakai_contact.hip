@@ -953,10 +953,23 @@ __device__ __forceinline__ long long ev_slot(const unsigned* s_pre, long long sh
 // Per-node gather of the event terms over the nodes that received one ("touched", a compact list
 // instead of a pass over all nN nodes): count -> per-node term ranges by a wave-aggregated bump
 // allocator (ranges are disjoint; their order is irrelevant) -> scatter -> sum.
+// Block 0 also poisons the step when a buffer overflowed in it (events beyond a shard, candidate
+// triangles beyond their buffer, a truncated multi-GPU mirror block): the nodal, BC, element and
+// interface kernels of this and later steps of the call then write nothing (hakai_kernels.hip,
+// poisoned), so the state stays the last good step's and hakai_step reports the overflow.
 __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                           int* cnt, int* touched, int* tpos, int tsel) {
+                           int* cnt, int* touched, int* tpos, int tsel, int* poison, long long cand_cap,
+                           const int* x1ctl, int t, const double* t_rd) {
     __shared__ unsigned s_pre[kEvShards + 1];
     const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0);
+        for (int q = 0; q < kEvShards; ++q) over |= (long long)evs[q * kShardStride] > shard_cap;
+        if (over && poison[0] == 0) {
+            poison[1] = t_rd ? (int)*t_rd + 1 : t;
+            poison[0] = 1;
+        }
+    }
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
@@ -1703,7 +1716,8 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     }
     const unsigned ge = (unsigned)C->g_ev;
     hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel);
+                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, C->cand_cap,
+                       M ? M->d_x1ctl : nullptr, in.t, c->g_trd);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
@@ -1726,6 +1740,19 @@ bool contact_graph_ok(const hakai_ctx* c, double t) {
     const Contact* C = c->contact;
     if (!C) return true;
     return !C->mir && !C->force_rebuild && !C->always_rebuild && !C->use_velo0 && (long long)t == C->last_t + 1;
+}
+
+// hakai_step found a poisoned step: the device state is the last good step's. Rebuild the live
+// lists at the next step; velo of the first step is the initial one only if no step survived. A
+// multi-GPU mirror's block sequence has advanced past the good step: steps are refused until the
+// state is uploaded or reset on every rank.
+void contact_after_overflow(hakai_ctx* c, long long steps_since_reset) {
+    Contact* C = c->contact;
+    if (!C) return;
+    C->force_rebuild = true;
+    C->use_velo0 = steps_since_reset == 0;
+    C->last_t = -1;
+    if (C->mir) c->poison_halt = true;
 }
 
 void contact_graph_advance(hakai_ctx* c, double t_last) {
@@ -2567,6 +2594,7 @@ int hakai_contact_force(hakai_ctx* c, double t, double d_time, double* external_
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(external_force, c->d_fext, 3 * (size_t)c->nN * sizeof(double), hipMemcpyDeviceToHost,
                           c->stream));
+    HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), c->stream));  // a probe changes no state
     HIPCHK(hipStreamSynchronize(c->stream));
     return hkc::contact_check(c);
 }

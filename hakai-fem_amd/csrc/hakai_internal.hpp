@@ -96,6 +96,8 @@ struct hakai_ctx {
     int* d_del_step = nullptr;   // [nEp+2] deletion step per element (0 = never), [nEp] dump slot,
                                  // [nEp+1] last step in which any element was deleted
     unsigned long long* d_negjac = nullptr;
+    int* d_poison = nullptr;     // [2]: contact buffer overflow in this call (flag, step); see ElemArgs
+    bool poison_halt = false;    // multi-GPU contact overflowed: steps refused until upload/reset
     bool any_plastic = false;
     bool model_ok = false;
     bool state_ok = false;
@@ -155,6 +157,7 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host);
 int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
 int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack the mirror block of the next step
 int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
+void contact_after_overflow(hakai_ctx* c, long long steps_since_reset);  // host state after a poisoned call
 void graph_invalidate(hakai_ctx* c);                      // drop captured step graphs (hakai_step)
 bool contact_graph_ok(const hakai_ctx* c, double t);       // step t's contact work can be captured
 void contact_graph_advance(hakai_ctx* c, double t_last);   // host state after a cached graph's steps

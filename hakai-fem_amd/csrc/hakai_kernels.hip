@@ -635,6 +635,10 @@ __device__ __forceinline__ void stage_pusai(const ElemArgs& a, double* s_pus) {
 // device counter. Every kernel of a step reads slot 1-p (the previous step's number) and adds 1;
 // the element kernel, the last of the step, stores that number into slot p, which the next step
 // reads. A divergent lane stores it, so it is an ordinary vector store.
+// A contact buffer overflowed earlier in this hakai_step call (hakai_contact.hip, k_ct_count):
+// every state-writing kernel returns at once, so the state stays the last good step's.
+__device__ __forceinline__ bool poisoned(const int* p) { return p && *p; }
+
 __device__ __forceinline__ void graph_step(ElemArgs& a) {
     if (a.t_rd) {
         const double tp = *a.t_rd;
@@ -649,6 +653,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
+    if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
@@ -677,6 +682,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
+    if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
     const int k = threadIdx.x & 7;
     const int grp = threadIdx.x >> 3;
@@ -934,6 +940,7 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
 template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false, bool BCF = false>
 __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
+    if (poisoned(a.poison)) return;
     const unsigned lb = a.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
     const long long n = (long long)lb * kBlock + threadIdx.x;
     if (n >= a.nN) return;
@@ -1027,6 +1034,7 @@ hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
 // in-order overwrite leaves behind.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_bc(BCArgs a) {
+    if (poisoned(a.poison)) return;
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.n) return;
     a.out[a.dof[i]] = bc_value(a, i);

@@ -41,6 +41,8 @@ struct ElemArgs {
     const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
     long long fe_mask;      // -1; 0 only in the timing diagnostic "diag_no_assembly" (all force
                             // rows land on one dummy row: no fe traffic, results invalid)
+    const int* poison;      // [0] != 0: a contact buffer overflowed in this call; every state-writing
+                            // kernel is a no-op from then on (the state stays the last good step's)
 };
 
 struct BCArgs {
@@ -56,6 +58,7 @@ struct BCArgs {
     double ct;             // current time t*d_time
     const double* t_rd;    // graph mode: ct = (*t_rd + 1) * dt (read on device), else ct
     double dt;
+    const int* poison;     // see ElemArgs::poison
 };
 
 struct NodalArgs {
@@ -76,6 +79,7 @@ struct NodalArgs {
     double dt;
     const int* bc_of_node; // one GPU: [nN] first entry of `bc` of each node (-1 none); the nodal
     BCArgs bc;             // kernel then applies the BCs itself (no k_bc launch)
+    const int* poison;     // see ElemArgs::poison
 };
 
 

@@ -125,24 +125,45 @@ def test_incremental_surface_lists_match_full_rebuild_and_oracle():
     assert p0["live_nodes_j"] == sum(p["n_nodes_j"] for p in cp)
 
 
-def test_event_cap_overflow_is_reported():
-    """A contact step with more events than the buffer holds fails loudly (no silent truncation);
-    raising the cap through hakai_set_tuning recovers."""
+@pytest.mark.parametrize("graph", [0, 16])
+def test_event_cap_overflow_is_reported(graph):
+    """A contact step with more events than the buffer holds fails loudly (no silent truncation) AT
+    that step: a device-side poison flag makes the nodal, BC and element kernels of that and every
+    later step of the call no-ops, so the state afterwards is the last good step's, bit for bit.
+    Raising the cap through hakai_set_tuning and stepping on from the failed step gives the same
+    run as a sufficient buffer from the start."""
+    import re
     from hakai._abi import HakaiError
     # > 64 events per step once the 9x9-node impactor face is in contact: the smallest buffer (one
     # event in each of the 64 shards) must overflow
     m = mesh.two_body_model(plate=(12, 12, 1), impactor=(8, 8, 1), v=-1e5, perturb=0.03, seed=4, n_steps=60)
     with Solver(m) as sv:
-        sv.set_tuning("contact_event_cap", 1)
-        with pytest.raises(HakaiError):
-            sv.step(1, m.n_steps)
-    o = O.Oracle(m)
-    o.run(1, m.n_steps)
-    with Solver(m) as sv:
+        sv.set_tuning("graph", graph)
         sv.set_tuning("contact_event_cap", 1 << 12)
         sv.step(1, m.n_steps)
-        g = sv.download()
-    assert rel_err(g.disp, o.s["disp"]) < 1e-9
+        full = sv.download()
+    with Solver(m) as sv:
+        sv.set_tuning("graph", graph)
+        sv.set_tuning("contact_event_cap", 1)
+        with pytest.raises(HakaiError) as ei:
+            sv.step(1, m.n_steps)
+        p = int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
+        assert 1 < p < m.n_steps
+        after = sv.download()
+        sv.set_tuning("contact_event_cap", 1 << 12)
+        sv.step(p, m.n_steps - p + 1)
+        cont = sv.download()
+    with Solver(m) as sv:
+        sv.set_tuning("graph", graph)
+        sv.set_tuning("contact_event_cap", 1 << 12)
+        sv.step(1, p - 1)
+        good = sv.download()
+    for k in ("disp", "disp_pre", "velo", "integ_stress", "integ_eq_plastic_strain", "element_flag"):
+        assert np.array_equal(getattr(after, k), getattr(good, k)), k
+        assert np.array_equal(getattr(cont, k), getattr(full, k)), k
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    assert rel_err(full.disp, o.s["disp"]) < 1e-9
 
 
 @pytest.mark.parametrize("surfaces", [False, True])
