@@ -784,10 +784,20 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 }
 
 // One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take
-// the step number from the device counter and the element kernel advances it.
-static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
+// the step number from the device counter and the element kernel advances it. phase: 1 = the
+// contact search (phase A), 2 = the rest (contact phase B, nodal, BCs, element, exchange), 3 = both;
+// an in-process group with the divided multi-GPU contact search runs phase 1 on every rank first
+// (hakai_step_group).
+static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase = 3) {
     hipStream_t s = c->stream;
     EventPair ep;
+    if ((phase & 1) && c->contact) {  // contact force into external_force (:500-560), search part
+        hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
+        const int rc = hkc::contact_step_a(c, t, d_time);
+        hkc::prof_end(c, &ep);
+        if (rc) return rc;
+    }
+    if (!(phase & 2)) return 0;
     const int par = c->cur;  // graph mode: this step reads counter slot 1-par, writes slot par
     // nodal update (:562-567), Q from the previous step's element forces (:668-675)
     hk::NodalArgs na;
@@ -830,11 +840,13 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last) {
         na.bc = ba;
     }
     int rc = 0;
-    if (c->contact) {  // contact force into external_force (:500-560)
-        hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
-        rc = hkc::contact_step(c, t, d_time);
-        hkc::prof_end(c, &ep);
-        if (rc) return rc;
+    if (c->contact) {  // divided multi-GPU search: event exchange and force sums
+        if (hkc::contact_divided(c)) {
+            hkc::prof_begin(c, HAKAI_K_CONTACT_SUM, &ep);
+            rc = hkc::contact_step_b(c);
+            hkc::prof_end(c, &ep);
+            if (rc) return rc;
+        }
         na.fext = c->d_fext;
     }
     rc = hkc::comm_pre_nodal(c);
@@ -930,6 +942,31 @@ static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
     return 0;
 }
 
+// End of a stepping call: the contact overflow check. An overflow poisoned step p: the device's
+// state-writing kernels of steps p.. were no-ops, so the device holds the state after step p-1;
+// bring the host's view back to that step.
+static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, long long done0) {
+    const int rc = hkc::contact_check(c);
+    if (rc && c->contact) {
+        int pz[2] = {0, 0};
+        HIPCHK(hipMemcpy(pz, c->d_poison, sizeof pz, hipMemcpyDeviceToHost));
+        if (pz[0]) {
+            const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
+            if (good >= 0 && good <= n_steps) {
+                c->cur = (good & 1) ? 1 - cur0 : cur0;
+                c->steps_done = done0 + good;
+            }
+            hkc::graph_invalidate(c);
+            hkc::contact_after_overflow(c, c->steps_done);
+            HIPCHK(hipMemset(c->d_poison, 0, 2 * sizeof(int)));
+            const std::string msg = hakai_last_error();
+            return fail(rc, "%s; step %d was not applied: the state is that after step %d", msg.c_str(), pz[1],
+                        pz[1] - 1);
+        }
+    }
+    return rc;
+}
+
 int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step before upload_model/reset_state");
@@ -960,27 +997,49 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         }
         if (rc) return rc;
     }
-    const int rc = hkc::contact_check(c);
-    if (rc && c->contact) {
-        // An overflow poisoned step p: the device state-writing kernels of steps p.. were no-ops, so
-        // the device holds the state after step p-1. Bring the host's view back to that step.
-        int pz[2] = {0, 0};
-        HIPCHK(hipMemcpy(pz, c->d_poison, sizeof pz, hipMemcpyDeviceToHost));
-        if (pz[0]) {
-            const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
-            if (good >= 0 && good <= n_steps) {
-                c->cur = (good & 1) ? 1 - cur0 : cur0;
-                c->steps_done = done0 + good;
-            }
-            hkc::graph_invalidate(c);
-            hkc::contact_after_overflow(c, c->steps_done);
-            HIPCHK(hipMemset(c->d_poison, 0, 2 * sizeof(int)));
-            const std::string msg = hakai_last_error();
-            return fail(rc, "%s; step %d was not applied: the state is that after step %d", msg.c_str(), pz[1],
-                        pz[1] - 1);
+    return finish_call(c, t_first, n_steps, cur0, done0);
+}
+
+int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
+    if (!ctxs || n <= 0) return fail(HAKAI_ERR_ARG, "step_group: no contexts");
+    if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step_group: n_steps=%lld d_time=%g",
+                                                  (long long)n_steps, d_time);
+    std::vector<int> cur0(n);
+    std::vector<long long> done0(n);
+    for (int r = 0; r < n; ++r) {
+        hakai_ctx* c = ctxs[r];
+        if (!c) return fail(HAKAI_ERR_ARG, "step_group: null context %d", r);
+        if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step_group: rank %d has no model/state", r);
+        if (c->poison_halt)
+            return fail(HAKAI_ERR_STATE, "step_group: rank %d: a contact buffer overflowed; upload or reset the "
+                        "state on every rank", r);
+        if (n > 1 && (!c->comm || hkc::comm_rank(c) != r || hkc::comm_size(c) != n ||
+                      hkc::comm_peer_ctx(c, r) != c))
+            return fail(HAKAI_ERR_ARG, "step_group: context %d is not rank %d of an in-process group of %d", r, r, n);
+        cur0[r] = c->cur;
+        done0[r] = c->steps_done;
+        hkc::graph_invalidate(c);
+    }
+    HIPCHK(hipSetDevice(ctxs[0]->device));
+    for (int64_t it = 0; it < n_steps; ++it) {
+        const double t = t_first + (double)it;
+        const bool last = it == n_steps - 1;
+        for (int r = 0; r < n; ++r) {  // every rank's contact search before any rank's exchange
+            if (int rc = step_once(ctxs[r], t, d_time, last, 1)) return rc;
+            if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
+        }
+        for (int r = 0; r < n; ++r) {
+            if (int rc = step_once(ctxs[r], t, d_time, last, 2)) return rc;
+            ctxs[r]->tdev_next = -1;
+            if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
         }
     }
-    return rc;
+    int first = 0;
+    for (int r = 0; r < n; ++r) {
+        const int rc = finish_call(ctxs[r], t_first, n_steps, cur0[r], done0[r]);
+        if (rc && !first) first = rc;
+    }
+    return first;
 }
 
 int hakai_graph_steps(hakai_ctx* c, int64_t* n) {
@@ -1074,6 +1133,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "diag_no_assembly must be 0 or 1");
         if (value && c->model_ok) HIPCHK(hipMemset(c->d_qbuf, 0, 3 * (size_t)c->nN * sizeof(double)));
         c->diag_no_assembly = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "group_serial")) {  // timing: hakai_step_group drains each rank's phase
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "group_serial must be 0 or 1");
+        c->group_serial = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_map")) {

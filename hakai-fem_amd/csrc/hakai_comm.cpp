@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -218,9 +220,40 @@ int comm_common_init(hakai_ctx* c, hkc::Comm* m) {
     return 0;
 }
 
+// In-process group all-gather: dst + off[q] <- src[q] (bytes[q]) for every rank q in ONE launch
+// (the peers' buffers live on the same device; one kernel instead of a copy per rank). 8-byte
+// words, then the tail bytes.
+__global__ void k_gather_local(hkc::LocalGather g, char* dst) {
+    const int q = (int)blockIdx.y;
+    const char* src = g.src[q];
+    char* out = dst + g.off[q];
+    const long long nb = g.bytes[q];
+    if (!src || nb <= 0) return;
+    const long long nw = nb >> 3;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    for (long long i = i0; i < nw; i += stride)
+        reinterpret_cast<unsigned long long*>(out)[i] = reinterpret_cast<const unsigned long long*>(src)[i];
+    for (long long i = (nw << 3) + i0; i < nb; i += stride) out[i] = src[i];
+}
+
 }  // namespace
 
 namespace hkc {
+
+int gather_local(hakai_ctx* c, const LocalGather& g, int n, void* dst) {
+    long long mx = 0;
+    for (int q = 0; q < n; ++q) {
+        if (((uintptr_t)g.src[q] | (uintptr_t)g.off[q]) & 7)
+            return fail(HAKAI_ERR_ARG, "gather_local: rank %d block not 8-byte aligned", q);
+        mx = std::max(mx, g.bytes[q]);
+    }
+    if (mx <= 0) return 0;
+    const unsigned gx = (unsigned)std::min<long long>(std::max<long long>(((mx >> 3) + 255) / 256, 1), 512);
+    hipLaunchKernelGGL(k_gather_local, dim3(gx, (unsigned)n), dim3(256), 0, c->stream, g, (char*)dst);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
 
 void comm_destroy(hakai_ctx* c) {
     Comm* m = c->comm;
@@ -287,14 +320,40 @@ int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes) {
     }
     // in-process group: pull every rank's block (the peers packed it at the end of their previous
     // step, or at their state reset / set_contact_global; see hakai_contact.hip, "mirror")
+    if (m->nranks > kMaxLocalGather) return fail(HAKAI_ERR_COMM, "local group: more than %d ranks", kMaxLocalGather);
+    LocalGather g{};
     for (int q = 0; q < m->nranks; ++q) {
         Comm* p = q == m->rank ? m : peer(m, q);
         if (!p || !p->ag_send[par]) return fail(HAKAI_ERR_COMM, "local group: rank %d has no contact mirror", q);
         HIPCHK(hipStreamWaitEvent(c->stream, p->ev_ag[par], 0));
-        HIPCHK(hipMemcpyAsync((char*)recv + (size_t)q * bytes, p->ag_send[par], bytes, hipMemcpyDeviceToDevice,
-                              c->stream));
+        g.src[q] = (const char*)p->ag_send[par];
+        g.bytes[q] = (long long)bytes;
+        g.off[q] = (long long)q * (long long)bytes;
     }
+    return gather_local(c, g, m->nranks, recv);
+}
+
+// RCCL only: recv[q*bytes .. (q+1)*bytes) = rank q's `send`, ordered on c->stream (the divided
+// contact search's per-step event exchange, hakai_contact.hip)
+int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes) {
+    Comm* m = c->comm;
+    if (!m || m->mode != 0) return fail(HAKAI_ERR_STATE, "all-gather: not an RCCL communicator");
+    if (bytes == 0) return 0;
+    HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
+    HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
+    NCCLCHK(ncclAllGather(send, recv, bytes, ncclUint8, m->nc, m->cs));
+    HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
+    HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
     return 0;
+}
+
+bool comm_is_rccl(const hakai_ctx* c) { return c->comm && c->comm->mode == 0; }
+
+// in-process group: the context of rank q (null otherwise)
+hakai_ctx* comm_peer_ctx(hakai_ctx* c, int q) {
+    Comm* m = c->comm;
+    if (!m || m->mode != 1 || !m->group || q < 0 || q >= m->nranks) return nullptr;
+    return m->group->ctx[q];
 }
 
 int comm_reset(hakai_ctx* c) {

@@ -114,6 +114,23 @@ struct Mirror {
     int* d_x1ctl = nullptr;           // [4] new marks since the last slot scan, max chunks needed, -, -
     int* d_last_del = nullptr;        // [neo] deletion step of own contact elements at the last pack
     size_t off_x1 = 0, off_x1v0 = 0;  // X1 region (u, u_pre per slot entry); at s = 0 also velo0
+    // Divided search (tuning "contact_divide", default on): rank r searches the candidate
+    // triangles j with j % nranks == r; the events of all ranks are all-gathered each step and
+    // every rank runs the same order-independent double-double sums, so the forces are unchanged.
+    int divide = 1;
+    bool div_step = false;            // the current step runs divided (set by phase A)
+    void* d_ev_send[2] = {nullptr, nullptr};  // [ev_cap] EvRec, this rank's events of step t in [t&1]
+                                      // (in-process peers copy them while this rank moves on)
+    long long ev_cap = 0;
+    int* d_evcnt = nullptr;           // [2] this rank's (event count, overflow) of the step
+    int* d_evcnt_all = nullptr;       // [2 nranks] every rank's
+    int* h_evcnt = nullptr;           // pinned [2 nranks]: every rank's, read by the host; [2 nranks..] own
+    hipEvent_t ev_evpacked = nullptr; // this rank's events packed (in-process peers wait on it)
+    char* d_ev_recv = nullptr;        // [nranks][max events of the step] EvRec
+    size_t ev_recv_bytes = 0;
+    long long ev_stride = 0;          // records per rank in d_ev_recv this step
+    int div_t = 0;                    // step number of the last phase A
+    long long div_seq = 0;            // divided phase A calls (equal on the ranks of a lockstep group)
 };
 
 struct Contact {
@@ -645,6 +662,23 @@ __device__ __forceinline__ unsigned wave_append(unsigned int* ctr, bool pred) {
     return base + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
 }
 
+// Same with one global atomic per BLOCK (the per-wave atomics of a large grid on one counter
+// serialise): every thread of the block must call it (block-uniform trip counts).
+__device__ __forceinline__ unsigned block_append(unsigned int* ctr, bool pred, unsigned* s_ctl) {
+    if (threadIdx.x == 0) s_ctl[0] = 0;
+    __syncthreads();
+    const unsigned long long m = __ballot(pred);
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = m ? __ffsll((long long)m) - 1 : 0;
+    unsigned off = 0;
+    if (m && lane == leader) off = atomicAdd(&s_ctl[0], (unsigned)__popcll(m));
+    off = __shfl(off, leader);
+    __syncthreads();
+    if (threadIdx.x == 0) s_ctl[1] = s_ctl[0] ? atomicAdd(ctr, s_ctl[0]) : 0u;
+    __syncthreads();
+    return s_ctl[1] + off + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
+}
+
 // Per-candidate triangle record, written by the prefilter: everything of the loop body at
 // :2371-2698 that does not depend on the contact point (same expressions as the reference, so the
 // same bits), so the per-cell threads start from one load instead of a chain of dependent ones.
@@ -709,12 +743,15 @@ __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const R
 
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
 // side of the range box along any axis -> candidate record
+// (multi-GPU divided search: only the triangles j with j % own_n == own_r)
 __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
                                                       const int* tri_pair, const int* tri_nodes, const int* tri_ele,
                                                       const PairParam* par, const unsigned long long* bbox,
-                                                      unsigned int* ctl, TriRec* cand, long long cand_cap) {
+                                                      unsigned int* ctl, TriRec* cand, long long cand_cap,
+                                                      int own_r, int own_n) {
     const int n = *tri_cnt;
-    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {  // wave-uniform trip count
+    __shared__ unsigned s_app[2];
+    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {  // block-uniform trip count
         const int q = q0 + (int)threadIdx.x;
         bool keep = false;
         int j = 0, pr = 0;
@@ -722,7 +759,7 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
         Range r;
         if (q < n) {
             j = tri_live[q];
-            keep = s.flag[tri_ele[j]] == 1;
+            keep = s.flag[tri_ele[j]] == 1 && (own_n <= 1 || j % own_n == own_r);
             if (keep) {
                 pr = tri_pair[j];
                 r = pair_range(bbox + 12 * pr);
@@ -738,7 +775,7 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
                 }
             }
         }
-        const unsigned slot = wave_append(&ctl[kNcand], keep);
+        const unsigned slot = block_append(&ctl[kNcand], keep, s_app);
         if (keep && (long long)slot < cand_cap) {
             TriRec T;
             tri_geom(s, j, pr, r, par[pr], tri_nodes, tri_ele, p0, p1, p2, T);
@@ -916,21 +953,31 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
     }
 }
 
-// Shard prefix of the event counts (clamped to the shard capacity) in LDS; thread 0 of block 0
-// also publishes the totals for the overflow check and the stats.
+// Shard prefix of the event counts (clamped to the shard capacity) in LDS, one lane per shard of
+// wave 0 (kEvShards == 64: one load and a wave scan, not 64 dependent loads on one thread);
+// s_pre[kEvShards + 1] = some shard overflowed. Block 0 also publishes the totals for the overflow
+// check and the stats.
+static_assert(kEvShards == 64, "shard_prefix: one wave lane per shard");
 __device__ __forceinline__ long long shard_prefix(unsigned int* ctl, const unsigned int* evs, long long shard_cap,
                                                   unsigned* s_pre) {
-    if (threadIdx.x == 0) {
-        unsigned run = 0, raw = 0, mx = 0;
-        for (int q = 0; q < kEvShards; ++q) {
-            const unsigned v = evs[q * kShardStride];
-            s_pre[q] = run;
-            run += (long long)v < shard_cap ? v : (unsigned)shard_cap;
-            raw += v;
-            mx = v > mx ? v : mx;
+    if (threadIdx.x < 64) {
+        const int q = (int)threadIdx.x;
+        const unsigned v = evs[q * kShardStride];
+        const unsigned cl = (long long)v < shard_cap ? v : (unsigned)shard_cap;
+        unsigned x = cl, raw = v, mx = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o);
+            if (q >= o) x += y;
+            raw += __shfl_xor(raw, o);
+            mx = max(mx, __shfl_xor(mx, o));
         }
-        s_pre[kEvShards] = run;
-        if (blockIdx.x == 0) {
+        s_pre[q] = x - cl;
+        const bool over = __any((long long)v > shard_cap);
+        if (q == 63) {
+            s_pre[kEvShards] = x;
+            s_pre[kEvShards + 1] = over ? 1u : 0u;
+        }
+        if (blockIdx.x == 0 && q == 0) {
             ctl[kEv] = raw;
             atomicMax(&ctl[kEvMax], raw);
             atomicMax(&ctl[kEvShardMax], mx);
@@ -960,16 +1007,16 @@ __device__ __forceinline__ long long ev_slot(const unsigned* s_pre, long long sh
 __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
                            int* cnt, int* touched, int* tpos, int tsel, int* poison, long long cand_cap,
                            const int* x1ctl, int t, const double* t_rd) {
-    __shared__ unsigned s_pre[kEvShards + 1];
+    __shared__ unsigned s_pre[kEvShards + 2];
     const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0);
-        for (int q = 0; q < kEvShards; ++q) over |= (long long)evs[q * kShardStride] > shard_cap;
+        const bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
         if (over && poison[0] == 0) {
             poison[1] = t_rd ? (int)*t_rd + 1 : t;
             poison[0] = 1;
         }
     }
+    __shared__ unsigned s_app[2];
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
@@ -978,7 +1025,7 @@ __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long
             node = ev_nodes[4 * ev_slot(s_pre, shard_cap, e >> 2) + (e & 3)];
             first = atomicAdd(&cnt[node], 1) == 0;
         }
-        const unsigned q = wave_append(&ctl[kTouched + tsel], first);
+        const unsigned q = block_append(&ctl[kTouched + tsel], first, s_app);
         if (first) {
             touched[q] = node;
             tpos[node] = (int)q;
@@ -1010,7 +1057,7 @@ __global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, cons
 __global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
                              const double* ev_f, const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
-    __shared__ unsigned s_pre[kEvShards + 1];
+    __shared__ unsigned s_pre[kEvShards + 2];
     const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
@@ -1051,6 +1098,115 @@ __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, 
                 e += err;
             }
             fext[3 * n + c] = s + e;
+        }
+    }
+}
+
+// ---- divided multi-GPU search: event exchange ------------------------------------------------
+struct EvRec {
+    int n[4];     // i, j0, j1, j2
+    double f[3];  // force on i (the triangle nodes get -f/3 each)
+};
+
+// this rank's events of the step, shard order -> one compact record list; (count, overflow) for the
+// all-gather. Overflow = events beyond a shard, candidates beyond their buffer, or a truncated mirror
+// block: exchanged with the counts so every rank poisons the same step.
+__global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
+                          const double* ev_f, EvRec* out, int* cnt_out, long long cand_cap, const int* x1ctl) {
+    __shared__ unsigned s_pre[kEvShards + 2];
+    const long long n = shard_prefix(ctl, evs, shard_cap, s_pre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
+        cnt_out[0] = (int)n;
+        cnt_out[1] = over ? 1 : 0;
+    }
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const long long sl = ev_slot(s_pre, shard_cap, e);
+        EvRec r;
+        for (int k = 0; k < 4; ++k) r.n[k] = ev_nodes[4 * sl + k];
+        for (int k = 0; k < 3; ++k) r.f[k] = ev_f[3 * sl + k];
+        out[e] = r;
+    }
+}
+
+constexpr int kMaxDivRanks = 64;  // divided search: ranks whose event offsets a block holds in LDS
+
+// an overflow on some rank (divided search): poison step t unless an earlier step already is
+__global__ void k_poison_mark(int* poison, int t) {
+    if (threadIdx.x == 0 && poison[0] == 0) {
+        poison[1] = t;
+        poison[0] = 1;
+    }
+}
+
+// rank prefix of the gathered counts (cnt[2q] = rank q's events) in LDS; block 0 publishes the total
+__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const int* cnt, int nr, long long* s_off) {
+    if (threadIdx.x == 0) {
+        long long run = 0;
+        for (int q = 0; q < nr; ++q) {
+            s_off[q] = run;
+            run += cnt[2 * q];
+        }
+        s_off[nr] = run;
+        if (blockIdx.x == 0) {
+            ctl[kEv] = (unsigned)run;
+            atomicMax(&ctl[kEvMax], (unsigned)run);
+        }
+    }
+    __syncthreads();
+    return s_off[nr];
+}
+
+__device__ __forceinline__ const EvRec* rank_ev(const EvRec* ev, long long stride, const long long* s_off, int nr,
+                                                long long E) {
+    int q = 0;
+    while (q + 1 < nr && s_off[q + 1] <= E) ++q;
+    return ev + q * stride + (E - s_off[q]);
+}
+
+// k_ct_count / k_ct_scatter over the gathered events of all ranks (same node terms, same sums)
+__global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long stride, const int* cnt_all, int nr,
+                             int* cnt, int* touched, int* tpos, int tsel) {
+    __shared__ long long s_off[kMaxDivRanks + 1];
+    __shared__ unsigned s_app[2];
+    const long long n = 4 * rank_prefix(ctl, cnt_all, nr, s_off);
+    for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
+        const long long e = e0 + threadIdx.x;
+        int node = -1;
+        bool first = false;
+        if (e < n) {
+            node = rank_ev(ev, stride, s_off, nr, e >> 2)->n[e & 3];
+            first = atomicAdd(&cnt[node], 1) == 0;
+        }
+        const unsigned q = block_append(&ctl[kTouched + tsel], first, s_app);
+        if (first) {
+            touched[q] = node;
+            tpos[node] = (int)q;
+        }
+    }
+}
+
+__global__ void k_ct_scatter_g(const EvRec* ev, long long stride, const int* cnt_all, int nr, unsigned int* ctl,
+                               const int* toff, const int* tpos, int* cnt, double* terms) {
+#pragma clang fp contract(off)
+    __shared__ long long s_off[kMaxDivRanks + 1];
+    const long long n = 4 * rank_prefix(ctl, cnt_all, nr, s_off);
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const EvRec* r = rank_ev(ev, stride, s_off, nr, e >> 2);
+        const int role = (int)(e & 3);
+        const int node = r->n[role];
+        const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
+        double* o = terms + 3 * (long long)slot;
+        if (role == 0) {  // c_force3[i] += f
+            o[0] = r->f[0];
+            o[1] = r->f[1];
+            o[2] = r->f[2];
+        } else {  // triangle nodes: += -f / 3.0
+            o[0] = -r->f[0] / 3.0;
+            o[1] = -r->f[1] / 3.0;
+            o[2] = -r->f[2] / 3.0;
         }
     }
 }
@@ -1182,22 +1338,25 @@ __global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* se
     if (x1ctl[0] == 0) return;
     int need = 0;
     __shared__ int s_w[1024 / 64];
-    for (int q = q0; q < q1; ++q) {
+    for (int q = q0; q < q1; ++q) {  // each thread a contiguous run of the segment: one block scan
         const int c0 = seg_chunk[q], c1 = seg_chunk[q + 1];
-        int carry = 0;
-        for (int b = c0; b < c1; b += (int)blockDim.x) {
-            const int c = b + (int)threadIdx.x;
-            const int f = c < c1 ? chunk_flag[c] : 0;
-            int tot;
-            const int slot = carry + block_excl_scan(f, s_w, tot);
-            if (f && slot < capc) slot_chunk[(long long)q * capc + slot] = c;
-            carry += tot;
-        }
+        const int run = (c1 - c0 + (int)blockDim.x - 1) / (int)blockDim.x;
+        const int b0 = min(c0 + (int)threadIdx.x * run, c1), b1 = min(b0 + run, c1);
+        int f = 0;
+        for (int c = b0; c < b1; ++c) f += chunk_flag[c] != 0;
+        int tot;
+        int slot = block_excl_scan(f, s_w, tot);
+        for (int c = b0; c < b1 && f > 0; ++c)
+            if (chunk_flag[c] != 0) {
+                if (slot < capc) slot_chunk[(long long)q * capc + slot] = c;
+                ++slot;
+                --f;
+            }
         if (threadIdx.x == 0) {
-            counts[q] = carry;
-            if (carry > capc) x1ctl[1] |= 1;
+            counts[q] = tot;
+            if (tot > capc) x1ctl[1] |= 1;
         }
-        need = max(need, carry);
+        need = max(need, tot);
     }
     __syncthreads();
     // only the unpack's scan over all ranks clears the flag and records the need (the same on every
@@ -1455,6 +1614,11 @@ void contact_destroy(hakai_ctx* c) {
         dfree(M->d_seg_chunk); dfree(M->d_chunk_first); dfree(M->d_chunk_end); dfree(M->d_x1_gid); dfree(M->d_x1_loc);
         dfree(M->d_x1_chunk); dfree(M->d_el2x_ptr); dfree(M->d_el2x); dfree(M->d_chunk_flag); dfree(M->d_slot_chunk);
         dfree(M->d_counts); dfree(M->d_x1ctl); dfree(M->d_last_del);
+        for (void* p : M->d_ev_send)
+            if (p) (void)hipFree(p);
+        dfree(M->d_evcnt); dfree(M->d_evcnt_all); dfree(M->d_ev_recv);
+        if (M->h_evcnt) (void)hipHostFree(M->h_evcnt);
+        if (M->ev_evpacked) (void)hipEventDestroy(M->ev_evpacked);
         if (M->h_need) (void)hipHostFree(M->h_need);
         for (auto& e : M->ev_need)
             if (e) (void)hipEventDestroy(e);
@@ -1595,8 +1759,10 @@ int contact_post_step(hakai_ctx* c) {
     return mir_pack(c, false);
 }
 
-// contact force of step t into c->d_fext (before the nodal update, :500-560)
-int contact_step(hakai_ctx* c, double t, double d_time) {
+// contact force of step t into c->d_fext (before the nodal update, :500-560). Phase A; with
+// divide_ok on a multi-GPU mirror it stops after packing this rank's share of the events, and
+// contact_step_b finishes the step.
+static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     Contact* C = c->contact;
     Mirror* M = C->mir;
     hipStream_t s = c->stream;
@@ -1705,16 +1871,30 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
     if (C->nseg > 0)
         hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
                            C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
+    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
+    if (M) M->div_step = div;
     if (C->n_tri > 0) {
         hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, 2048))),
                            dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
                            C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ctl, (TriRec*)C->d_cand,
-                           C->cand_cap);
+                           C->cand_cap, div ? M->rank : 0, div ? M->nranks : 1);
         hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, (const TriRec*)C->d_cand, C->cand_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
     }
     const unsigned ge = (unsigned)C->g_ev;
+    if (div) {  // pack this rank's events; the exchange and the sums are phase B
+        hipLaunchKernelGGL(k_ev_pack, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
+                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt, C->cand_cap, M->d_x1ctl);
+        HIPCHK(hipGetLastError());
+        if (!comm_is_rccl(c))  // in-process peers read the count from pinned memory
+            HIPCHK(hipMemcpyAsync(M->h_evcnt + 2 * M->nranks, M->d_evcnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(M->ev_evpacked, s));
+        M->div_t = in.t;
+        ++M->div_seq;
+        C->use_velo0 = false;
+        return 0;
+    }
     hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, C->cand_cap,
                        M ? M->d_x1ctl : nullptr, in.t, c->g_trd);
@@ -1729,6 +1909,87 @@ int contact_step(hakai_ctx* c, double t, double d_time) {
                            M->g_fext, c->d_fext);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
+    return 0;
+}
+
+int contact_step(hakai_ctx* c, double t, double d_time) { return step_a(c, t, d_time, false); }
+int contact_step_a(hakai_ctx* c, double t, double d_time) { return step_a(c, t, d_time, true); }
+bool contact_divided(const hakai_ctx* c) { return c->contact && c->contact->mir && c->contact->mir->div_step; }
+
+// Phase B of a divided step: every rank's (count, overflow), then its events, all-gathered (RCCL, or
+// device copies from the in-process peers, which all finished phase A); an overflow anywhere
+// poisons the step on every rank; then the same count / scatter / double-double sums as one GPU.
+int contact_step_b(hakai_ctx* c) {
+    Contact* C = c->contact;
+    Mirror* M = C ? C->mir : nullptr;
+    if (!M || !M->div_step) return 0;
+    hipStream_t s = c->stream;
+    const int nr = M->nranks;
+    int* h = M->h_evcnt;
+    if (comm_is_rccl(c)) {
+        if (int rc = comm_allgather_raw(c, M->d_evcnt, M->d_evcnt_all, 2 * sizeof(int))) return rc;
+        HIPCHK(hipMemcpyAsync(h, M->d_evcnt_all, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        for (int q = 0; q < nr; ++q) {
+            hakai_ctx* pc = comm_peer_ctx(c, q);
+            Mirror* pm = pc && pc->contact ? pc->contact->mir : nullptr;
+            if (!pm || pm->div_seq != M->div_seq || pm->div_t != M->div_t)
+                return fail(HAKAI_ERR_STATE, "divided contact: rank %d has not searched step %d (step an in-process "
+                            "group with hakai_step_group)", q, M->div_t);
+            HIPCHK(hipEventSynchronize(pm->ev_evpacked));
+            h[2 * q] = pm->h_evcnt[2 * nr];
+            h[2 * q + 1] = pm->h_evcnt[2 * nr + 1];
+        }
+        HIPCHK(hipMemcpyAsync(M->d_evcnt_all, h, 2 * nr * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));  // h is rewritten by the next step's phase B
+    }
+    long long mx = 0;
+    bool over = false;
+    for (int q = 0; q < nr; ++q) {
+        mx = std::max<long long>(mx, h[2 * q]);
+        over |= h[2 * q + 1] != 0;
+    }
+    if (over)  // the same step on every rank (the counts are the same everywhere)
+        hipLaunchKernelGGL(k_poison_mark, dim3(1), dim3(64), 0, s, c->d_poison, M->div_t);
+    const size_t need = (size_t)nr * (size_t)std::max<long long>(mx, 1) * sizeof(EvRec);
+    if (need > M->ev_recv_bytes) {
+        HIPCHK(hipStreamSynchronize(s));
+        dfree(M->d_ev_recv);
+        HIPCHK(dalloc(&M->d_ev_recv, need));
+        M->ev_recv_bytes = need;
+    }
+    M->ev_stride = std::max<long long>(mx, 1);
+    if (comm_is_rccl(c)) {
+        if (mx > 0)
+            if (int rc = comm_allgather_raw(c, M->d_ev_send[M->div_t & 1], M->d_ev_recv, (size_t)mx * sizeof(EvRec)))
+                return rc;
+    } else {
+        LocalGather g{};
+        for (int q = 0; q < nr; ++q) {
+            Mirror* pm = comm_peer_ctx(c, q)->contact->mir;
+            if (q != M->rank) HIPCHK(hipStreamWaitEvent(s, pm->ev_evpacked, 0));
+            g.src[q] = (const char*)pm->d_ev_send[M->div_t & 1];
+            g.bytes[q] = (long long)h[2 * q] * (long long)sizeof(EvRec);
+            g.off[q] = (long long)q * M->ev_stride * (long long)sizeof(EvRec);
+        }
+        if (int rc = gather_local(c, g, nr, M->d_ev_recv)) return rc;
+    }
+    const int tsel = C->tsel;
+    const unsigned ge = (unsigned)C->g_ev;
+    const EvRec* ev = (const EvRec*)M->d_ev_recv;
+    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, ev, M->ev_stride, M->d_evcnt_all, nr, C->d_cnt,
+                       C->d_touched[tsel], C->d_tpos, tsel);
+    hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
+                       C->d_tcnt);
+    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, ev, M->ev_stride, M->d_evcnt_all, nr, C->d_ctl,
+                       C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
+    hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
+                       C->d_terms, M->g_fext);
+    hipLaunchKernelGGL(k_mir_fext_copy, dim3(64), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], M->d_g2l,
+                       M->g_fext, c->d_fext);
+    HIPCHK(hipGetLastError());
+    M->div_step = false;
     return 0;
 }
 
@@ -1798,6 +2059,11 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipStreamSynchronize(c->stream));
         return 0;
     }
+    if (!std::strcmp(key, "contact_divide")) {  // multi-GPU: divided search (1, default) or replicated (0)
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_divide must be 0 or 1");
+        if (C && C->mir) C->mir->divide = (int)value;
+        return 0;
+    }
     if (!std::strcmp(key, "contact_full_rebuild")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_full_rebuild must be 0 or 1");
         C->always_rebuild = value != 0;
@@ -1815,6 +2081,13 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         dfree(C->d_tcnt);
         C->cap = (value + kEvShards - 1) / kEvShards * kEvShards;
         C->tcap = std::min<long long>(C->nN, 4 * C->cap);
+        if (Mirror* M = C->mir) {  // divided search: this rank's events of a step
+            for (auto& p : M->d_ev_send) {
+                if (p) (void)hipFree(p);
+                HIPCHK(hipMalloc(&p, (size_t)C->cap * sizeof(EvRec)));
+            }
+            M->ev_cap = C->cap;
+        }
         HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
@@ -1861,6 +2134,11 @@ int contact_check(hakai_ctx* c) {
     if ((long long)ms > C->cap / kEvShards)
         return fail(HAKAI_ERR_STATE, "contact: %u events in one step (%u in one of %d shards) exceed the buffer "
                     "(%lld); raise hakai_set_tuning(\"contact_event_cap\")", mx, ms, kEvShards, C->cap);
+    int pz = 0;
+    HIPCHK(hipMemcpy(&pz, c->d_poison, sizeof(int), hipMemcpyDeviceToHost));
+    if (pz)  // divided multi-GPU search: another rank's buffers overflowed
+        return fail(HAKAI_ERR_STATE, "contact: a contact buffer of another rank overflowed; raise "
+                    "hakai_set_tuning(\"contact_event_cap\" / \"contact_candidate_cap\") on every rank");
     return 0;
 }
 
@@ -2413,6 +2691,13 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
                               hipMemcpyHostToDevice, s));
     else
         HIPCHK(hipMemsetAsync(M->d_velo0_loc, 0, 3 * (size_t)c->nN * sizeof(double), s));
+    // divided search: this rank's events of a step (up to the event buffer), the counts
+    M->ev_cap = C->cap;
+    for (auto& p : M->d_ev_send) HIPCHK(hipMalloc(&p, (size_t)M->ev_cap * sizeof(EvRec)));
+    HIPCHK(dalloc(&M->d_evcnt, 2));
+    HIPCHK(dalloc(&M->d_evcnt_all, 2 * (size_t)nr));
+    HIPCHK(hipHostMalloc((void**)&M->h_evcnt, (2 * (size_t)nr + 2) * sizeof(int), hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&M->ev_evpacked, hipEventDisableTiming));
     for (int p = 0; p < 2; ++p)
         if (int rc = hkc::mir_buffers(c, p)) return rc;
     if (int rc = hkc::mir_reset(c)) return rc;

@@ -70,6 +70,9 @@ struct hakai_ctx {
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
     int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
     int elem_exact = 0;          // tuning "elem_exact": reference-order element arithmetic
+    int group_serial = 0;        // tuning "group_serial" (rank 0 of a hakai_step_group): drain every rank's
+                                 // phase before the next rank's (per-rank timings without the ranks
+                                 // sharing the one GPU)
     int diag_no_assembly = 0;    // tuning "diag_no_assembly": TIMING DIAGNOSTIC, results invalid --
                                  // no element-force traffic (rows to one dummy row, Q read from a
                                  // zero buffer): the step's cost without any force assembly
@@ -151,10 +154,28 @@ int comm_size(const hakai_ctx* c);
 int comm_gather_register(hakai_ctx* c, void* send0, void* send1);
 int comm_gather_mark(hakai_ctx* c, int par);                             // send[par] packed (c->stream)
 int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes);     // ordered on c->stream
+// in-process group: dst + off[q] <- src[q] (bytes[q], 8-byte aligned), all ranks in one launch on
+// c->stream (the caller orders it after the peers' producers)
+constexpr int kMaxLocalGather = 64;
+struct LocalGather {
+    const char* src[kMaxLocalGather];
+    long long bytes[kMaxLocalGather];
+    long long off[kMaxLocalGather];
+};
+int gather_local(hakai_ctx* c, const LocalGather& g, int n, void* dst);
+int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes);  // RCCL only
+bool comm_is_rccl(const hakai_ctx* c);
+hakai_ctx* comm_peer_ctx(hakai_ctx* c, int q);                          // in-process group member q
 // Contact (no-ops without hakai_set_contact).
 void contact_destroy(hakai_ctx* c);
 int contact_state_reset(hakai_ctx* c, const double* velo0_host);
 int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
+// the same in two phases (multi-GPU divided search): A = mirror update + search of this rank's
+// share of the triangles + event pack; B = event all-gather + force sums. An in-process group
+// runs A on every rank before B on any (hakai_step_group).
+int contact_step_a(hakai_ctx* c, double t, double d_time);
+int contact_step_b(hakai_ctx* c);
+bool contact_divided(const hakai_ctx* c);                 // this step runs the divided search
 int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack the mirror block of the next step
 int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
 void contact_after_overflow(hakai_ctx* c, long long steps_since_reset);  // host state after a poisoned call

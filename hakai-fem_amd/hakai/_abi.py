@@ -23,8 +23,9 @@ HAKAI_ERR_STATE = -4
 HAKAI_ERR_MODEL = -5
 HAKAI_ERR_COMM = -6
 
-K_ELEMENT, K_NODAL, K_BC, K_EXCHANGE, K_CONTACT = 0, 1, 2, 3, 4
-KERNEL_NAMES = {K_ELEMENT: "element", K_NODAL: "nodal", K_BC: "bc", K_EXCHANGE: "exchange", K_CONTACT: "contact"}
+K_ELEMENT, K_NODAL, K_BC, K_EXCHANGE, K_CONTACT, K_CONTACT_SUM = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = {K_ELEMENT: "element", K_NODAL: "nodal", K_BC: "bc", K_EXCHANGE: "exchange", K_CONTACT: "contact",
+                K_CONTACT_SUM: "contact_sum"}
 
 PD = POINTER(c_double)
 PI64 = POINTER(c_int64)
@@ -90,6 +91,7 @@ def lib() -> ctypes.CDLL:
         "hakai_upload_state": (c_int, [c_void_p, POINTER(StateT)]),
         "hakai_download_state": (c_int, [c_void_p, POINTER(StateT)]),
         "hakai_step": (c_int, [c_void_p, c_double, c_int64, c_double]),
+        "hakai_step_group": (c_int, [POINTER(c_void_p), c_int32, c_double, c_int64, c_double]),
         "hakai_sync": (c_int, [c_void_p]),
         "hakai_deleted": (c_int, [c_void_p, PI64, PI64, c_int64]),
         "hakai_negative_jacobians": (c_int, [c_void_p, PI64]),
@@ -142,7 +144,7 @@ def exported_symbols() -> list[str]:
     return [
         "hakai_abi_version", "hakai_last_error", "hakai_device_count", "hakai_create", "hakai_destroy",
         "hakai_upload_model", "hakai_set_bc", "hakai_reset_state", "hakai_upload_state",
-        "hakai_download_state", "hakai_step", "hakai_sync", "hakai_deleted", "hakai_negative_jacobians",
+        "hakai_download_state", "hakai_step", "hakai_step_group", "hakai_sync", "hakai_deleted", "hakai_negative_jacobians",
         "hakai_node_stress_strain", "hakai_stress_hexa", "hakai_triax_stress", "hakai_lumped_mass",
         "hakai_profile_enable", "hakai_profile_mask", "hakai_profile_read", "hakai_set_tuning", "hakai_set_contact",
         "hakai_set_contact_cp", "hakai_set_contact_global", "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_stats", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",

@@ -27,7 +27,7 @@ import numpy as np
 from . import dist as _dist
 from ._abi import check, lib, ptr
 from .model import read_inp
-from .solver import Solver, State, comm_unique_id
+from .solver import Solver, State, comm_unique_id, step_group
 
 I64 = ctypes.c_int64
 
@@ -148,9 +148,7 @@ def hakai_multi(fname: str, out_dir: str = "temp", local_ranks: int = 0, device:
         while t0 <= n_steps:
             t1 = n_steps if d_out <= 0 else min(n_steps, ((t0 + d_out - 1) // d_out) * d_out)
             if local_ranks:
-                for t in range(t0, t1 + 1):
-                    for sv in svs:
-                        sv.step(t, 1, dt)
+                step_group(svs, t0, t1 - t0 + 1, dt)
             else:
                 svs[0].step(t0, t1 - t0 + 1, dt)
             if verbose:

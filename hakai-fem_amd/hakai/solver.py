@@ -237,11 +237,14 @@ class Solver:
                                          ptr(hi, ctypes.c_int32)))
 
 
-def step_group(solvers: list[Solver], t_first: float, n_steps: int):
-    """Advance an in-process group (hakai_comm_init_local) in lockstep: one step per rank per call."""
-    for i in range(int(n_steps)):
-        for sv in solvers:
-            sv.step(t_first + i, 1)
+def step_group(solvers: list[Solver], t_first: float, n_steps: int, d_time: float | None = None):
+    """Advance an in-process group (hakai_comm_init_local, solvers[r] = rank r) in lockstep
+    (hakai_step_group): per step every rank's contact search, then every rank's exchange and update."""
+    if not solvers:
+        return
+    arr = (ctypes.c_void_p * len(solvers))(*[sv.ctx for sv in solvers])
+    dt = solvers[0].model.dt if d_time is None else d_time
+    check(lib().hakai_step_group(arr, len(solvers), float(t_first), int(n_steps), float(dt)))
 
 
 def comm_unique_id() -> bytes:

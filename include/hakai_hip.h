@@ -153,8 +153,10 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
                       double mass_scaling, double* diag_M, double* elementVolume);
 
 /* ---- profiling: per-kernel device time measured with HIP events on the context's stream ---- */
+/* HAKAI_K_CONTACT: the contact step (multi-GPU divided search: the search part); HAKAI_K_CONTACT_SUM:
+ * the divided search's event all-gather and force sums (multi-GPU contact only). */
 enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_CONTACT = 4,
-       HAKAI_K_COUNT = 5 };
+       HAKAI_K_CONTACT_SUM = 5, HAKAI_K_COUNT = 6 };
 int hakai_profile_enable(hakai_ctx* ctx, int on);  /* all kernels on / off; resets the totals */
 /* Time only the kernels whose bit (1 << HAKAI_K_*) is set (fewer events in a timed loop). */
 int hakai_profile_mask(hakai_ctx* ctx, uint32_t mask);
@@ -179,7 +181,10 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
  *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
- *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy. */
+ *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy;
+ *   "contact_divide"    multi-GPU contact: 1 (default) divided search, 0 replicated search;
+ *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
+ *                       next rank's (uncontended per-rank timings on one GPU; default 0). */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
 
 /* ---- contact: all-exterior instance-vs-instance penalty contact --------- */
@@ -207,6 +212,9 @@ int hakai_set_contact_cp(hakai_ctx* ctx, int32_t contact_flag, const int64_t* el
  * rank with a communicator returns HAKAI_ERR_STATE. With a mirror, hakai_step, hakai_reset_state,
  * hakai_upload_state, hakai_contact_force and hakai_set_tuning("contact_mirror_chunks" /
  * "contact_mirror_deletions") are collective: every rank calls them in the same order. */
+/* (Divided search, tuning "contact_divide", default 1: rank r searches the candidate triangles
+ * j % nranks == r and the ranks' events are all-gathered each step -- the force sums, and so the
+ * results, are unchanged; 0 = every rank searches every triangle.) */
 int hakai_set_contact_global(hakai_ctx* ctx, int32_t contact_flag, int64_t nNode, const double* coordmat,
                              int64_t nElement, const int64_t* elementmat, const int64_t* element_material,
                              const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
@@ -238,6 +246,12 @@ int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128])
  * sum / fix kernels as the RCCL path). The host must step all ranks in lockstep (rank 0..n-1,
  * one hakai_step call of equal length each) on the same device. */
 int hakai_comm_init_local(hakai_ctx* ctx, int rank, int nranks, int64_t group_key);
+/* Steps an in-process group (the n contexts of hakai_comm_init_local, ctxs[r] = rank r) in lockstep,
+ * n_steps steps from t_first: per step every rank's contact search (phase A) runs before any rank's
+ * event exchange, force sums, nodal update and element update (phase B), so the divided multi-GPU
+ * contact search works in one process. hakai_step on such a rank steps it alone (one step per call,
+ * no divided contact). */
+int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time);
 /* Interface description for this rank's local model ("multi-GPU"):
  * shared nodes (local 0-based ids, sorted by global id) with the rank range [lo, hi] of ranks
  * whose elements touch each node (hi == lo+1 for slab partitions). */

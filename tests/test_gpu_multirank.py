@@ -76,9 +76,10 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key):
+def _run_contact_group(glob, world, n_steps, key, divide=1):
     """Range-partitioned contact model on an in-process group, each rank mirroring the global
-    contact model (hakai_set_contact_global)."""
+    contact model (hakai_set_contact_global); divide=1 (default): each rank searches its share of
+    the triangles and the events are all-gathered."""
     gdiag, _ = glob.lumped_mass()
     parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
     svs = []
@@ -88,6 +89,7 @@ def _run_contact_group(glob, world, n_steps, key):
         sv.comm_init_local(r, world, key)
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
+        sv.set_tuning("contact_divide", divide)
         svs.append(sv)
     step_group(svs, 1, n_steps)
     out = [(loc, l2g, sv.download(), [tuple(x) for x in sv.deleted()], sv.contact_stats())
@@ -111,11 +113,13 @@ def _assert_group_equals_single(glob, parts, g, gdel):
         assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_contact_group_bitexact_with_deletion(world):
+@pytest.mark.parametrize("world,divide", [(2, 1), (3, 1), (4, 1), (2, 0), (3, 0)])
+def test_contact_group_bitexact_with_deletion(world, divide):
     """Multi-GPU contact: contact-driven deletion with the surface update, the
     impactor and the plate split over ranks; every rank's displacements, stresses and the
-    deletion log equal the single-context run bit for bit."""
+    deletion log equal the single-context run bit for bit -- with the divided search (each rank
+    tests its share of the candidate triangles, events all-gathered, the same order-independent
+    sums) and with the replicated one."""
     from hakai import mesh
     glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
     with Solver(glob) as sv:
@@ -124,10 +128,16 @@ def test_contact_group_bitexact_with_deletion(world):
         gdel = [tuple(x) for x in sv.deleted()]
         gst = sv.contact_stats()
     assert len(gdel) >= 4
-    parts = _run_contact_group(glob, world, glob.n_steps, key=300 + world)
+    parts = _run_contact_group(glob, world, glob.n_steps, key=300 + 10 * divide + world, divide=divide)
     _assert_group_equals_single(glob, parts, g, gdel)
-    for *_, st in parts:  # every rank ran the whole (replicated) contact search
+    for *_, st in parts:  # every rank keeps the whole live lists and sums every rank's events
         assert st["live_triangles"] == gst["live_triangles"] and st["events"] == gst["events"]
+    cand = [st["candidate_triangles"] for *_, st in parts]
+    gc = gst["candidate_triangles"]
+    if divide:  # the candidate triangles of the last step, split over the ranks
+        assert sum(cand) == gc and (gc < world or max(cand) < gc)
+    else:
+        assert cand == [gc] * world
 
 
 @pytest.mark.parametrize("flag,myu,surfaces", [(1, None, False), (2, 0.0, False), (1, None, True)])

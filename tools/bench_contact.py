@@ -23,6 +23,12 @@ def main():
     ap.add_argument("--ranks", type=int, default=1,
                     help=">1: range-partitioned in-process group on this one GPU (multi-GPU contact mirror; "
                          "measures the per-rank contact cost incl. the all-gather, not scaling)")
+    ap.add_argument("--divide", type=int, default=1,
+                    help="multi-rank contact: 1 = each rank searches its share of the triangles and the events "
+                         "are all-gathered (default), 0 = every rank searches every triangle")
+    ap.add_argument("--serial", type=int, default=1,
+                    help="multi-rank: drain each rank's phase before the next rank's (tuning group_serial), so "
+                         "the per-rank kernel timings are not inflated by the ranks sharing this one GPU")
     a = ap.parse_args()
     if a.ranks > 1:
         return group(a)
@@ -72,7 +78,7 @@ def main():
 def group(a):
     import numpy as np
     from hakai import dist, mesh
-    from hakai._abi import K_BC, K_CONTACT, K_ELEMENT, K_EXCHANGE, K_NODAL
+    from hakai._abi import K_BC, K_CONTACT, K_CONTACT_SUM, K_ELEMENT, K_EXCHANGE, K_NODAL
     from hakai.solver import Solver, step_group
     m = mesh.config_c4(a.scale)
     gdiag, _ = m.lumped_mass()
@@ -85,6 +91,8 @@ def group(a):
         sv.comm_init_local(r, a.ranks, 4242)
         sv.set_interface(*iface)
         sv.set_contact_global(m, l2g, off, gdiag)
+        sv.set_tuning("contact_divide", a.divide)
+        sv.set_tuning("group_serial", a.serial)
         svs.append(sv)
     t1 = time.time()
     step_group(svs, 1, a.preload)
@@ -99,11 +107,14 @@ def group(a):
     ranks = []
     for sv, (loc, *_) in zip(svs, parts):
         k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
-                                                (K_CONTACT, "contact"), (K_EXCHANGE, "exchange"))}
-        ranks.append({"elements": loc.nElement, "nodes": loc.nNode,
-                      "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
+                                                (K_CONTACT, "contact"), (K_CONTACT_SUM, "contact_sum"),
+                                                (K_EXCHANGE, "exchange"))}
+        per = {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]}
+        ranks.append({"elements": loc.nElement, "nodes": loc.nNode, "kernel_ms_per_step": per,
+                      "contact_total_ms_per_step": round(per.get("contact", 0) + per.get("contact_sum", 0), 4),
                       "contact_stats_last_step": sv.contact_stats()})
-    out = {"workload": f"C4 two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group)",
+    out = {"workload": f"C4 two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group), "
+                       f"contact_divide={a.divide}, group_serial={a.serial}",
            "elements": m.nElement, "steps": a.steps, "preload": a.preload,
            "group_ms_per_step_all_ranks": round(el / a.steps * 1e3, 4), "setup_s": round(t1 - t0, 2),
            "ranks": ranks}
