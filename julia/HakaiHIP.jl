@@ -153,6 +153,13 @@ end
 step!(c::Ctx, t_first, n, d_time) =
     check(ccall((:hakai_step, lib), Cint, (Ptr{Cvoid}, Float64, Int64, Float64), c.p, t_first, n, d_time))
 sync(c::Ctx) = check(ccall((:hakai_sync, lib), Cint, (Ptr{Cvoid},), c.p))
+# an in-process group (rank r = cs[r+1]) in lockstep: every rank's contact search, then every
+# rank's exchange and update, per step (the divided multi-GPU contact search in one process)
+function step_group!(cs::Vector{Ctx}, t_first, n, d_time)
+    ps = Ptr{Cvoid}[c.p for c in cs]
+    check(ccall((:hakai_step_group, lib), Cint, (Ptr{Ptr{Cvoid}}, Int32, Float64, Int64, Float64), ps,
+                length(cs), t_first, n, d_time))
+end
 function graph_steps(c::Ctx)
     n = Ref{Int64}(0)
     check(ccall((:hakai_graph_steps, lib), Cint, (Ptr{Cvoid}, Ref{Int64}), c.p, n))

@@ -157,6 +157,12 @@ class Oracle:
                                      _p(self.s["element_flag"], c_int64), _p(f))
         return f, n
 
+    def apply_deletions(self, elements):
+        """Surface update for elements deleted before this oracle took over a state (1-based ids,
+        in deletion order; hko_contact_element_deleted, v2/HAKAI_j.jl:766-804)."""
+        for e in elements:
+            self.L.hko_contact_element_deleted(self.ct, _p(self._inst, c_int64), int(e))
+
     def contact_pairs(self):
         out = []
         for c in range(self.L.hko_contact_n_pairs(self.ct)):

@@ -303,3 +303,66 @@ def test_contact_mirror_capacity_grows_between_steps():
         assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
         sv.close()
     assert sorted(dels) == gdel
+
+
+def test_contact_group_divided_window_vs_oracle():
+    """A multi-rank run handed to the oracle: a 3-rank divided-search group (reference-order
+    element arithmetic) runs past the first contact deletions; its ranks' states are assembled
+    into the global state, the oracle takes over (surfaces updated for the deletions so far) and
+    both run the next steps -- every rank's state equals the oracle's bit for bit."""
+    from hakai import mesh
+    import oracle as O
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    gdiag, _ = glob.lumped_mass()
+    world, t0, k = 3, 260, 60
+    parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_tuning("elem_exact", 1)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, world, 9090)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        svs.append(sv)
+    step_group(svs, 1, t0)
+    o = O.Oracle(glob)
+    s = o.s
+    dels = []
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        n = l2g - 1
+        for key in ("disp", "disp_pre", "velo"):
+            s[key].reshape(-1, 3)[n] = getattr(st, key).reshape(-1, 3)
+        e0, ne = loc.global_element_offset, loc.nElement
+        gp = slice(8 * e0, 8 * (e0 + ne))
+        for key in ("integ_stress", "integ_strain"):
+            s[key][gp] = getattr(st, key).reshape(-1, 6)
+        for key in ("integ_yield_stress", "integ_eq_plastic_strain", "integ_triax_stress"):
+            s[key][gp] = getattr(st, key)
+        s["element_flag"][e0:e0 + ne] = st.element_flag
+        s["Qe"][e0:e0 + ne] = st.Qe.reshape(-1, 24)
+        dels += [tuple(int(v) for v in x) for x in sv.deleted()]
+    dels.sort()
+    # Q of the last step: the serial element-order assembly (v2/HAKAI_j.jl:668-675) of the ranks' Qe
+    # (a rank's own Q of an interface node is completed only by the next step's exchange)
+    idx = (3 * (glob.elementmat - 1)[:, :, None] + np.arange(3)[None, None, :]).ravel()
+    s["Q"][...] = 0.0
+    np.add.at(s["Q"], idx, s["Qe"].ravel())
+    assert len(dels) > 0, "window must start after contact deletions"
+    s["position"][...] = glob.coordmat + s["disp"].reshape(-1, 3)
+    o.apply_deletions([e for _, e in dels])
+    o.run(t0 + 1, k)
+    step_group(svs, t0 + 1, k)
+    new = []
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        n = l2g - 1
+        assert np.array_equal(st.disp.reshape(-1, 3), s["disp"].reshape(-1, 3)[n])
+        assert np.array_equal(st.velo.reshape(-1, 3), s["velo"].reshape(-1, 3)[n])
+        e0, ne = loc.global_element_offset, loc.nElement
+        assert np.array_equal(st.integ_stress.reshape(-1, 6), s["integ_stress"][8 * e0:8 * (e0 + ne)])
+        assert np.array_equal(st.element_flag, s["element_flag"][e0:e0 + ne])
+        new += [tuple(int(v) for v in x) for x in sv.deleted() if x[0] > t0]
+        sv.close()
+    assert sorted(new) == sorted(tuple(int(v) for v in x) for x in o.deletions)
