@@ -173,6 +173,7 @@ struct Contact {
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
     long long* d_ni_map = nullptr;
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
+
     // events and per-node gather over the touched nodes
     long long cap = 0;
     unsigned int* d_ctl = nullptr;  // kCtl control words (events, max events, dirty, touched counts)
@@ -186,8 +187,10 @@ struct Contact {
     long long tcap = 0;
     int* d_toff = nullptr;          // [tcap] start of each touched node's term range
     int* d_tcnt = nullptr;          // [tcap] its length
-    void* d_cand = nullptr;         // [cand_cap] TriRec of the triangles passing the prefilter
-    long long cand_cap = 0;
+    void* d_cand = nullptr;         // [cand_cap] TriRec of the triangles passing the prefilter, in
+                                    // kCandShards shards of cshard_cap records
+    long long cand_cap = 0, cshard_cap = 0;
+    unsigned int* d_ccnt = nullptr; // [kCandShards * kShardStride] candidate count of each shard
     double* d_terms = nullptr;      // [4 cap][3]
     void* d_tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -247,16 +250,14 @@ struct Range {
 __device__ __forceinline__ Range pair_range(const unsigned long long* bb) {
     Range r;
     r.empty = false;
-    for (int d = 0; d < 3; ++d) {
-        if (bb[d] == ~0ULL || bb[6 + d] == ~0ULL) {  // a side without live nodes
-            r.empty = true;
-            r.mn[d] = r.mx[d] = r.amn[d] = 0.0;
-            continue;
-        }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {  // branch-free: a side without live nodes makes the range empty
+        const bool none = bb[d] == ~0ULL || bb[6 + d] == ~0ULL;
         const double mni = dec(bb[d]), mxi = dec(bb[3 + d]), mnj = dec(bb[6 + d]), mxj = dec(bb[9 + d]);
-        r.mn[d] = fmax(mni, mnj);
-        r.mx[d] = fmin(mxi, mxj);
-        r.amn[d] = fmin(mni, mnj);
+        r.empty |= none;
+        r.mn[d] = none ? 0.0 : fmax(mni, mnj);
+        r.mx[d] = none ? 0.0 : fmin(mxi, mxj);
+        r.amn[d] = none ? 0.0 : fmin(mni, mnj);
     }
     if (!r.empty && (r.mn[0] > r.mx[0] || r.mn[1] > r.mx[1] || r.mn[2] > r.mx[2])) r.empty = true;  // :2304-2306
     return r;
@@ -266,23 +267,28 @@ __device__ __forceinline__ Range pair_range(const unsigned long long* bb) {
 // incremental update (an element was deleted in the previous step), deleted elements found, and
 // the number of nodes with contact force in each of the two ping-pong "touched" lists.
 enum { kEv = 0, kEvMax = 1, kDirty = 2, kDel = 3, kNdel = 4, kTouched = 5 /* [5], [6] */, kNcand = 7, kTerms = 8,
-       kNcandMax = 9, kEvShardMax = 10, kCtl = 16 };
+       kNcandMax = 9, kEvShardMax = 10, kCandShardMax = 11, kCandOver = 12, kCtl = 16 };
 // Events are appended into kEvShards shards, each with its own counter on its own 128-B line: with
 // one counter, every wave that found an event waited on the same memory-side atomic (measured:
 // 0.13 ms of a 0.30 ms contact step on C4).
 constexpr int kEvShards = 64;
 constexpr int kShardStride = 32;  // unsigned ints between shard counters
+// Candidate triangles likewise: prefilter block b appends to shard b % kCandShards (one atomic per
+// block on that shard's counter; clustered candidates fall in consecutive blocks, so shards stay even).
+constexpr int kCandShards = 64;
+constexpr int kFilterBlocks = 2048;  // prefilter grid cap
 
 // Step prologue: pair boxes to (+inf, -inf), event counter to 0, full rebuild if the host forces
 // it, incremental update if an element was deleted in the previous step (del_any == t-1), and
 // the contact forces of the previous step's touched nodes back to 0 (external_force is otherwise
 // never rewritten).
-__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs, int force,
-                           const int* del_any, int t, const double* t_rd, const int* touched_prev, int tsel,
-                           double* fext) {
+__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs,
+                           unsigned int* ccnt, int force, const int* del_any, int t, const double* t_rd,
+                           const int* touched_prev, int tsel, double* fext) {
     if (t_rd) t = (int)*t_rd + 1;  // graph mode: step number from the device counter
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < kEvShards) evs[i * kShardStride] = 0;
+    if (i < kCandShards) ccnt[i * kShardStride] = 0;
     if (i < 12 * npairs) bbox[i] = ((i % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
     if (i == 0) {
         ctl[kEv] = 0;
@@ -290,6 +296,7 @@ __global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* c
         ctl[kDel] = (!force && *del_any == t - 1) ? 1u : 0u;
         ctl[kNdel] = 0;
         ctl[kNcand] = 0;
+        ctl[kCandOver] = 0;
         ctl[kTerms] = 0;
         ctl[kTouched + tsel] = 0;
     }
@@ -679,6 +686,45 @@ __device__ __forceinline__ unsigned block_append(unsigned int* ctr, bool pred, u
     return s_ctl[1] + off + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
 }
 
+// Prefix of 64 shard counters (each clamped to the shard capacity) in LDS, one lane per shard of
+// wave 0 (one load and a wave scan, not 64 dependent loads on one thread): s_pre[0..64] = prefix,
+// s_pre[65] = some shard overflowed, s_pre[66] = raw total, s_pre[67] = largest shard. Returns the
+// clamped total. s_pre holds 68 entries.
+__device__ __forceinline__ long long shard_scan(const unsigned int* cnts, long long shard_cap, unsigned* s_pre) {
+    if (threadIdx.x < 64) {
+        const int q = (int)threadIdx.x;
+        const unsigned v = cnts[q * kShardStride];
+        const unsigned cl = (long long)v < shard_cap ? v : (unsigned)shard_cap;
+        unsigned x = cl, raw = v, mx = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o);
+            if (q >= o) x += y;
+            raw += __shfl_xor(raw, o);
+            mx = max(mx, __shfl_xor(mx, o));
+        }
+        s_pre[q] = x - cl;
+        const bool over = __any((long long)v > shard_cap);
+        if (q == 63) {
+            s_pre[64] = x;
+            s_pre[65] = over ? 1u : 0u;
+            s_pre[66] = raw;
+            s_pre[67] = mx;
+        }
+    }
+    __syncthreads();
+    return s_pre[64];
+}
+
+// index in shard-prefix order -> slot of the shard buffers
+__device__ __forceinline__ long long shard_slot(const unsigned* s_pre, long long shard_cap, long long ev) {
+    int lo = 0, hi = kEvShards;  // s_pre[lo] <= ev < s_pre[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((long long)s_pre[mid] <= ev) lo = mid; else hi = mid;
+    }
+    return (long long)lo * shard_cap + (ev - s_pre[lo]);
+}
+
 // Per-candidate triangle record, written by the prefilter: everything of the loop body at
 // :2371-2698 that does not depend on the contact point (same expressions as the reference, so the
 // same bits), so the per-cell threads start from one load instead of a chain of dependent ones.
@@ -747,7 +793,7 @@ __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const R
 __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
                                                       const int* tri_pair, const int* tri_nodes, const int* tri_ele,
                                                       const PairParam* par, const unsigned long long* bbox,
-                                                      unsigned int* ctl, TriRec* cand, long long cand_cap,
+                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap,
                                                       int own_r, int own_n) {
     const int n = *tri_cnt;
     __shared__ unsigned s_app[2];
@@ -759,7 +805,7 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
         Range r;
         if (q < n) {
             j = tri_live[q];
-            keep = s.flag[tri_ele[j]] == 1 && (own_n <= 1 || j % own_n == own_r);
+            keep = (own_n <= 1 || j % own_n == own_r) && s.flag[tri_ele[j]] == 1;  // own triangles only
             if (keep) {
                 pr = tri_pair[j];
                 r = pair_range(bbox + 12 * pr);
@@ -775,11 +821,12 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
                 }
             }
         }
-        const unsigned slot = block_append(&ctl[kNcand], keep, s_app);
-        if (keep && (long long)slot < cand_cap) {
+        const int shard = (int)(blockIdx.x % kCandShards);
+        const unsigned slot = block_append(&ccnt[shard * kShardStride], keep, s_app);
+        if (keep && (long long)slot < cshard_cap) {
             TriRec T;
             tri_geom(s, j, pr, r, par[pr], tri_nodes, tri_ele, p0, p1, p2, T);
-            cand[slot] = T;
+            cand[shard * cshard_cap + slot] = T;
         }
     }
 }
@@ -890,13 +937,20 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
 }
 
 // 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
-__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const TriRec* cand, long long cand_cap,
+__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
+                                                const TriRec* cand, long long cshard_cap,
                                                 const PairParam* par, const int* boff, const int* blist,
                                                 const int* ni_node, const long long* ni_map, double d_lim,
                                                 double myu, unsigned int* evs, long long shard_cap, int* ev_nodes,
                                                 double* ev_f) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&ctl[kNcandMax], ctl[kNcand]);
-    const long long n = 32LL * std::min<long long>((long long)ctl[kNcand], cand_cap);
+    __shared__ unsigned s_cpre[kCandShards + 4];
+    const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
+        ctl[kNcand] = s_cpre[kCandShards + 2];
+        atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
+        atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
+        ctl[kCandOver] = s_cpre[kCandShards + 1];
+    }
     const int lane = (int)(threadIdx.x & 63);
     const int shard = (int)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kEvShards);
     unsigned int* evn = evs + shard * kShardStride;
@@ -912,7 +966,7 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
         // visited once. Buckets are compared across lanes (readlane), one hash per lane.
         const int cell = (int)(q & 31);
         const bool valid = q < n && cell < 27;
-        const TriRec* rec = cand + (valid ? (q >> 5) : 0);
+        const TriRec* rec = cand + (valid ? shard_slot(s_cpre, cshard_cap, q >> 5) : 0);
         long long mj[3] = {0, 0, 0};
         unsigned hb = 0x80000000u | (unsigned)lane;  // never equal to a real bucket (< 2^31)
         int hoff = 0;
@@ -953,49 +1007,19 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
     }
 }
 
-// Shard prefix of the event counts (clamped to the shard capacity) in LDS, one lane per shard of
-// wave 0 (kEvShards == 64: one load and a wave scan, not 64 dependent loads on one thread);
-// s_pre[kEvShards + 1] = some shard overflowed. Block 0 also publishes the totals for the overflow
-// check and the stats.
-static_assert(kEvShards == 64, "shard_prefix: one wave lane per shard");
+// the event shards; block 0 also publishes the totals for the overflow check and the stats
+static_assert(kEvShards == 64 && kCandShards == 64, "shard_scan: one wave lane per shard");
 __device__ __forceinline__ long long shard_prefix(unsigned int* ctl, const unsigned int* evs, long long shard_cap,
                                                   unsigned* s_pre) {
-    if (threadIdx.x < 64) {
-        const int q = (int)threadIdx.x;
-        const unsigned v = evs[q * kShardStride];
-        const unsigned cl = (long long)v < shard_cap ? v : (unsigned)shard_cap;
-        unsigned x = cl, raw = v, mx = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned y = __shfl_up(x, o);
-            if (q >= o) x += y;
-            raw += __shfl_xor(raw, o);
-            mx = max(mx, __shfl_xor(mx, o));
-        }
-        s_pre[q] = x - cl;
-        const bool over = __any((long long)v > shard_cap);
-        if (q == 63) {
-            s_pre[kEvShards] = x;
-            s_pre[kEvShards + 1] = over ? 1u : 0u;
-        }
-        if (blockIdx.x == 0 && q == 0) {
-            ctl[kEv] = raw;
-            atomicMax(&ctl[kEvMax], raw);
-            atomicMax(&ctl[kEvShardMax], mx);
-        }
+    const long long n = shard_scan(evs, shard_cap, s_pre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl[kEv] = s_pre[kEvShards + 2];
+        atomicMax(&ctl[kEvMax], s_pre[kEvShards + 2]);
+        atomicMax(&ctl[kEvShardMax], s_pre[kEvShards + 3]);
     }
-    __syncthreads();
-    return s_pre[kEvShards];
+    return n;
 }
 
-// event index (in shard-prefix order) -> slot of the shard buffers
-__device__ __forceinline__ long long ev_slot(const unsigned* s_pre, long long shard_cap, long long ev) {
-    int lo = 0, hi = kEvShards;  // s_pre[lo] <= ev < s_pre[hi]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if ((long long)s_pre[mid] <= ev) lo = mid; else hi = mid;
-    }
-    return (long long)lo * shard_cap + (ev - s_pre[lo]);
-}
 
 // Per-node gather of the event terms over the nodes that received one ("touched", a compact list
 // instead of a pass over all nN nodes): count -> per-node term ranges by a wave-aggregated bump
@@ -1005,12 +1029,12 @@ __device__ __forceinline__ long long ev_slot(const unsigned* s_pre, long long sh
 // interface kernels of this and later steps of the call then write nothing (hakai_kernels.hip,
 // poisoned), so the state stays the last good step's and hakai_step reports the overflow.
 __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                           int* cnt, int* touched, int* tpos, int tsel, int* poison, long long cand_cap,
+                           int* cnt, int* touched, int* tpos, int tsel, int* poison,
                            const int* x1ctl, int t, const double* t_rd) {
-    __shared__ unsigned s_pre[kEvShards + 2];
+    __shared__ unsigned s_pre[kEvShards + 4];
     const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
+        const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
         if (over && poison[0] == 0) {
             poison[1] = t_rd ? (int)*t_rd + 1 : t;
             poison[0] = 1;
@@ -1022,7 +1046,7 @@ __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long
         int node = -1;
         bool first = false;
         if (e < n) {
-            node = ev_nodes[4 * ev_slot(s_pre, shard_cap, e >> 2) + (e & 3)];
+            node = ev_nodes[4 * shard_slot(s_pre, shard_cap, e >> 2) + (e & 3)];
             first = atomicAdd(&cnt[node], 1) == 0;
         }
         const unsigned q = block_append(&ctl[kTouched + tsel], first, s_app);
@@ -1057,11 +1081,11 @@ __global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, cons
 __global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
                              const double* ev_f, const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
-    __shared__ unsigned s_pre[kEvShards + 2];
+    __shared__ unsigned s_pre[kEvShards + 4];
     const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const long long ev = ev_slot(s_pre, shard_cap, e >> 2);
+        const long long ev = shard_slot(s_pre, shard_cap, e >> 2);
         const int role = (int)(e & 3);
         const int node = ev_nodes[4 * ev + role];
         const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
@@ -1112,17 +1136,17 @@ struct EvRec {
 // all-gather. Overflow = events beyond a shard, candidates beyond their buffer, or a truncated mirror
 // block: exchanged with the counts so every rank poisons the same step.
 __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                          const double* ev_f, EvRec* out, int* cnt_out, long long cand_cap, const int* x1ctl) {
-    __shared__ unsigned s_pre[kEvShards + 2];
+                          const double* ev_f, EvRec* out, int* cnt_out, const int* x1ctl) {
+    __shared__ unsigned s_pre[kEvShards + 4];
     const long long n = shard_prefix(ctl, evs, shard_cap, s_pre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const bool over = (long long)ctl[kNcand] > cand_cap || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
+        const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
         cnt_out[0] = (int)n;
         cnt_out[1] = over ? 1 : 0;
     }
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const long long sl = ev_slot(s_pre, shard_cap, e);
+        const long long sl = shard_slot(s_pre, shard_cap, e);
         EvRec r;
         for (int k = 0; k < 4; ++k) r.n[k] = ev_nodes[4 * sl + k];
         for (int k = 0; k < 3; ++k) r.f[k] = ev_f[3 * sl + k];
@@ -1603,7 +1627,7 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_ni_map);
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
-    dfree(C->d_terms); dfree(C->d_velo0);
+    dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt);
     if (C->d_tmp) (void)hipFree(C->d_tmp);
     if (Mirror* M = C->mir) {
         (void)comm_gather_register(c, nullptr, nullptr);
@@ -1817,7 +1841,7 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
-    hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
+    hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
                        C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
     if (M)
         hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
@@ -1862,6 +1886,8 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
                            C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
                            C->g_seg);
     }
+    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
+    if (M) M->div_step = div;
     if (C->htot + 1 <= kSmallScan) {
         hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, s, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
     } else {
@@ -1871,21 +1897,20 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     if (C->nseg > 0)
         hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
                            C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
-    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
-    if (M) M->div_step = div;
     if (C->n_tri > 0) {
-        hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, 2048))),
+        hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks))),
                            dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
-                           C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ctl, (TriRec*)C->d_cand,
-                           C->cand_cap, div ? M->rank : 0, div ? M->nranks : 1);
-        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, (const TriRec*)C->d_cand, C->cand_cap,
+                           C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ccnt, (TriRec*)C->d_cand,
+                           C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
+        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
+                           C->cshard_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
     }
     const unsigned ge = (unsigned)C->g_ev;
     if (div) {  // pack this rank's events; the exchange and the sums are phase B
         hipLaunchKernelGGL(k_ev_pack, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt, C->cand_cap, M->d_x1ctl);
+                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt, M->d_x1ctl);
         HIPCHK(hipGetLastError());
         if (!comm_is_rccl(c))  // in-process peers read the count from pinned memory
             HIPCHK(hipMemcpyAsync(M->h_evcnt + 2 * M->nranks, M->d_evcnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1896,7 +1921,7 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
         return 0;
     }
     hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, C->cand_cap,
+                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison,
                        M ? M->d_x1ctl : nullptr, in.t, c->g_trd);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
@@ -2022,6 +2047,17 @@ void contact_graph_advance(hakai_ctx* c, double t_last) {
     C->last_t = (long long)t_last;  // two steps: tsel flipped twice
 }
 
+// candidate buffer of about `total` records in kCandShards shards. A shard holds at least what
+// its prefilter blocks can append in one pass over the triangles (kB per block), so a deck whose
+// triangles fit one pass of the grid cannot overflow a shard -- as the unsharded n_tri-sized
+// buffer could not.
+static void size_cand(Contact* C, long long total) {
+    const long long blocks = std::max<long long>(1, std::min<long long>((C->n_tri + kB - 1) / kB, kFilterBlocks));
+    const long long one_pass = (blocks + kCandShards - 1) / kCandShards * kB;
+    C->cshard_cap = std::max<long long>((total + kCandShards - 1) / kCandShards, one_pass);
+    C->cand_cap = C->cshard_cap * kCandShards;
+}
+
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
@@ -2030,9 +2066,9 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipStreamSynchronize(c->stream));
         if (C->d_cand) (void)hipFree(C->d_cand);
         C->d_cand = nullptr;
-        C->cand_cap = value;
+        size_cand(C, value);
         HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
-        HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, sizeof(unsigned int), c->stream));
+        HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, 3 * sizeof(unsigned int), c->stream));  // + shard max, over
         return 0;
     }
     if (!std::strcmp(key, "contact_mirror_chunks") || !std::strcmp(key, "contact_mirror_deletions")) {
@@ -2110,13 +2146,14 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
 int contact_check(hakai_ctx* c) {
     Contact* C = c->contact;
     if (!C) return 0;
-    unsigned int mx = 0, mc = 0;
+    unsigned int mx = 0, mc[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(&mx, C->d_ctl + kEvMax, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&mc, C->d_ctl + kNcandMax, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(mc, C->d_ctl + kNcandMax, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if ((long long)mc > C->cand_cap)
-        return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step exceed the buffer (%lld); raise "
-                    "hakai_set_tuning(\"contact_candidate_cap\")", mc, C->cand_cap);
+    if ((long long)mc[kCandShardMax - kNcandMax] > C->cshard_cap)
+        return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step (%u in one of %d shards) exceed the "
+                    "buffer (%lld); raise hakai_set_tuning(\"contact_candidate_cap\")", mc[0],
+                    mc[kCandShardMax - kNcandMax], kCandShards, C->cand_cap);
     if (Mirror* M = C->mir) {
         int x1[4];
         HIPCHK(hipMemcpy(x1, M->d_x1ctl, sizeof(x1), hipMemcpyDeviceToHost));
@@ -2517,8 +2554,9 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     {
         long long t0 = 0;  // initial live triangles
         for (int p = 0; p < C->npairs; ++p) t0 += C->pair_counts[3 * p + 1];
-        C->cand_cap = std::min<long long>(std::max<long long>(C->n_tri, 1), std::max<long long>(1 << 16, 4 * t0));
+        size_cand(C, std::min<long long>(std::max<long long>(C->n_tri, 1), std::max<long long>(1 << 16, 4 * t0)));
     }
+    HIPCHK(dalloc(&C->d_ccnt, (size_t)kCandShards * kShardStride));
     HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)H.nN));

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 2: wave-parallel shard prefix + one-scan X1 slots: contact suites, then the C4 contact split
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multirank.py tests/test_gpu_contact.py tests/test_gpu_configs.py tests/test_gpu_graph.py tests/test_gpu_decks.py -m gpu > gpurun_out/r2n_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/r2n_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4n_r1 -o c4 -- python3 -u tools/bench_contact.py --ranks 1 --steps 40 > gpurun_out/r2n_r1.log 2>&1
+rc=$?; echo "r1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4n_r4 -o c4 -- python3 -u tools/bench_contact.py --ranks 4 --divide 1 --serial 1 --steps 40 > gpurun_out/r2n_r4.log 2>&1
+rc=$?; echo "r4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+for r in 1 2 4; do
+  timeout -k 10 300 python -u tools/bench_contact.py --ranks $r --divide 1 --serial 1 --steps 40 >> gpurun_out/r2n_contact.jsonl 2>> gpurun_out/r2n_contact.err
+  rc=$?; echo "bench ranks=$r rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+exit 0
