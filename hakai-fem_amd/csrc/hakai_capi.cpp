@@ -256,6 +256,7 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.exact = c->elem_exact;
     ea.pusai = c->d_pusai;
     ea.fe_mask = c->diag_no_assembly ? 0 : -1;
+    ea.qatomic = c->diag_atomic_q ? c->d_qbuf : nullptr;
     ea.poison = c->d_poison;
     return ea;
 }
@@ -812,7 +813,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.fe_nt = c->nodal_fe_nt;
     na.reverse = c->nodal_reverse;
     na.fe = c->d_fe;
-    na.qbuf = (c->q_from_buf || c->diag_no_assembly) ? c->d_qbuf : nullptr;
+    na.qbuf = (c->q_from_buf || c->diag_no_assembly || c->diag_atomic_q) ? c->d_qbuf : nullptr;
     na.fext = nullptr;
     na.nN = c->nN;
     na.dt = d_time;
@@ -865,6 +866,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     }
     c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
     c->q_from_buf = false;
+    if (c->diag_atomic_q)  // the element kernel adds this step's forces into it
+        HIPCHK(hipMemsetAsync(c->d_qbuf, 0, 3 * (size_t)c->nN * sizeof(double), s));
     // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
@@ -1127,6 +1130,13 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "elem_exact")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact must be 0 or 1");
         c->elem_exact = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "diag_atomic_q")) {  // timing diagnostic only: nondeterministic sums
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "diag_atomic_q must be 0 or 1");
+        if (c->comm && value) return fail(HAKAI_ERR_STATE, "diag_atomic_q: one GPU only");
+        c->diag_atomic_q = (int)value;
+        hkc::graph_invalidate(c);
         return 0;
     }
     if (!std::strcmp(key, "diag_no_assembly")) {  // timing diagnostic only: results are invalid

@@ -73,6 +73,8 @@ struct hakai_ctx {
     int group_serial = 0;        // tuning "group_serial" (rank 0 of a hakai_step_group): drain every rank's
                                  // phase before the next rank's (per-rank timings without the ranks
                                  // sharing the one GPU)
+    int diag_atomic_q = 0;       // tuning "diag_atomic_q": TIMING DIAGNOSTIC -- the element kernel adds the
+                                 // node forces into d_qbuf with FP64 atomics (order nondeterministic)
     int diag_no_assembly = 0;    // tuning "diag_no_assembly": TIMING DIAGNOSTIC, results invalid --
                                  // no element-force traffic (rows to one dummy row, Q read from a
                                  // zero buffer): the step's cost without any force assembly

@@ -105,15 +105,22 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
 
 // Unconditional write-back of one lane (selects, no branches): its node's force fk, its Gauss
 // point's state, the element flag and the deletion log.
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false>
 __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, int k, const ElemIn& in, bool active,
                                                bool kill, const double (&fk)[3], const double (&fin)[6],
                                                const double (&eps)[6], double eqp, double ys, double tri) {
     const long long gp = 8 * e + k, ld = a.ld;
-    double* fo = a.fe + (in.fb & a.fe_mask);
-    fo[0] = active ? fk[0] : 0.0;
-    fo[a.cstride] = active ? fk[1] : 0.0;
-    fo[2 * a.cstride] = active ? fk[2] : 0.0;
+    if (a.qatomic) {  // timing diagnostic: atomics into Q instead of the fe round trip
+        const int src = (int)(threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k));
+        const int node = __shfl(in.n, src);
+        if (active)
+            for (int c = 0; c < 3; ++c) atomicAdd(a.qatomic + 3 * (long long)node + c, fk[c]);
+    } else {
+        double* fo = a.fe + (in.fb & a.fe_mask);
+        fo[0] = active ? fk[0] : 0.0;
+        fo[a.cstride] = active ? fk[1] : 0.0;
+        fo[2 * a.cstride] = active ? fk[2] : 0.0;
+    }
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -623,7 +630,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (WITH_VOL) a.vol[e] = V;
-    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
 }
 
 // Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.

@@ -39,6 +39,9 @@ struct ElemArgs {
     int exact;              // 1: reference-order arithmetic (elem_step_exact), bit-identical to
                             //    cal_stress_hexa; 0: fused single-pass form (elem_step)
     const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
+    double* qatomic;        // null; the timing diagnostic "diag_atomic_q": node forces are added
+                            // straight into this 3nN array with FP64 atomics (no fe round trip,
+                            // nondeterministic summation order: results not bit-reproducible)
     long long fe_mask;      // -1; 0 only in the timing diagnostic "diag_no_assembly" (all force
                             // rows land on one dummy row: no fe traffic, results invalid)
     const int* poison;      // [0] != 0: a contact buffer overflowed in this call; every state-writing
