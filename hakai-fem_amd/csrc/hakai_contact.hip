@@ -173,6 +173,9 @@ struct Contact {
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
     long long* d_ni_map = nullptr;
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
+    // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
+    bool small = false;
+    int fuse_small = 1;
 
     // events and per-node gather over the touched nodes
     long long cap = 0;
@@ -282,14 +285,25 @@ constexpr int kFilterBlocks = 2048;  // prefilter grid cap
 // it, incremental update if an element was deleted in the previous step (del_any == t-1), and
 // the contact forces of the previous step's touched nodes back to 0 (external_force is otherwise
 // never rewritten).
-__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs,
-                           unsigned int* ccnt, int force, const int* del_any, int t, const double* t_rd,
-                           const int* touched_prev, int tsel, double* fext) {
+// Counters the kernels of one launch read after other workgroups' (or, in the fused small-deck
+// kernels, other waves') atomics: an agent-scope load, never a stale L1 line.
+__device__ __forceinline__ unsigned ld_ctl(const unsigned int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The per-step kernels below are bodies over (workgroup bid of nb): the __global__ wrappers pass
+// blockIdx.x / gridDim.x, and the fused small-deck kernels (one workgroup, "Small decks") run
+// several bodies back to back with a workgroup barrier between them.
+__device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* bbox, int npairs, unsigned int* ctl,
+                                           unsigned int* evs, unsigned int* ccnt, int force, const int* del_any,
+                                           int t, const double* t_rd, const int* touched_prev, int tsel,
+                                           double* fext) {
     if (t_rd) t = (int)*t_rd + 1;  // graph mode: step number from the device counter
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = bid * blockDim.x + threadIdx.x;
     if (i < kEvShards) evs[i * kShardStride] = 0;
     if (i < kCandShards) ccnt[i * kShardStride] = 0;
-    if (i < 12 * npairs) bbox[i] = ((i % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
+    for (int q = i; q < 12 * npairs; q += nb * blockDim.x)
+        bbox[q] = ((q % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
     if (i == 0) {
         ctl[kEv] = 0;
         ctl[kDirty] = force ? 1u : 0u;
@@ -300,13 +314,20 @@ __global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* c
         ctl[kTerms] = 0;
         ctl[kTouched + tsel] = 0;
     }
-    const int np = (int)ctl[kTouched + 1 - tsel];
-    for (int q = i; q < np; q += gridDim.x * blockDim.x) {
+    const int np = (int)ld_ctl(&ctl[kTouched + 1 - tsel]);
+    for (int q = i; q < np; q += nb * blockDim.x) {
         const int n = touched_prev[q];
         fext[3 * (long long)n] = 0.0;
         fext[3 * (long long)n + 1] = 0.0;
         fext[3 * (long long)n + 2] = 0.0;
     }
+}
+
+__global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs,
+                           unsigned int* ccnt, int force, const int* del_any, int t, const double* t_rd,
+                           const int* touched_prev, int tsel, double* fext) {
+    reset_body(blockIdx.x, gridDim.x, bbox, npairs, ctl, evs, ccnt, force, del_any, t, t_rd, touched_prev, tsel,
+               fext);
 }
 
 struct StepIn {
@@ -450,22 +471,27 @@ __global__ __launch_bounds__(kB) void k_ct_live_write(const unsigned int* ctl, L
 }
 
 // incremental update, part 1: the elements deleted in the previous step (int4 sweep of del_step)
-__global__ void k_ct_find_del(unsigned int* ctl, const int* del_step, int nE, int t, const double* t_rd, int* dlist) {
-    if (ctl[kDel] == 0) return;
+__device__ __forceinline__ void find_del_body(int bid, int nb, unsigned int* ctl, const int* del_step, int nE, int t,
+                                              const double* t_rd, int* dlist) {
+    if (ld_ctl(&ctl[kDel]) == 0) return;
     if (t_rd) t = (int)*t_rd + 1;
     const int n4 = nE >> 2;
     const int4* d4 = reinterpret_cast<const int4*>(del_step);
-    for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += gridDim.x * blockDim.x) {
+    for (int v = bid * blockDim.x + threadIdx.x; v < n4; v += nb * blockDim.x) {
         const int4 d = d4[v];
         if (d.x == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v;
         if (d.y == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 1;
         if (d.z == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 2;
         if (d.w == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = 4 * v + 3;
     }
-    if (blockIdx.x == 0 && (int)threadIdx.x < nE - 4 * n4) {
+    if (bid == 0 && (int)threadIdx.x < nE - 4 * n4) {
         const int e = 4 * n4 + (int)threadIdx.x;
         if (del_step[e] == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = e;
     }
+}
+
+__global__ void k_ct_find_del(unsigned int* ctl, const int* del_step, int nE, int t, const double* t_rd, int* dlist) {
+    find_del_body(blockIdx.x, gridDim.x, ctl, del_step, nE, t, t_rd, dlist);
 }
 
 // a node entry becomes live with the first deletion among its adders; of several adders deleted in
@@ -490,12 +516,13 @@ struct AppendIn {
 
 // incremental update, part 2: one block per deleted element, one thread per entry its deletion
 // exposes (triangles, then i-node entries, then j-node entries)
-__global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t,
-                            const double* t_rd, int* reg, int* ni_live, int* nj_live, int* tri_live) {
-    if (ctl[kDel] == 0) return;
+__device__ __forceinline__ void append_body(int bid, int nb, unsigned int* ctl, const int* dlist, const AppendIn& A,
+                                            const int* del_step, int t, const double* t_rd, int* reg, int* ni_live,
+                                            int* nj_live, int* tri_live) {
+    if (ld_ctl(&ctl[kDel]) == 0) return;
     if (t_rd) t = (int)*t_rd + 1;
-    const int nd = (int)ctl[kNdel];
-    for (int q = blockIdx.x; q < nd; q += gridDim.x) {
+    const int nd = (int)ld_ctl(&ctl[kNdel]);
+    for (int q = bid; q < nd; q += nb) {
         const int e = dlist[q];
         const int t0 = A.el_tri_ptr[e], nt = A.el_tri_ptr[e + 1] - t0;
         const int i0 = A.el_ni_ptr[e], ni = A.el_ni_ptr[e + 1] - i0;
@@ -516,6 +543,11 @@ __global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, con
             }
         }
     }
+}
+
+__global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t,
+                            const double* t_rd, int* reg, int* ni_live, int* nj_live, int* tri_live) {
+    append_body(blockIdx.x, gridDim.x, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live);
 }
 
 // bounding boxes of the live node lists per pair (:2281-2299). Segment = the live node entries of
@@ -578,15 +610,17 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
 
 // cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts.
 // sb blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
-__global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
-                                               const int* ni_pair, const int* ni_node, const PairParam* par,
-                                               const unsigned long long* bbox, int* qbucket, long long* ni_map,
-                                               int* bcnt, int sb) {
+// vb = virtual block (segment vb / sb, part vb % sb); a launch of nseg * sb workgroups has one each
+__device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* segs, const int* reg, const int* ni_live,
+                                         const int* ni_pair, const int* ni_node, const PairParam* par,
+                                         const unsigned long long* bbox, int* qbucket, long long* ni_map, int* bcnt,
+                                         int sb) {
 #pragma clang fp contract(off)
-    const Seg sg = segs[blockIdx.x / sb];
+    const Seg sg = segs[vb / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
-    for (int q = (blockIdx.x % sb) * kB + (int)threadIdx.x; q < n; q += sb * kB) {
+    const int bd = (int)blockDim.x;
+    for (int q = (vb % sb) * bd + (int)threadIdx.x; q < n; q += sb * bd) {
         const int k = ni_live[base + q];
         const int pr = ni_pair[k];
         const Range r = pair_range(bbox + 12 * pr);
@@ -609,11 +643,18 @@ __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const 
     }
 }
 
+__global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                               const int* ni_pair, const int* ni_node, const PairParam* par,
+                                               const unsigned long long* bbox, int* qbucket, long long* ni_map,
+                                               int* bcnt, int sb) {
+    bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, ni_map, bcnt, sb);
+}
+
 // Exclusive scan of the bucket counts for small bucket tables (n <= kSmallScan): one block of
 // 1024 threads, each scanning a contiguous run. It replaces the two-kernel device-wide scan, whose
 // launches dominate the contact step of small decks ("Launch-bound step loops").
 constexpr int kSmallScan = 32768;
-__global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) {
+__device__ __forceinline__ void scan_small_body(const int* in, int* out, int n) {
     __shared__ int s_w[16];
     // each thread scans a run of `per` entries (a multiple of 4, so the run is whole 16-B vectors:
     // a quarter of the load/store instructions of an element-wise loop)
@@ -645,17 +686,25 @@ __global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out,
     }
 }
 
-__global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
-    const Seg sg = segs[blockIdx.x / sb];
+__global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) { scan_small_body(in, out, n); }
+
+__device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* reg, const int* ni_live,
+                                          const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
+    const Seg sg = segs[vb / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
-    for (int q = (blockIdx.x % sb) * kB + (int)threadIdx.x; q < n; q += sb * kB) {
+    const int bd = (int)blockDim.x;
+    for (int q = (vb % sb) * bd + (int)threadIdx.x; q < n; q += sb * bd) {
         const int b = qbucket[base + q];
         if (b < 0) continue;
         const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
         blist[slot] = ni_live[base + q];
     }
+}
+
+__global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
+                                                const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
+    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, sb);
 }
 
 // wave-aggregated append: one atomic per wave; every lane of the wave must call it
@@ -790,14 +839,14 @@ __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const R
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
 // side of the range box along any axis -> candidate record
 // (multi-GPU divided search: only the triangles j with j % own_n == own_r)
-__global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
-                                                      const int* tri_pair, const int* tri_nodes, const int* tri_ele,
-                                                      const PairParam* par, const unsigned long long* bbox,
-                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap,
-                                                      int own_r, int own_n) {
+__device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s, const int* tri_cnt,
+                                                const int* tri_live, const int* tri_pair, const int* tri_nodes,
+                                                const int* tri_ele, const PairParam* par,
+                                                const unsigned long long* bbox, unsigned int* ccnt, TriRec* cand,
+                                                long long cshard_cap, int own_r, int own_n) {
     const int n = *tri_cnt;
     __shared__ unsigned s_app[2];
-    for (int q0 = blockIdx.x * blockDim.x; q0 < n; q0 += gridDim.x * blockDim.x) {  // block-uniform trip count
+    for (int q0 = bid * blockDim.x; q0 < n; q0 += nb * blockDim.x) {  // block-uniform trip count
         const int q = q0 + (int)threadIdx.x;
         bool keep = false;
         int j = 0, pr = 0;
@@ -821,7 +870,7 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
                 }
             }
         }
-        const int shard = (int)(blockIdx.x % kCandShards);
+        const int shard = bid % kCandShards;
         const unsigned slot = block_append(&ccnt[shard * kShardStride], keep, s_app);
         if (keep && (long long)slot < cshard_cap) {
             TriRec T;
@@ -829,6 +878,15 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
             cand[shard * cshard_cap + slot] = T;
         }
     }
+}
+
+__global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
+                                                      const int* tri_pair, const int* tri_nodes, const int* tri_ele,
+                                                      const PairParam* par, const unsigned long long* bbox,
+                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap,
+                                                      int own_r, int own_n) {
+    tri_filter_body(blockIdx.x, gridDim.x, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par, bbox, ccnt, cand,
+                    cshard_cap, own_r, own_n);
 }
 
 // events of one thread, kept in registers and appended with one atomic per wave (a same-address
@@ -1009,10 +1067,10 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
 
 // the event shards; block 0 also publishes the totals for the overflow check and the stats
 static_assert(kEvShards == 64 && kCandShards == 64, "shard_scan: one wave lane per shard");
-__device__ __forceinline__ long long shard_prefix(unsigned int* ctl, const unsigned int* evs, long long shard_cap,
-                                                  unsigned* s_pre) {
+__device__ __forceinline__ long long shard_prefix(int bid, unsigned int* ctl, const unsigned int* evs,
+                                                  long long shard_cap, unsigned* s_pre) {
     const long long n = shard_scan(evs, shard_cap, s_pre);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
         ctl[kEv] = s_pre[kEvShards + 2];
         atomicMax(&ctl[kEvMax], s_pre[kEvShards + 2]);
         atomicMax(&ctl[kEvShardMax], s_pre[kEvShards + 3]);
@@ -1028,12 +1086,13 @@ __device__ __forceinline__ long long shard_prefix(unsigned int* ctl, const unsig
 // triangles beyond their buffer, a truncated multi-GPU mirror block): the nodal, BC, element and
 // interface kernels of this and later steps of the call then write nothing (hakai_kernels.hip,
 // poisoned), so the state stays the last good step's and hakai_step reports the overflow.
-__global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                           int* cnt, int* touched, int* tpos, int tsel, int* poison,
-                           const int* x1ctl, int t, const double* t_rd) {
+__device__ __forceinline__ void count_body(int bid, int nb, unsigned int* ctl, const unsigned int* evs,
+                                           long long shard_cap, const int* ev_nodes, int* cnt, int* touched,
+                                           int* tpos, int tsel, int* poison, const int* x1ctl, int t,
+                                           const double* t_rd) {
     __shared__ unsigned s_pre[kEvShards + 4];
-    const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const long long n = 4 * shard_prefix(bid, ctl, evs, shard_cap, s_pre);
+    if (bid == 0 && threadIdx.x == 0) {
         const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
         if (over && poison[0] == 0) {
             poison[1] = t_rd ? (int)*t_rd + 1 : t;
@@ -1041,7 +1100,7 @@ __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long
         }
     }
     __shared__ unsigned s_app[2];
-    for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
+    for (long long e0 = bid * (long long)blockDim.x; e0 < n; e0 += (long long)nb * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
         bool first = false;
@@ -1057,10 +1116,17 @@ __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long
     }
 }
 
-__global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, const int* cnt, int* toff, int* tcnt) {
-    const int nt = (int)ctl[kTouched + tsel];
+__global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
+                           int* cnt, int* touched, int* tpos, int tsel, int* poison,
+                           const int* x1ctl, int t, const double* t_rd) {
+    count_body(blockIdx.x, gridDim.x, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, x1ctl, t, t_rd);
+}
+
+__device__ __forceinline__ void alloc_body(int bid, int nb, unsigned int* ctl, int tsel, const int* touched,
+                                           const int* cnt, int* toff, int* tcnt) {
+    const int nt = (int)ld_ctl(&ctl[kTouched + tsel]);
     const int lane = (int)(threadIdx.x & 63);
-    for (int q0 = blockIdx.x * blockDim.x; q0 < nt; q0 += gridDim.x * blockDim.x) {
+    for (int q0 = bid * blockDim.x; q0 < nt; q0 += nb * blockDim.x) {
         const int q = q0 + (int)threadIdx.x;
         const int c = q < nt ? cnt[touched[q]] : 0;
         int x = c;  // wave inclusive scan
@@ -1078,13 +1144,17 @@ __global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, cons
     }
 }
 
-__global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                             const double* ev_f, const int* toff, const int* tpos, int* cnt, double* terms) {
+__global__ void k_ct_alloc(unsigned int* ctl, int tsel, const int* touched, const int* cnt, int* toff, int* tcnt) {
+    alloc_body(blockIdx.x, gridDim.x, ctl, tsel, touched, cnt, toff, tcnt);
+}
+
+__device__ __forceinline__ void scatter_body(int bid, int nb, unsigned int* ctl, const unsigned int* evs,
+                                             long long shard_cap, const int* ev_nodes, const double* ev_f,
+                                             const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
     __shared__ unsigned s_pre[kEvShards + 4];
-    const long long n = 4 * shard_prefix(ctl, evs, shard_cap, s_pre);
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
-         e += (long long)gridDim.x * blockDim.x) {
+    const long long n = 4 * shard_prefix(bid, ctl, evs, shard_cap, s_pre);
+    for (long long e = bid * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)nb * blockDim.x) {
         const long long ev = shard_slot(s_pre, shard_cap, e >> 2);
         const int role = (int)(e & 3);
         const int node = ev_nodes[4 * ev + role];
@@ -1103,12 +1173,17 @@ __global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long lo
     }
 }
 
+__global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
+                             const double* ev_f, const int* toff, const int* tpos, int* cnt, double* terms) {
+    scatter_body(blockIdx.x, gridDim.x, ctl, evs, shard_cap, ev_nodes, ev_f, toff, tpos, cnt, terms);
+}
+
 // external_force = 0.0 + (sum of the node's terms), summed in double-double and rounded once
-__global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
-                         const double* terms, double* fext) {
+__device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ctl, int tsel, const int* touched,
+                                         const int* toff, const int* tcnt, const double* terms, double* fext) {
 #pragma clang fp contract(off)
-    const int nt = (int)ctl[kTouched + tsel];
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
+    const int nt = (int)ld_ctl(&ctl[kTouched + tsel]);
+    for (int q = bid * blockDim.x + threadIdx.x; q < nt; q += nb * blockDim.x) {
         const long long n = touched[q];
         const int a = toff[q], b = a + tcnt[q];
         for (int c = 0; c < 3; ++c) {
@@ -1126,6 +1201,100 @@ __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, 
     }
 }
 
+__global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
+                         const double* terms, double* fext) {
+    sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext);
+}
+
+// ---- small decks: fused single-workgroup phases ------------------------------------------------
+// The reference's own decks have a few thousand contact entries and tens of events per step, so
+// the ~13 launches of a contact step (each >= ~2.4 us from a graph, tools/barrier_probe.hip) cost
+// more than their work. For models small at setup (Contact::small) the step runs the prologue
+// (reset, deletion scan, surface append), the bucket scan + fill, and the event gather (count,
+// alloc, scatter, sum) each as ONE 1024-thread workgroup, the bodies separated by workgroup
+// barriers; the binning and the triangle prefilter share one launch. Same bodies, same results.
+constexpr int kSmallThreads = 1024;
+
+__global__ __launch_bounds__(kSmallThreads) void k_ct_prologue1(
+    unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs, unsigned int* ccnt, const int* del_any,
+    int t, const double* t_rd, const int* touched_prev, int tsel, double* fext, const int* del_step, int nE,
+    int* dlist, AppendIn A, int* reg, int* ni_live, int* nj_live, int* tri_live, int with_lists) {
+    reset_body(0, 1, bbox, npairs, ctl, evs, ccnt, 0, del_any, t, t_rd, touched_prev, tsel, fext);
+    if (!with_lists) return;
+    __syncthreads();
+    find_del_body(0, 1, ctl, del_step, nE, t, t_rd, dlist);
+    __syncthreads();
+    append_body(0, 1, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live);
+}
+
+// the fill over every i-node entry of every pair at once: the segments' live counts are loaded in
+// parallel (one thread each) and prefix-summed in LDS, and each thread finds its entry's segment by
+// binary search (a loop over the segments would chain their latencies; nseg <= kSmallThreads)
+__global__ __launch_bounds__(kSmallThreads) void k_ct_scanfill1(const Seg* segs, int nseg, const int* reg,
+                                                                const int* ni_live, const int* qbucket, int* bcnt,
+                                                                int* boff, int nb1, int* blist) {
+    __shared__ int s_base[kSmallThreads], s_off[kSmallThreads + 1], s_w[kSmallThreads / 64];
+    const int g = (int)threadIdx.x;
+    int cnt = 0, base = 0;
+    if (g < nseg) {
+        const Seg sg = segs[g];
+        if (sg.side == 0) {
+            base = reg[2 * sg.region];
+            cnt = reg[2 * sg.region + 1];
+        }
+    }
+    int total;
+    const int off = block_excl_scan(cnt, s_w, total);
+    s_base[g] = base;
+    s_off[g] = off;
+    if (g == 0) s_off[kSmallThreads] = total;
+    scan_small_body(bcnt, boff, nb1);  // its barriers also publish s_base / s_off
+    __syncthreads();
+    for (int q = g; q < total; q += (int)blockDim.x) {
+        int lo = 0, hi = kSmallThreads;  // s_off[lo] <= q < s_off[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_off[mid] <= q) lo = mid; else hi = mid;
+        }
+        const int idx = s_base[lo] + (q - s_off[lo]);
+        const int b = qbucket[idx];
+        if (b < 0) continue;
+        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
+        blist[slot] = ni_live[idx];
+    }
+}
+
+__global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl, const unsigned int* evs,
+                                                              long long shard_cap, const int* ev_nodes,
+                                                              const double* ev_f, int* cnt, int* touched, int* tpos,
+                                                              int tsel, int* poison, const int* x1ctl, int t,
+                                                              const double* t_rd, int* toff, int* tcnt,
+                                                              double* terms, double* fext) {
+    count_body(0, 1, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, x1ctl, t, t_rd);
+    __syncthreads();
+    alloc_body(0, 1, ctl, tsel, touched, cnt, toff, tcnt);
+    __syncthreads();
+    scatter_body(0, 1, ctl, evs, shard_cap, ev_nodes, ev_f, toff, tpos, cnt, terms);
+    __syncthreads();
+    sum_body(0, 1, ctl, tsel, touched, toff, tcnt, terms, fext);
+}
+
+// binning (workgroups [0, nbin)) and the triangle prefilter (the rest) in one launch: both need
+// only the pair boxes
+__global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                                     const int* ni_pair, const int* ni_node, const PairParam* par,
+                                                     const unsigned long long* bbox, int* qbucket, long long* ni_map,
+                                                     int* bcnt, int sb, int nbin, const int* tri_cnt,
+                                                     const int* tri_live, const int* tri_pair, const int* tri_nodes,
+                                                     const int* tri_ele, unsigned int* ccnt, TriRec* cand,
+                                                     long long cshard_cap) {
+    if ((int)blockIdx.x < nbin)
+        bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, ni_map, bcnt, sb);
+    else
+        tri_filter_body(blockIdx.x - nbin, gridDim.x - nbin, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par,
+                        bbox, ccnt, cand, cshard_cap, 0, 1);
+}
+
 // ---- divided multi-GPU search: event exchange ------------------------------------------------
 struct EvRec {
     int n[4];     // i, j0, j1, j2
@@ -1138,7 +1307,7 @@ struct EvRec {
 __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
                           const double* ev_f, EvRec* out, int* cnt_out, const int* x1ctl) {
     __shared__ unsigned s_pre[kEvShards + 4];
-    const long long n = shard_prefix(ctl, evs, shard_cap, s_pre);
+    const long long n = shard_prefix(blockIdx.x, ctl, evs, shard_cap, s_pre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
         cnt_out[0] = (int)n;
@@ -1841,67 +2010,94 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
-    hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
-                       C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
-    if (M)
-        hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
-                           M->d_g2l, c->d_fext);
-    C->force_rebuild = false;
-    C->last_t = in.t;
-    if (C->ntile > 0) {
-        LiveIn L;
-        L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
-        L.nj_orig = C->d_nj_orig; L.nj_aptr = C->d_nj_aptr; L.nj_add = C->d_nj_add;
-        L.tri_ele = C->d_tri_ele; L.tri_adder = C->d_tri_adder;
-        L.flag = in.flag; L.del_step = del_step; L.t = in.t;
-        const Tile* tl = (const Tile*)C->d_tiles;
-        const unsigned gt = (unsigned)std::min(C->ntile, 2048);
-        // full rebuild (forced steps only: the host knows them, so the kernels are not even launched
-        // otherwise)
-        if (rebuild) {
-            hipLaunchKernelGGL(k_ct_live_count, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_cnt);
-            hipLaunchKernelGGL(k_ct_live_scan, dim3(1), dim3(kB), 0, s, C->d_ctl, C->ntile, C->d_tile_cnt,
-                               C->d_tile_off, C->nreg, C->d_reg_first, C->d_reg);
-            hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
-                               C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+    // small decks: reset + deletion scan + surface append in one workgroup (not on full-rebuild
+    // steps, whose live-list rebuild sits between the reset and the scan)
+    const bool fused = C->small && C->fuse_small && !M;
+    AppendIn A;
+    A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
+    A.el_ni_ptr = C->d_el_ni_ptr; A.el_ni = C->d_el_ni; A.el_nj_ptr = C->d_el_nj_ptr; A.el_nj = C->d_el_nj;
+    A.ni_orig = C->d_ni_orig; A.ni_aptr = C->d_ni_aptr; A.ni_add = C->d_ni_add; A.ni_pair = C->d_ni_pair;
+    A.nj_orig = C->d_nj_orig; A.nj_aptr = C->d_nj_aptr; A.nj_add = C->d_nj_add; A.nj_pair = C->d_nj_pair;
+    A.pair_reg = C->d_pair_reg;
+    A.tri_reg = C->tri_reg;
+    if (fused && !rebuild) {
+        hipLaunchKernelGGL(k_ct_prologue1, dim3(1), dim3(kSmallThreads), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
+                           C->d_ccnt, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext, del_step,
+                           (int)C->nE, C->d_dlist, A, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live,
+                           C->ntile > 0 ? 1 : 0);
+        C->force_rebuild = false;
+        C->last_t = in.t;
+    } else {
+        hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
+                           C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
+        if (M)
+            hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
+                               M->d_g2l, c->d_fext);
+        C->force_rebuild = false;
+        C->last_t = in.t;
+        if (C->ntile > 0) {
+            LiveIn L;
+            L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
+            L.nj_orig = C->d_nj_orig; L.nj_aptr = C->d_nj_aptr; L.nj_add = C->d_nj_add;
+            L.tri_ele = C->d_tri_ele; L.tri_adder = C->d_tri_adder;
+            L.flag = in.flag; L.del_step = del_step; L.t = in.t;
+            const Tile* tl = (const Tile*)C->d_tiles;
+            const unsigned gt = (unsigned)std::min(C->ntile, 2048);
+            // full rebuild (forced steps only: the host knows them, so the kernels are not even launched
+            // otherwise)
+            if (rebuild) {
+                hipLaunchKernelGGL(k_ct_live_count, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_cnt);
+                hipLaunchKernelGGL(k_ct_live_scan, dim3(1), dim3(kB), 0, s, C->d_ctl, C->ntile, C->d_tile_cnt,
+                                   C->d_tile_off, C->nreg, C->d_reg_first, C->d_reg);
+                hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
+                                   C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
+            }
+            // incremental update (steps after a deletion)
+            hipLaunchKernelGGL(k_ct_find_del, dim3(C->g_del), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
+                               c->g_trd, C->d_dlist);
+            hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
+                               c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
         }
-        // incremental update (steps after a deletion)
-        hipLaunchKernelGGL(k_ct_find_del, dim3(C->g_del), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
-                           c->g_trd, C->d_dlist);
-        AppendIn A;
-        A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
-        A.el_ni_ptr = C->d_el_ni_ptr; A.el_ni = C->d_el_ni; A.el_nj_ptr = C->d_el_nj_ptr; A.el_nj = C->d_el_nj;
-        A.ni_orig = C->d_ni_orig; A.ni_aptr = C->d_ni_aptr; A.ni_add = C->d_ni_add; A.ni_pair = C->d_ni_pair;
-        A.nj_orig = C->d_nj_orig; A.nj_aptr = C->d_nj_aptr; A.nj_add = C->d_nj_add; A.nj_pair = C->d_nj_pair;
-        A.pair_reg = C->d_pair_reg;
-        A.tri_reg = C->tri_reg;
-        hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
-                           c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
     }
+    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
+    if (M) M->div_step = div;
+    const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
+    // small decks: binning + prefilter in one launch, bucket scan + fill in one workgroup
+    const bool fused_mid = fused && C->nseg > 0 && C->nseg <= kSmallThreads && C->n_tri > 0 && C->htot + 1 <= kSmallScan;
     if (C->nseg > 0) {
         const Seg* sg = (const Seg*)C->d_seg;
         hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
                            C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_seg);
-        hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                           C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
-                           C->g_seg);
+        if (fused_mid) {
+            const int nbin = C->nseg * C->g_seg;
+            hipLaunchKernelGGL(k_ct_binfilter, dim3((unsigned)nbin + gfilt), dim3(kB), 0, s, in, sg, C->d_reg,
+                               C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map,
+                               C->d_bcnt, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
+                               C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_ccnt, (TriRec*)C->d_cand,
+                               C->cshard_cap);
+            hipLaunchKernelGGL(k_ct_scanfill1, dim3(1), dim3(kSmallThreads), 0, s, sg, C->nseg, C->d_reg,
+                               C->d_ni_live, C->d_qbucket, C->d_bcnt, C->d_boff, (int)(C->htot + 1), C->d_blist);
+        } else {
+            hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                               C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
+                               C->g_seg);
+        }
     }
-    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
-    if (M) M->div_step = div;
-    if (C->htot + 1 <= kSmallScan) {
+    if (fused_mid) {
+    } else if (C->htot + 1 <= kSmallScan) {
         hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, s, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
     } else {
         size_t tb = C->tmp_bytes;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
     }
-    if (C->nseg > 0)
+    if (C->nseg > 0 && !fused_mid)
         hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
                            C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
     if (C->n_tri > 0) {
-        hipLaunchKernelGGL(k_ct_tri_filter, dim3((unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks))),
-                           dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live, C->d_tri_pair,
-                           C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox, C->d_ccnt, (TriRec*)C->d_cand,
-                           C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
+        if (!fused_mid)
+            hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
+                               C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
+                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
         hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
                            C->cshard_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
@@ -1917,6 +2113,14 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
         HIPCHK(hipEventRecord(M->ev_evpacked, s));
         M->div_t = in.t;
         ++M->div_seq;
+        C->use_velo0 = false;
+        return 0;
+    }
+    if (fused) {  // small decks: count, alloc, scatter and sum in one workgroup
+        hipLaunchKernelGGL(k_ct_gather1, dim3(1), dim3(kSmallThreads), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
+                           C->d_ev_nodes, C->d_ev_f, C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison,
+                           nullptr, in.t, c->g_trd, C->d_toff, C->d_tcnt, C->d_terms, fext);
+        HIPCHK(hipGetLastError());
         C->use_velo0 = false;
         return 0;
     }
@@ -2061,6 +2265,12 @@ static void size_cand(Contact* C, long long total) {
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
+    if (!std::strcmp(key, "contact_fuse_small")) {  // small decks: fused single-workgroup phases
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_small must be 0 or 1");
+        C->fuse_small = (int)value;
+        graph_invalidate(c);
+        return 0;
+    }
     if (!std::strcmp(key, "contact_candidate_cap")) {
         if (value < 1 || value > (1LL << 31) - 1) return fail(HAKAI_ERR_ARG, "contact_candidate_cap out of range");
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -2406,6 +2616,9 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     C->n_nj = (int)nj_node.size();
     C->n_tri = (int)tri_ele.size();
     C->nseg = (int)seg.size() / 8;
+    // fused small-deck phases: one 1024-thread workgroup scans the deletion steps, the bucket table
+    // and the i-node entries a few times at most
+    C->small = C->nE <= (1 << 16) && C->n_ni <= (1 << 16) && C->htot + 1 <= kSmallScan;
     {  // event buffer: 8 events per initial contact point (overflow is detected and reported)
         long long ci0 = 0;
         for (int p = 0; p < C->npairs; ++p) ci0 += C->pair_counts[3 * p];
