@@ -1250,17 +1250,35 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_scanfill1(const Seg* segs,
     if (g == 0) s_off[kSmallThreads] = total;
     scan_small_body(bcnt, boff, nb1);  // its barriers also publish s_base / s_off
     __syncthreads();
-    for (int q = g; q < total; q += (int)blockDim.x) {
-        int lo = 0, hi = kSmallThreads;  // s_off[lo] <= q < s_off[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (s_off[mid] <= q) lo = mid; else hi = mid;
+    // four entries per thread per pass, their loads and atomics issued together (a plain loop chains
+    // each entry's load -> atomic -> store latency)
+    constexpr int U = 4;
+    for (int q0 = 0; q0 < total; q0 += U * (int)blockDim.x) {
+        int idx[U], b[U], node[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = q0 + u * (int)blockDim.x + g;
+            idx[u] = -1;
+            if (q < total) {
+                int lo = 0, hi = kSmallThreads;  // s_off[lo] <= q < s_off[hi]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_off[mid] <= q) lo = mid; else hi = mid;
+                }
+                idx[u] = s_base[lo] + (q - s_off[lo]);
+            }
         }
-        const int idx = s_base[lo] + (q - s_off[lo]);
-        const int b = qbucket[idx];
-        if (b < 0) continue;
-        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-        blist[slot] = ni_live[idx];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            b[u] = idx[u] >= 0 ? qbucket[idx[u]] : -1;
+            node[u] = idx[u] >= 0 ? ni_live[idx[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b[u] >= 0) b[u] = boff[b[u]] + atomicSub(&bcnt[b[u]], 1) - 1;  // leaves bcnt zeroed
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b[u] >= 0) blist[b[u]] = node[u];
     }
 }
 
@@ -2636,7 +2654,9 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         for (int q = 0; q < C->nseg; ++q) maxseg = std::max<long long>(maxseg, seg[8 * q + 1] - seg[8 * q]);
         C->g_seg = clampi((maxseg + kB - 1) / kB, 1, kSegBlocks);
         C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
-        C->g_tri = clampi((32 * ct0 / 4 + 127) / 128, 32, 4096);  // >= 64 waves: every event shard
+        // >= 64 waves (every event shard); one pass over every live triangle as a candidate (32
+        // lanes each) up to the 4096-block cap -- small self-contact decks keep half their triangles
+        C->g_tri = clampi((32 * ct0 + 127) / 128, 32, 4096);
         C->g_node = clampi((2 * ci0 + kB - 1) / kB, 4, 256);
         C->g_del = clampi((C->nE / 4 + kB - 1) / kB, 1, 1024);
         C->g_reset = clampi((std::max<long long>(std::max<long long>(kEvShards, 12LL * C->npairs), 2 * ci0) + kB - 1) / kB,

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=10000, help="steps per hakai_step call (output cadence)")
     ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_fuse_small=0")
     ap.add_argument("--modes", default="1,0", help="elem_exact values to time")
+    ap.add_argument("--max-steps", type=int, default=0, help="cap the GPU steps (profiling runs)")
     a = ap.parse_args()
     tuning = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in a.tuning.split(",") if kv]
     import numpy as np
@@ -54,7 +55,7 @@ def main():
     for name in a.decks.split(","):
         z = np.load(os.path.join(ROOT, "tests", "golden", f"deck_{name}.npz"))
         m = model_from_arrays(z, name)
-        steps = int(z["steps"])
+        steps = int(z["steps"]) if a.max_steps <= 0 else min(int(z["steps"]), a.max_steps)
         out = {"deck": name, "elements": int(m.nElement), "nodes": int(m.nNode), "steps": steps,
                "contact_flag": int(m.contact_flag), "tuning": dict(tuning)}
         for exact in [int(x) for x in a.modes.split(",")]:
