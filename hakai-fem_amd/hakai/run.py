@@ -32,11 +32,51 @@ from .solver import Solver, State, comm_unique_id, step_group
 I64 = ctypes.c_int64
 
 
+OUT_KEYS = ("disp", "velo", "integ_stress", "integ_strain", "integ_eq_plastic_strain", "integ_triax_stress",
+            "element_flag")
+
+
 def _gather_state(sv: Solver) -> dict:
     st = sv.download(disp=True, velo=True, integ_stress=True, integ_strain=True, integ_eq_plastic_strain=True,
                      integ_triax_stress=True, element_flag=True)
-    return {k: getattr(st, k) for k in ("disp", "velo", "integ_stress", "integ_strain", "integ_eq_plastic_strain",
-                                        "integ_triax_stress", "element_flag")}
+    return {k: getattr(st, k) for k in OUT_KEYS}
+
+
+def _out_shapes(n_nodes: int, n_elem: int) -> dict:
+    """Shapes and dtypes of a rank's output arrays (as Solver.download returns them)."""
+    return {"disp": ((3 * n_nodes,), np.float64), "velo": ((3 * n_nodes,), np.float64),
+            "integ_stress": ((8 * n_elem, 6), np.float64), "integ_strain": ((8 * n_elem, 6), np.float64),
+            "integ_eq_plastic_strain": ((8 * n_elem,), np.float64),
+            "integ_triax_stress": ((8 * n_elem,), np.float64), "element_flag": ((n_elem,), np.int64)}
+
+
+def gather_parts(tdist, group, rank: int, world: int, part: dict, metas: list, device=None):
+    """Rank 0 collects every rank's output arrays for one output step: raw point-to-point transfers
+    into preallocated buffers, no pickling (gather_object pickled ~1.8 GB per rank per
+    output at C5). device=None: host tensors over `group` (gloo); a CUDA device: the arrays travel
+    as device tensors over the NCCL (RCCL, xGMI) group. metas[r] = (l2g, e0, n_elem) of rank r
+    (exchanged once at setup). Returns [(meta, arrays)] on rank 0, None elsewhere."""
+    import torch
+    if rank != 0:
+        for k in OUT_KEYS:
+            t = torch.from_numpy(np.ascontiguousarray(part[k]))
+            tdist.send(t if device is None else t.to(device), 0, group=group)
+        return None
+    out = [(metas[0][:2], part)]
+    for r in range(1, world):
+        l2g, e0, ne = metas[r]
+        arrs = {}
+        for k, (shape, dt) in _out_shapes(len(l2g), ne).items():
+            if device is None:
+                buf = np.empty(shape, dt)
+                tdist.recv(torch.from_numpy(buf), r, group=group)
+            else:
+                t = torch.empty(shape, dtype=torch.float64 if dt == np.float64 else torch.int64, device=device)
+                tdist.recv(t, r, group=group)
+                buf = t.cpu().numpy()
+            arrs[k] = buf
+        out.append(((l2g, e0), arrs))
+    return out
 
 
 class _Output:
@@ -128,6 +168,12 @@ def hakai_multi(fname: str, out_dir: str = "temp", local_ranks: int = 0, device:
         tdist.broadcast_object_list(obj, src=0)
         sv, mt = _setup_rank(glob, gdiag, rank, world, device, lambda s: s.comm_init(rank, world, obj[0]))
         svs, meta = [sv], [mt]
+        # output transfers: raw arrays as device tensors over the world's NCCL (RCCL) group, or host
+        # tensors if the world runs gloo; the partition metadata once
+        out_group = None
+        out_dev = torch.device("cuda", device) if tdist.get_backend() == "nccl" else None
+        metas = [None] * world if rank == 0 else None
+        tdist.gather_object((mt[0], mt[1], sv.model.nElement), metas, dst=0)
     if verbose and rank == 0:
         print(f"readInpFile:{fname}\nnNode:{glob.nNode}\nnElement:{glob.nElement}\ncontact_flag:{glob.contact_flag}")
         print(f"mass_scaling:{glob.mass_scaling:g}\ntime_num:{time_num:g}\nranks:{world}")
@@ -136,9 +182,7 @@ def hakai_multi(fname: str, out_dir: str = "temp", local_ranks: int = 0, device:
     def output(idx):
         parts = [(mt, _gather_state(sv)) for sv, mt in zip(svs, meta)]
         if tdist is not None:
-            allp = [None] * world if rank == 0 else None
-            tdist.gather_object(parts[0], allp, dst=0)
-            parts = allp
+            parts = gather_parts(tdist, out_group, rank, world, parts[0][1], metas, out_dev)
         if out is not None:
             out.write(idx, parts)
 
