@@ -122,7 +122,8 @@ struct Mirror {
     void* d_ev_send[2] = {nullptr, nullptr};  // [ev_cap] EvRec, this rank's events of step t in [t&1]
                                       // (in-process peers copy them while this rank moves on)
     long long ev_cap = 0;
-    int* d_evcnt = nullptr;           // [2] this rank's (event count, overflow) of the step
+    int* d_evcnt = nullptr;           // [2][2] this rank's (event count, overflow) of step t in slot t & 1
+                                      // (double-buffered like d_ev_send: in-process peers read it)
     int* d_evcnt_all = nullptr;       // [2 nranks] every rank's
     int* h_evcnt = nullptr;           // pinned [2 nranks]: every rank's, read by the host; [2 nranks..] own
     hipEvent_t ev_evpacked = nullptr; // this rank's events packed (in-process peers wait on it)
@@ -168,6 +169,8 @@ struct Contact {
     // launch grids sized at setup from the contact model (small decks: few blocks, so the ~20
     // per-step kernels are not dominated by dispatching idle workgroups); every loop is grid-stride
     int g_seg = 256, g_ev = 1024, g_tri = 4096, g_node = 256, g_del = 1024, g_reset = 64;
+    int g_box = 32;  // bounding boxes: blocks per segment (each block ends in 6 atomics on the pair's
+                     // 6 bounds, so fewer, longer blocks: ~16 entries per thread)
     // hash grid over i-nodes
     int htot = 0;
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
@@ -294,10 +297,12 @@ __device__ __forceinline__ unsigned ld_ctl(const unsigned int* p) {
 // The per-step kernels below are bodies over (workgroup bid of nb): the __global__ wrappers pass
 // blockIdx.x / gridDim.x, and the fused small-deck kernels (one workgroup, "Small decks") run
 // several bodies back to back with a workgroup barrier between them.
+// (multi-GPU mirror: g2l maps a global touched node to this rank's copy in lfext, -1 if none;
+// null without a mirror)
 __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* bbox, int npairs, unsigned int* ctl,
                                            unsigned int* evs, unsigned int* ccnt, int force, const int* del_any,
                                            int t, const double* t_rd, const int* touched_prev, int tsel,
-                                           double* fext) {
+                                           double* fext, const int* g2l = nullptr, double* lfext = nullptr) {
     if (t_rd) t = (int)*t_rd + 1;  // graph mode: step number from the device counter
     const int i = bid * blockDim.x + threadIdx.x;
     if (i < kEvShards) evs[i * kShardStride] = 0;
@@ -320,14 +325,22 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
         fext[3 * (long long)n] = 0.0;
         fext[3 * (long long)n + 1] = 0.0;
         fext[3 * (long long)n + 2] = 0.0;
+        if (g2l) {
+            const long long l = g2l[n];
+            if (l >= 0) {
+                lfext[3 * l] = 0.0;
+                lfext[3 * l + 1] = 0.0;
+                lfext[3 * l + 2] = 0.0;
+            }
+        }
     }
 }
 
 __global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs,
                            unsigned int* ccnt, int force, const int* del_any, int t, const double* t_rd,
-                           const int* touched_prev, int tsel, double* fext) {
+                           const int* touched_prev, int tsel, double* fext, const int* g2l, double* lfext) {
     reset_body(blockIdx.x, gridDim.x, bbox, npairs, ctl, evs, ccnt, force, del_any, t, t_rd, touched_prev, tsel,
-               fext);
+               fext, g2l, lfext);
 }
 
 struct StepIn {
@@ -557,7 +570,9 @@ constexpr int kSegBlocks = 256;
 
 struct Seg {
     int start, end, pair, side;  // side 0: i-nodes, 1: j-nodes
-    int region, pad[3];
+    int region;
+    int dup;       // 1: the same live node set as an earlier segment, whose boxes also fill this one's
+    int alias[2];  // bbox offsets (12 pair + 6 side) of up to two such duplicates, -1 if none
 };
 
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
@@ -567,13 +582,15 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
                                                 const int* nj_live, const int* ni_node, const int* nj_node,
                                                 unsigned long long* bbox, int sb) {
     const Seg sg = segs[blockIdx.x / sb];
+    if (sg.dup) return;  // another segment's blocks fill its boxes
     const int sub = blockIdx.x % sb;
     const bool side_i = sg.side == 0;
     const int* node = side_i ? ni_node : nj_node;
     const int* lst = (side_i ? ni_live : nj_live) + reg[2 * sg.region];
     const int cnt = reg[2 * sg.region + 1];
     unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
-    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += sb * kB) {
+#pragma unroll 4
+    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += sb * kB) {  // iterations overlap their loads
         double p[3];
         pos(s, node[lst[q]], p);
         for (int d = 0; d < 3; ++d) {
@@ -599,11 +616,15 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
         const int q = threadIdx.x;
         unsigned long long v = red[0][q];
         for (int ww = 1; ww < kB / 64; ++ww) v = q < 3 ? umin64(v, red[ww][q]) : umax64(v, red[ww][q]);
-        unsigned long long* bb = bbox + 12 * sg.pair + (side_i ? 0 : 6);
-        if (q < 3) {
-            if (v != ~0ULL) atomicMin(&bb[q], v);
-        } else if (v != 0ULL) {
-            atomicMax(&bb[q], v);
+        for (int a = -1; a < 2; ++a) {  // own slot, then the duplicates'
+            const int off = a < 0 ? 12 * sg.pair + (side_i ? 0 : 6) : sg.alias[a];
+            if (off < 0) continue;
+            unsigned long long* bb = bbox + off;
+            if (q < 3) {
+                if (v != ~0ULL) atomicMin(&bb[q], v);
+            } else if (v != 0ULL) {
+                atomicMax(&bb[q], v);
+            }
         }
     }
 }
@@ -1180,7 +1201,8 @@ __global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long lo
 
 // external_force = 0.0 + (sum of the node's terms), summed in double-double and rounded once
 __device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ctl, int tsel, const int* touched,
-                                         const int* toff, const int* tcnt, const double* terms, double* fext) {
+                                         const int* toff, const int* tcnt, const double* terms, double* fext,
+                                         const int* g2l = nullptr, double* lfext = nullptr) {
 #pragma clang fp contract(off)
     const int nt = (int)ld_ctl(&ctl[kTouched + tsel]);
     for (int q = bid * blockDim.x + threadIdx.x; q < nt; q += nb * blockDim.x) {
@@ -1198,12 +1220,17 @@ __device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ct
             }
             fext[3 * n + c] = s + e;
         }
+        if (g2l) {  // multi-GPU mirror: this rank's copy of the node
+            const long long l = g2l[n];
+            if (l >= 0)
+                for (int c = 0; c < 3; ++c) lfext[3 * l + c] = fext[3 * n + c];
+        }
     }
 }
 
 __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
-                         const double* terms, double* fext) {
-    sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext);
+                         const double* terms, double* fext, const int* g2l, double* lfext) {
+    sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext, g2l, lfext);
 }
 
 // ---- small decks: fused single-workgroup phases ------------------------------------------------
@@ -1343,21 +1370,19 @@ __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long 
 
 constexpr int kMaxDivRanks = 64;  // divided search: ranks whose event offsets a block holds in LDS
 
-// an overflow on some rank (divided search): poison step t unless an earlier step already is
-__global__ void k_poison_mark(int* poison, int t) {
-    if (threadIdx.x == 0 && poison[0] == 0) {
-        poison[1] = t;
-        poison[0] = 1;
-    }
-}
+// every rank's (count, overflow) word pair, wherever it lives: the RCCL-gathered array, or the
+// in-process peers' own device words (read directly, no host round trip)
+struct CntPtrs {
+    const int* p[kMaxDivRanks];
+};
 
-// rank prefix of the gathered counts (cnt[2q] = rank q's events) in LDS; block 0 publishes the total
-__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const int* cnt, int nr, long long* s_off) {
+// rank prefix of the gathered counts in LDS; block 0 publishes the total
+__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const CntPtrs& cp, int nr, long long* s_off) {
     if (threadIdx.x == 0) {
         long long run = 0;
         for (int q = 0; q < nr; ++q) {
             s_off[q] = run;
-            run += cnt[2 * q];
+            run += __hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         s_off[nr] = run;
         if (blockIdx.x == 0) {
@@ -1376,12 +1401,21 @@ __device__ __forceinline__ const EvRec* rank_ev(const EvRec* ev, long long strid
     return ev + q * stride + (E - s_off[q]);
 }
 
-// k_ct_count / k_ct_scatter over the gathered events of all ranks (same node terms, same sums)
-__global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long stride, const int* cnt_all, int nr,
-                             int* cnt, int* touched, int* tpos, int tsel) {
+// (block 0 also poisons step pstep when any rank's buffers overflowed: every rank sees the same
+// words, so every rank poisons the same step)
+__global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long stride, CntPtrs cp, int nr, int* cnt,
+                             int* touched, int* tpos, int tsel, int* poison, int pstep) {
     __shared__ long long s_off[kMaxDivRanks + 1];
     __shared__ unsigned s_app[2];
-    const long long n = 4 * rank_prefix(ctl, cnt_all, nr, s_off);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        bool over = false;
+        for (int q = 0; q < nr; ++q) over |= __hip_atomic_load(cp.p[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        if (over && poison[0] == 0) {
+            poison[1] = pstep;
+            poison[0] = 1;
+        }
+    }
+    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
@@ -1398,11 +1432,11 @@ __global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long strid
     }
 }
 
-__global__ void k_ct_scatter_g(const EvRec* ev, long long stride, const int* cnt_all, int nr, unsigned int* ctl,
+__global__ void k_ct_scatter_g(const EvRec* ev, long long stride, CntPtrs cp, int nr, unsigned int* ctl,
                                const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
     __shared__ long long s_off[kMaxDivRanks + 1];
-    const long long n = 4 * rank_prefix(ctl, cnt_all, nr, s_off);
+    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
         const EvRec* r = rank_ev(ev, stride, s_off, nr, e >> 2);
@@ -1420,6 +1454,23 @@ __global__ void k_ct_scatter_g(const EvRec* ev, long long stride, const int* cnt
             o[2] = -r->f[2] / 3.0;
         }
     }
+}
+
+// in-process group: every peer's packed events (count read on the device) into rank q's stride
+// slot of dst, one row of workgroups per peer; 40-B records as five 8-B words
+struct PeerEv {
+    const EvRec* src[kMaxDivRanks];
+    const int* cnt[kMaxDivRanks];
+};
+
+__global__ void k_ev_gather_peers(PeerEv pe, long long stride, EvRec* dst) {
+    const int q = (int)blockIdx.y;
+    const long long n = min((long long)__hip_atomic_load(pe.cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), stride);
+    const unsigned long long* a = reinterpret_cast<const unsigned long long*>(pe.src[q]);
+    unsigned long long* b = reinterpret_cast<unsigned long long*>(dst + q * stride);
+    static_assert(sizeof(EvRec) == 40, "EvRec: five 8-B words");
+    for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < 5 * n; w += (long long)gridDim.x * blockDim.x)
+        b[w] = a[w];
 }
 
 // ---- multi-GPU mirror (see hkc::Mirror) -----------------------------------------------------
@@ -1631,31 +1682,6 @@ __global__ void k_x1_unpack(const char* recv, size_t blk, int nranks, X1Slots S,
     if (full) {
         const double* v = reinterpret_cast<const double*>(recv + (size_t)q * blk + off_x1v0) + 3 * o;
         for (int c = 0; c < 3; ++c) gvelo0[3 * g + c] = v[c];
-    }
-}
-
-// the local external force follows the global one on the touched nodes this rank holds: the
-// previous step's back to 0 (after k_ct_reset), this step's copied (after k_ct_sum)
-__global__ void k_mir_fext_zero(const unsigned int* ctl, int sel, const int* touched, const int* g2l, double* fext) {
-    const int nt = (int)ctl[kTouched + sel];
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
-        const long long l = g2l[touched[q]];
-        if (l < 0) continue;
-        fext[3 * l] = 0.0;
-        fext[3 * l + 1] = 0.0;
-        fext[3 * l + 2] = 0.0;
-    }
-}
-
-__global__ void k_mir_fext_copy(const unsigned int* ctl, int sel, const int* touched, const int* g2l,
-                                const double* gfext, double* fext) {
-    const int nt = (int)ctl[kTouched + sel];
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nt; q += gridDim.x * blockDim.x) {
-        const long long n = touched[q], l = g2l[n];
-        if (l < 0) continue;
-        fext[3 * l] = gfext[3 * n];
-        fext[3 * l + 1] = gfext[3 * n + 1];
-        fext[3 * l + 2] = gfext[3 * n + 2];
     }
 }
 
@@ -2047,10 +2073,8 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
         C->last_t = in.t;
     } else {
         hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
-                           C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext);
-        if (M)
-            hipLaunchKernelGGL(k_mir_fext_zero, dim3(64), dim3(kB), 0, s, C->d_ctl, 1 - tsel, C->d_touched[1 - tsel],
-                               M->d_g2l, c->d_fext);
+                           C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext,
+                           M ? M->d_g2l : nullptr, M ? c->d_fext : nullptr);
         C->force_rebuild = false;
         C->last_t = in.t;
         if (C->ntile > 0) {
@@ -2084,8 +2108,8 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     const bool fused_mid = fused && C->nseg > 0 && C->nseg <= kSmallThreads && C->n_tri > 0 && C->htot + 1 <= kSmallScan;
     if (C->nseg > 0) {
         const Seg* sg = (const Seg*)C->d_seg;
-        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_seg);
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_box), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_box);
         if (fused_mid) {
             const int nbin = C->nseg * C->g_seg;
             hipLaunchKernelGGL(k_ct_binfilter, dim3((unsigned)nbin + gfilt), dim3(kB), 0, s, in, sg, C->d_reg,
@@ -2124,10 +2148,8 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     const unsigned ge = (unsigned)C->g_ev;
     if (div) {  // pack this rank's events; the exchange and the sums are phase B
         hipLaunchKernelGGL(k_ev_pack, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt, M->d_x1ctl);
+                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt + 2 * (in.t & 1), M->d_x1ctl);
         HIPCHK(hipGetLastError());
-        if (!comm_is_rccl(c))  // in-process peers read the count from pinned memory
-            HIPCHK(hipMemcpyAsync(M->h_evcnt + 2 * M->nranks, M->d_evcnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(M->ev_evpacked, s));
         M->div_t = in.t;
         ++M->div_seq;
@@ -2150,10 +2172,7 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, fext);
-    if (M)
-        hipLaunchKernelGGL(k_mir_fext_copy, dim3(64), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], M->d_g2l,
-                           M->g_fext, c->d_fext);
+                       C->d_terms, fext, M ? M->d_g2l : nullptr, M ? c->d_fext : nullptr);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
@@ -2172,69 +2191,68 @@ int contact_step_b(hakai_ctx* c) {
     if (!M || !M->div_step) return 0;
     hipStream_t s = c->stream;
     const int nr = M->nranks;
-    int* h = M->h_evcnt;
+    CntPtrs cp{};
+    const EvRec* ev = nullptr;
+    long long stride = 1;
     if (comm_is_rccl(c)) {
-        if (int rc = comm_allgather_raw(c, M->d_evcnt, M->d_evcnt_all, 2 * sizeof(int))) return rc;
+        // the counts first (8 B per rank), read back to size the event all-gather exactly
+        int* h = M->h_evcnt;
+        if (int rc = comm_allgather_raw(c, M->d_evcnt + 2 * (M->div_t & 1), M->d_evcnt_all, 2 * sizeof(int)))
+            return rc;
         HIPCHK(hipMemcpyAsync(h, M->d_evcnt_all, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-    } else {
-        for (int q = 0; q < nr; ++q) {
-            hakai_ctx* pc = comm_peer_ctx(c, q);
-            Mirror* pm = pc && pc->contact ? pc->contact->mir : nullptr;
-            if (!pm || pm->div_seq != M->div_seq || pm->div_t != M->div_t)
-                return fail(HAKAI_ERR_STATE, "divided contact: rank %d has not searched step %d (step an in-process "
-                            "group with hakai_step_group)", q, M->div_t);
-            HIPCHK(hipEventSynchronize(pm->ev_evpacked));
-            h[2 * q] = pm->h_evcnt[2 * nr];
-            h[2 * q + 1] = pm->h_evcnt[2 * nr + 1];
+        long long mx = 0;
+        for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, h[2 * q]);
+        const size_t need = (size_t)nr * (size_t)std::max<long long>(mx, 1) * sizeof(EvRec);
+        if (need > M->ev_recv_bytes) {
+            HIPCHK(hipStreamSynchronize(s));
+            dfree(M->d_ev_recv);
+            HIPCHK(dalloc(&M->d_ev_recv, need));
+            M->ev_recv_bytes = need;
         }
-        HIPCHK(hipMemcpyAsync(M->d_evcnt_all, h, 2 * nr * sizeof(int), hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));  // h is rewritten by the next step's phase B
-    }
-    long long mx = 0;
-    bool over = false;
-    for (int q = 0; q < nr; ++q) {
-        mx = std::max<long long>(mx, h[2 * q]);
-        over |= h[2 * q + 1] != 0;
-    }
-    if (over)  // the same step on every rank (the counts are the same everywhere)
-        hipLaunchKernelGGL(k_poison_mark, dim3(1), dim3(64), 0, s, c->d_poison, M->div_t);
-    const size_t need = (size_t)nr * (size_t)std::max<long long>(mx, 1) * sizeof(EvRec);
-    if (need > M->ev_recv_bytes) {
-        HIPCHK(hipStreamSynchronize(s));
-        dfree(M->d_ev_recv);
-        HIPCHK(dalloc(&M->d_ev_recv, need));
-        M->ev_recv_bytes = need;
-    }
-    M->ev_stride = std::max<long long>(mx, 1);
-    if (comm_is_rccl(c)) {
+        stride = std::max<long long>(mx, 1);
         if (mx > 0)
             if (int rc = comm_allgather_raw(c, M->d_ev_send[M->div_t & 1], M->d_ev_recv, (size_t)mx * sizeof(EvRec)))
                 return rc;
+        for (int q = 0; q < nr; ++q) cp.p[q] = M->d_evcnt_all + 2 * q;
     } else {
-        LocalGather g{};
+        // in-process group: the peers' counts and events are read on the device after a stream
+        // wait on their phase A (no host round trip); every peer gets a slot of ev_cap records
+        PeerEv pe{};
         for (int q = 0; q < nr; ++q) {
-            Mirror* pm = comm_peer_ctx(c, q)->contact->mir;
+            hakai_ctx* pc = comm_peer_ctx(c, q);
+            Mirror* pm = pc && pc->contact ? pc->contact->mir : nullptr;
+            if (!pm || pm->div_seq != M->div_seq || pm->div_t != M->div_t || pm->ev_cap != M->ev_cap)
+                return fail(HAKAI_ERR_STATE, "divided contact: rank %d has not searched step %d (step an in-process "
+                            "group with hakai_step_group; the same contact_event_cap on every rank)", q, M->div_t);
             if (q != M->rank) HIPCHK(hipStreamWaitEvent(s, pm->ev_evpacked, 0));
-            g.src[q] = (const char*)pm->d_ev_send[M->div_t & 1];
-            g.bytes[q] = (long long)h[2 * q] * (long long)sizeof(EvRec);
-            g.off[q] = (long long)q * M->ev_stride * (long long)sizeof(EvRec);
+            pe.src[q] = (const EvRec*)pm->d_ev_send[M->div_t & 1];
+            pe.cnt[q] = pm->d_evcnt + 2 * (M->div_t & 1);
+            cp.p[q] = pe.cnt[q];
         }
-        if (int rc = gather_local(c, g, nr, M->d_ev_recv)) return rc;
+        stride = std::max<long long>(M->ev_cap, 1);
+        const size_t need = (size_t)nr * (size_t)stride * sizeof(EvRec);
+        if (need > M->ev_recv_bytes) {
+            HIPCHK(hipStreamSynchronize(s));
+            dfree(M->d_ev_recv);
+            HIPCHK(dalloc(&M->d_ev_recv, need));
+            M->ev_recv_bytes = need;
+        }
+        hipLaunchKernelGGL(k_ev_gather_peers, dim3(64, (unsigned)nr), dim3(kB), 0, s, pe, stride,
+                           (EvRec*)M->d_ev_recv);
     }
+    M->ev_stride = stride;
+    ev = (const EvRec*)M->d_ev_recv;
     const int tsel = C->tsel;
     const unsigned ge = (unsigned)C->g_ev;
-    const EvRec* ev = (const EvRec*)M->d_ev_recv;
-    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, ev, M->ev_stride, M->d_evcnt_all, nr, C->d_cnt,
-                       C->d_touched[tsel], C->d_tpos, tsel);
+    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, ev, stride, cp, nr, C->d_cnt,
+                       C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, M->div_t);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
-    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, ev, M->ev_stride, M->d_evcnt_all, nr, C->d_ctl,
-                       C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
+    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, ev, stride, cp, nr, C->d_ctl, C->d_toff, C->d_tpos,
+                       C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, M->g_fext);
-    hipLaunchKernelGGL(k_mir_fext_copy, dim3(64), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], M->d_g2l,
-                       M->g_fext, c->d_fext);
+                       C->d_terms, M->g_fext, M->d_g2l, c->d_fext);
     HIPCHK(hipGetLastError());
     M->div_step = false;
     return 0;
@@ -2526,6 +2544,12 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     std::vector<int> ni_pair, ni_node, ni_orig, ni_aptr{0}, ni_add;
     std::vector<int> nj_pair, nj_node, nj_orig, nj_aptr{0}, nj_add;
     std::vector<int> tri_pair, tri_nodes, tri_ele, tri_adder, seg;
+    struct SegKey {
+        int inst;
+        const void* filt;
+        int adds;
+    };
+    std::vector<SegKey> seg_key;
     // node list of a pair side: initial exterior nodes + nodes exposed by each element's deletion
     auto keep = [](const Inst& I, const std::vector<char>* filt, int f) {
         return !filt || (*filt)[I.faces[f].ele - I.e0];
@@ -2614,8 +2638,16 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
                         tri_adder.push_back(inst[b].e0 + j);
                     }
                 }
-        if (ni_node.size() > ni0) seg.insert(seg.end(), {(int)ni0, (int)ni_node.size(), pr, 0, -1, 0, 0, 0});
-        if (nj_node.size() > nj0) seg.insert(seg.end(), {(int)nj0, (int)nj_node.size(), pr, 1, -1, 0, 0, 0});
+        // a segment's live node set is a function of (instance, face filter, adders or not): equal
+        // keys, equal sets at every step, so one segment's boxes serve both
+        if (ni_node.size() > ni0) {
+            seg.insert(seg.end(), {(int)ni0, (int)ni_node.size(), pr, 0, -1, 0, -1, -1});
+            seg_key.push_back({a, (const void*)ct[pr].fa, 1});
+        }
+        if (nj_node.size() > nj0) {
+            seg.insert(seg.end(), {(int)nj0, (int)nj_node.size(), pr, 1, -1, 0, -1, -1});
+            seg_key.push_back({b, (const void*)ct[pr].fb, self ? 0 : 1});
+        }
         // sized for the initial surface; nodes exposed later share buckets (slower, same result)
         int hs = 64;
         while (hs < 2 * c_i) hs <<= 1;
@@ -2634,6 +2666,17 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     C->n_nj = (int)nj_node.size();
     C->n_tri = (int)tri_ele.size();
     C->nseg = (int)seg.size() / 8;
+    for (int q = 0; q < C->nseg; ++q)  // bounding-box duplicates (Seg::dup / alias)
+        for (int r = 0; r < q; ++r) {
+            const SegKey &x = seg_key[q], &y = seg_key[r];
+            if (seg[8 * r + 5] || x.inst != y.inst || x.filt != y.filt || x.adds != y.adds) continue;
+            int* al = &seg[8 * r + 6];
+            const int k = al[0] < 0 ? 0 : (al[1] < 0 ? 1 : -1);
+            if (k < 0) break;  // r already serves two: q computes its own
+            al[k] = 12 * seg[8 * q + 2] + 6 * seg[8 * q + 3];
+            seg[8 * q + 5] = 1;
+            break;
+        }
     // fused small-deck phases: one 1024-thread workgroup scans the deletion steps, the bucket table
     // and the i-node entries a few times at most
     C->small = C->nE <= (1 << 16) && C->n_ni <= (1 << 16) && C->htot + 1 <= kSmallScan;
@@ -2653,6 +2696,7 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         }
         for (int q = 0; q < C->nseg; ++q) maxseg = std::max<long long>(maxseg, seg[8 * q + 1] - seg[8 * q]);
         C->g_seg = clampi((maxseg + kB - 1) / kB, 1, kSegBlocks);
+        C->g_box = clampi((maxseg + 16 * kB - 1) / (16 * kB), 1, 32);
         C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
         // >= 64 waves (every event shard); one pass over every live triangle as a candidate (32
         // lanes each) up to the 4096-block cap -- small self-contact decks keep half their triangles
@@ -2965,7 +3009,7 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     // divided search: this rank's events of a step (up to the event buffer), the counts
     M->ev_cap = C->cap;
     for (auto& p : M->d_ev_send) HIPCHK(hipMalloc(&p, (size_t)M->ev_cap * sizeof(EvRec)));
-    HIPCHK(dalloc(&M->d_evcnt, 2));
+    HIPCHK(dalloc(&M->d_evcnt, 4));
     HIPCHK(dalloc(&M->d_evcnt_all, 2 * (size_t)nr));
     HIPCHK(hipHostMalloc((void**)&M->h_evcnt, (2 * (size_t)nr + 2) * sizeof(int), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&M->ev_evpacked, hipEventDisableTiming));
