@@ -249,6 +249,9 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.variant = c->elem_variant;
     // nEp / 32 = batches of 32 elements (kEPB); small meshes take the one-batch-per-block kernel
     ea.pipe_blocks = (c->nEp / 32 >= (long long)c->pipe_min * c->pipe_blocks) ? c->pipe_blocks : 0;
+    // the reference-order arithmetic keeps ~50 more live registers: its pipelined form spills and
+    // runs slower than the one-batch kernel (C3: 1.49 vs 1.29 ms, profiles/r02_exact_kernel_variants.log)
+    if (c->elem_exact && !c->exact_pipe) ea.pipe_blocks = 0;
     ea.pipe_map = c->pipe_map;
     ea.gp_nt = c->gp_nt;
     ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
@@ -1120,6 +1123,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "fuse_bc")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fuse_bc must be 0 or 1");
         c->fuse_bc = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "elem_exact_pipe")) {  // 1: the persistent pipelined kernel in elem_exact mode too
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact_pipe must be 0 or 1");
+        c->exact_pipe = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_pipe_min")) {

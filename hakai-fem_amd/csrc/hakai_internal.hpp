@@ -70,6 +70,7 @@ struct hakai_ctx {
     int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
     int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
     int elem_exact = 0;          // tuning "elem_exact": reference-order element arithmetic
+    int exact_pipe = 0;          // tuning "elem_exact_pipe": the persistent kernel in elem_exact mode (default: one-batch)
     int group_serial = 0;        // tuning "group_serial" (rank 0 of a hakai_step_group): drain every rank's
                                  // phase before the next rank's (per-rank timings without the ranks
                                  // sharing the one GPU)

@@ -167,6 +167,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       trajectories bit-identical to the reference's expression order; the mode
  *                       hakai_run_inp uses), 0 (default for hakai_step): fused single-pass element
  *                       kernel (rounding-level differences); env HAKAI_ELEM_EXACT sets the default;
+ *   "elem_exact_pipe"   1: elem_exact mode also uses the persistent kernel (default 0: one batch
+ *                       per block, faster for the reference-order arithmetic);
  *   "elem_pipe_blocks"  >0: persistent software-pipelined element kernel on that many blocks
  *                       (default 512); 0: one batch of 32 elements per block;
  *   "elem_pipe_min"     persistent kernel only with >= this many batches per block (default 2);

@@ -79,6 +79,7 @@ def test_exact_bar_with_deletion_bitexact(pipe_min):
     assert len(o.deletions) > 0
     with Solver(m) as sv:
         sv.set_tuning("elem_exact", 1)
+        sv.set_tuning("elem_exact_pipe", 1)
         sv.set_tuning("elem_pipe_min", pipe_min)
         sv.step(1, 1000)
         sv.step(1001, m.n_steps - 1000)
@@ -95,6 +96,7 @@ def test_exact_elastic_bar_bitexact():
     o.run(1, m.n_steps)
     with Solver(m) as sv:
         sv.set_tuning("elem_exact", 1)
+        sv.set_tuning("elem_exact_pipe", 1)
         sv.set_tuning("elem_pipe_min", 0)
         sv.step(1, m.n_steps)
         g = sv.download()
