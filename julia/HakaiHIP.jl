@@ -258,6 +258,9 @@ function comm_unique_id()
 end
 comm_init(c::Ctx, rank, nranks, id::Vector{UInt8}) =
     check(ccall((:hakai_comm_init, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{UInt8}), c.p, rank, nranks, id))
+# an in-process group of contexts on one device (rank r of n, same key on every member)
+comm_init_local(c::Ctx, rank, nranks, key) =
+    check(ccall((:hakai_comm_init_local, lib), Cint, (Ptr{Cvoid}, Cint, Cint, Int64), c.p, rank, nranks, key))
 set_interface(c::Ctx, local_node::Vector{Int64}, rank_lo::Vector{Int32}, rank_hi::Vector{Int32}) =
     check(ccall((:hakai_set_interface, lib), Cint, (Ptr{Cvoid}, Int64, Ptr{Int64}, Ptr{Int32}, Ptr{Int32}),
                 c.p, length(local_node), local_node, rank_lo, rank_hi))
