@@ -134,6 +134,13 @@ struct Mirror {
     long long div_seq = 0;            // divided phase A calls (equal on the ranks of a lockstep group)
 };
 
+// A hash-bucket entry: the i-node's cell and node id, written by the fill so the triangle search
+// reads one 32-B record per entry instead of an index and then its cell and node.
+struct BEnt {
+    long long m[3];
+    int node, pad;
+};
+
 struct Contact {
     // node / element space of the kernels: the context's own (one GPU) or the global mirror
     long long nN = 0, nE = 0;
@@ -173,8 +180,9 @@ struct Contact {
                      // 6 bounds, so fewer, longer blocks: ~16 entries per thread)
     // hash grid over i-nodes
     int htot = 0;
-    int *d_bcnt = nullptr, *d_boff = nullptr, *d_blist = nullptr, *d_qbucket = nullptr;
-    long long* d_ni_map = nullptr;
+    int *d_bcnt = nullptr, *d_boff = nullptr, *d_qbucket = nullptr;
+    BEnt* d_blist = nullptr;
+    BEnt* d_qrec = nullptr;  // [n_ni] by live-list position: the binned i-node's cell and node (bin -> fill)
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
     // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
     bool small = false;
@@ -215,6 +223,7 @@ namespace {
 
 using hkc::Contact;
 using hkc::PairParam;
+using hkc::BEnt;
 
 constexpr int kB = 256;
 
@@ -634,7 +643,7 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
 // vb = virtual block (segment vb / sb, part vb % sb); a launch of nseg * sb workgroups has one each
 __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* segs, const int* reg, const int* ni_live,
                                          const int* ni_pair, const int* ni_node, const PairParam* par,
-                                         const unsigned long long* bbox, int* qbucket, long long* ni_map, int* bcnt,
+                                         const unsigned long long* bbox, int* qbucket, BEnt* qrec, int* bcnt,
                                          int sb) {
 #pragma clang fp contract(off)
     const Seg sg = segs[vb / sb];
@@ -645,20 +654,21 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
         const int k = ni_live[base + q];
         const int pr = ni_pair[k];
         const Range r = pair_range(bbox + 12 * pr);
+        const int nd = ni_node[k];
         double p[3];
-        pos(s, ni_node[k], p);
+        pos(s, nd, p);
         if (r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] || p[1] > r.mx[1] ||
             p[2] > r.mx[2]) {  // the candidate test of :2514-2519, applied before binning
             qbucket[base + q] = -1;
             continue;
         }
         const PairParam pp = par[pr];
-        long long m[3];
-        for (int d = 0; d < 3; ++d) {
-            m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
-            ni_map[3 * (long long)k + d] = m[d];
-        }
-        const int b = pp.hash_off + (int)(hash3(m[0], m[1], m[2]) & (unsigned)(pp.hash_size - 1));
+        BEnt e;
+        for (int d = 0; d < 3; ++d) e.m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
+        e.node = nd;
+        e.pad = 0;
+        qrec[base + q] = e;  // coalesced by live position; the fill moves it into the bucket list
+        const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
         qbucket[base + q] = b;
         atomicAdd(&bcnt[b], 1);
     }
@@ -666,9 +676,9 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
 
 __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                const int* ni_pair, const int* ni_node, const PairParam* par,
-                                               const unsigned long long* bbox, int* qbucket, long long* ni_map,
+                                               const unsigned long long* bbox, int* qbucket, BEnt* qrec,
                                                int* bcnt, int sb) {
-    bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, ni_map, bcnt, sb);
+    bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
 }
 
 // Exclusive scan of the bucket counts for small bucket tables (n <= kSmallScan): one block of
@@ -710,7 +720,8 @@ __device__ __forceinline__ void scan_small_body(const int* in, int* out, int n) 
 __global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) { scan_small_body(in, out, n); }
 
 __device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* reg, const int* ni_live,
-                                          const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
+                                          const int* qbucket, const int* boff, int* bcnt, BEnt* blist, int sb,
+                                          const BEnt* qrec) {
     const Seg sg = segs[vb / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
@@ -719,13 +730,14 @@ __device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* re
         const int b = qbucket[base + q];
         if (b < 0) continue;
         const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-        blist[slot] = ni_live[base + q];
+        blist[slot] = qrec[base + q];
     }
 }
 
 __global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* qbucket, const int* boff, int* bcnt, int* blist, int sb) {
-    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, sb);
+                                                const int* qbucket, const int* boff, int* bcnt, BEnt* blist, int sb,
+                                                const BEnt* qrec) {
+    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, sb, qrec);
 }
 
 // wave-aggregated append: one atomic per wave; every lane of the wave must call it
@@ -801,7 +813,8 @@ __device__ __forceinline__ long long shard_slot(const unsigned* s_pre, long long
 struct TriRec {
     double q0[3], c[3], Rmax, n[3], vdet, im[9], kk;
     long long mj[3];
-    int j0, j1, j2, eleid, pr, pad;
+    int j0, j1, j2, eleid, pr;
+    int hoff, hmask, self;  // the pair's hash region and self-contact flag (no parameter load in the search)
 };
 
 __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const Range& r, const PairParam& pp,
@@ -854,7 +867,9 @@ __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const R
     T.j2 = tri_nodes[3 * j + 2];
     T.eleid = tri_ele[j];
     T.pr = pr;
-    T.pad = 0;
+    T.hoff = pp.hash_off;
+    T.hmask = pp.hash_size - 1;
+    T.self = pp.self ? 1 : 0;
 }
 
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
@@ -935,19 +950,17 @@ __device__ __forceinline__ void ev_write(int* ev_nodes, double* ev_f, long long 
 // one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
 // i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
-                                         int b, const PairParam* par, const int* boff, const int* blist,
-                                         const int* ni_node, const long long* ni_map, double d_lim, double myu,
+                                         int b, const PairParam* par, const int* boff, const BEnt* blist,
+                                         double d_lim, double myu,
                                          unsigned int* evn, long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
 #pragma clang fp contract(off)
     const int pr = rec->pr;
     const int sl0 = boff[b], sl1 = boff[b + 1];
     for (int sl = sl0; sl < sl1; ++sl) {
-        const int k = blist[sl];
-        const long long* mk = ni_map + 3 * (long long)k;
-        if (llabs(mj[0] - mk[0]) > 1 || llabs(mj[1] - mk[1]) > 1 || llabs(mj[2] - mk[2]) > 1) continue;
-        const int i = ni_node[k];
-        const PairParam pp = par[pr];
-        if (pp.self) {
+        const BEnt be = blist[sl];
+        if (llabs(mj[0] - be.m[0]) > 1 || llabs(mj[1] - be.m[1]) > 1 || llabs(mj[2] - be.m[2]) > 1) continue;
+        const int i = be.node;
+        if (rec->self) {
             bool own = false;
             for (int a = 0; a < 8; ++a) own |= (i == s.conn[8 * (long long)rec->eleid + a]);
             if (own) continue;
@@ -987,7 +1000,7 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
         const double F = kk * d;
         double fx = F * nx, fy = F * ny, fz = F * nz;
         // damping: diag_M[i] indexes the dof vector with a node id (:2592)
-        const double Cd = 2 * sqrt(s.mass[(i) / 3] * kk) * pp.Cr;
+        const double Cd = 2 * sqrt(s.mass[(i) / 3] * kk) * par[pr].Cr;
         const double fc_x = -Cd * vx, fc_y = -Cd * vy, fc_z = -Cd * vz;
         const double dot_ve_n = vex * nx + vey * ny + vez * nz;
         const double vsx = vex - dot_ve_n * nx, vsy = vey - dot_ve_n * ny, vsz = vez - dot_ve_n * nz;
@@ -1018,10 +1031,9 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
 // 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
 __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
                                                 const TriRec* cand, long long cshard_cap,
-                                                const PairParam* par, const int* boff, const int* blist,
-                                                const int* ni_node, const long long* ni_map, double d_lim,
-                                                double myu, unsigned int* evs, long long shard_cap, int* ev_nodes,
-                                                double* ev_f) {
+                                                const PairParam* par, const int* boff, const BEnt* blist,
+                                                double d_lim, double myu, unsigned int* evs, long long shard_cap,
+                                                int* ev_nodes, double* ev_f) {
     __shared__ unsigned s_cpre[kCandShards + 4];
     const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
@@ -1050,13 +1062,12 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
         unsigned hb = 0x80000000u | (unsigned)lane;  // never equal to a real bucket (< 2^31)
         int hoff = 0;
         if (valid) {
-            const int pr = rec->pr;
-            hoff = par[pr].hash_off;
+            hoff = rec->hoff;
             mj[0] = rec->mj[0];
             mj[1] = rec->mj[1];
             mj[2] = rec->mj[2];
             hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
-                 (unsigned)(par[pr].hash_size - 1);
+                 (unsigned)rec->hmask;
         }
         bool dup = false;
         const int half = lane & 32;
@@ -1067,8 +1078,7 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
             dup |= c2 < cell && (half ? hi : lo) == hb;
         }
         if (valid && !dup)
-            tri_cell(s, rec, mj, hoff + (int)hb, par, boff, blist, ni_node, ni_map, d_lim, myu, evn, shard_cap,
-                     sh_nodes, sh_f, eb);
+            tri_cell(s, rec, mj, hoff + (int)hb, par, boff, blist, d_lim, myu, evn, shard_cap, sh_nodes, sh_f, eb);
         const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
         int x = c;  // wave inclusive scan of the buffered counts
         for (int o = 1; o < 64; o <<= 1) {
@@ -1237,9 +1247,9 @@ __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, 
 // The reference's own decks have a few thousand contact entries and tens of events per step, so
 // the ~13 launches of a contact step (each >= ~2.4 us from a graph, tools/barrier_probe.hip) cost
 // more than their work. For models small at setup (Contact::small) the step runs the prologue
-// (reset, deletion scan, surface append), the bucket scan + fill, and the event gather (count,
-// alloc, scatter, sum) each as ONE 1024-thread workgroup, the bodies separated by workgroup
-// barriers; the binning and the triangle prefilter share one launch. Same bodies, same results.
+// (reset, deletion scan, surface append) and the event gather (count, alloc, scatter, sum) each as
+// ONE 1024-thread workgroup, the bodies separated by workgroup barriers; the binning and the
+// triangle prefilter share one launch. Same bodies, same results.
 constexpr int kSmallThreads = 1024;
 
 __global__ __launch_bounds__(kSmallThreads) void k_ct_prologue1(
@@ -1252,61 +1262,6 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_prologue1(
     find_del_body(0, 1, ctl, del_step, nE, t, t_rd, dlist);
     __syncthreads();
     append_body(0, 1, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live);
-}
-
-// the fill over every i-node entry of every pair at once: the segments' live counts are loaded in
-// parallel (one thread each) and prefix-summed in LDS, and each thread finds its entry's segment by
-// binary search (a loop over the segments would chain their latencies; nseg <= kSmallThreads)
-__global__ __launch_bounds__(kSmallThreads) void k_ct_scanfill1(const Seg* segs, int nseg, const int* reg,
-                                                                const int* ni_live, const int* qbucket, int* bcnt,
-                                                                int* boff, int nb1, int* blist) {
-    __shared__ int s_base[kSmallThreads], s_off[kSmallThreads + 1], s_w[kSmallThreads / 64];
-    const int g = (int)threadIdx.x;
-    int cnt = 0, base = 0;
-    if (g < nseg) {
-        const Seg sg = segs[g];
-        if (sg.side == 0) {
-            base = reg[2 * sg.region];
-            cnt = reg[2 * sg.region + 1];
-        }
-    }
-    int total;
-    const int off = block_excl_scan(cnt, s_w, total);
-    s_base[g] = base;
-    s_off[g] = off;
-    if (g == 0) s_off[kSmallThreads] = total;
-    scan_small_body(bcnt, boff, nb1);  // its barriers also publish s_base / s_off
-    __syncthreads();
-    // four entries per thread per pass, their loads and atomics issued together (a plain loop chains
-    // each entry's load -> atomic -> store latency)
-    constexpr int U = 4;
-    for (int q0 = 0; q0 < total; q0 += U * (int)blockDim.x) {
-        int idx[U], b[U], node[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = q0 + u * (int)blockDim.x + g;
-            idx[u] = -1;
-            if (q < total) {
-                int lo = 0, hi = kSmallThreads;  // s_off[lo] <= q < s_off[hi]
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (s_off[mid] <= q) lo = mid; else hi = mid;
-                }
-                idx[u] = s_base[lo] + (q - s_off[lo]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            b[u] = idx[u] >= 0 ? qbucket[idx[u]] : -1;
-            node[u] = idx[u] >= 0 ? ni_live[idx[u]] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (b[u] >= 0) b[u] = boff[b[u]] + atomicSub(&bcnt[b[u]], 1) - 1;  // leaves bcnt zeroed
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (b[u] >= 0) blist[b[u]] = node[u];
-    }
 }
 
 __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl, const unsigned int* evs,
@@ -1328,13 +1283,13 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl,
 // only the pair boxes
 __global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                      const int* ni_pair, const int* ni_node, const PairParam* par,
-                                                     const unsigned long long* bbox, int* qbucket, long long* ni_map,
+                                                     const unsigned long long* bbox, int* qbucket, BEnt* qrec,
                                                      int* bcnt, int sb, int nbin, const int* tri_cnt,
                                                      const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                      const int* tri_ele, unsigned int* ccnt, TriRec* cand,
                                                      long long cshard_cap) {
     if ((int)blockIdx.x < nbin)
-        bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, ni_map, bcnt, sb);
+        bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
     else
         tri_filter_body(blockIdx.x - nbin, gridDim.x - nbin, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par,
                         bbox, ccnt, cand, cshard_cap, 0, 1);
@@ -1837,7 +1792,7 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_el_tri_ptr); dfree(C->d_el_tri); dfree(C->d_el_ni_ptr); dfree(C->d_el_ni); dfree(C->d_el_nj_ptr);
     dfree(C->d_el_nj); dfree(C->d_dlist);
     dfree(C->d_ni_live); dfree(C->d_nj_live); dfree(C->d_tri_live);
-    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_ni_map);
+    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_qrec);
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt);
@@ -2104,37 +2059,37 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
     if (M) M->div_step = div;
     const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
-    // small decks: binning + prefilter in one launch, bucket scan + fill in one workgroup
-    const bool fused_mid = fused && C->nseg > 0 && C->nseg <= kSmallThreads && C->n_tri > 0 && C->htot + 1 <= kSmallScan;
+    // small decks: the binning and the triangle prefilter in one launch (both need only the boxes)
+    const bool fused_mid = fused && C->nseg > 0 && C->n_tri > 0;
+    const Seg* sg = (const Seg*)C->d_seg;
     if (C->nseg > 0) {
-        const Seg* sg = (const Seg*)C->d_seg;
         hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_box), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
                            C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_box);
         if (fused_mid) {
             const int nbin = C->nseg * C->g_seg;
             hipLaunchKernelGGL(k_ct_binfilter, dim3((unsigned)nbin + gfilt), dim3(kB), 0, s, in, sg, C->d_reg,
-                               C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map,
+                               C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_qrec,
                                C->d_bcnt, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
                                C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_ccnt, (TriRec*)C->d_cand,
                                C->cshard_cap);
-            hipLaunchKernelGGL(k_ct_scanfill1, dim3(1), dim3(kSmallThreads), 0, s, sg, C->nseg, C->d_reg,
-                               C->d_ni_live, C->d_qbucket, C->d_bcnt, C->d_boff, (int)(C->htot + 1), C->d_blist);
         } else {
             hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                               C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_ni_map, C->d_bcnt,
+                               C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_qrec, C->d_bcnt,
                                C->g_seg);
         }
     }
-    if (fused_mid) {
-    } else if (C->htot + 1 <= kSmallScan) {
+    // the bucket scan and the fill: one workgroup for tables up to kSmallScan, then a workgroup per
+    // segment part (fusing the fill into the scan's one workgroup was slower on every reference deck:
+    // the fill's scattered atomics and stores want more than one CU)
+    if (C->htot + 1 <= kSmallScan) {
         hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, s, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
     } else {
         size_t tb = C->tmp_bytes;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
     }
-    if (C->nseg > 0 && !fused_mid)
-        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, (const Seg*)C->d_seg, C->d_reg,
-                           C->d_ni_live, C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg);
+    if (C->nseg > 0)
+        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, sg, C->d_reg, C->d_ni_live,
+                           C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg, C->d_qrec);
     if (C->n_tri > 0) {
         if (!fused_mid)
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
@@ -2142,7 +2097,7 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
                                C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
         hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
                            C->cshard_cap,
-                           C->d_par, C->d_boff, C->d_blist, C->d_ni_node, C->d_ni_map, C->d_lim, C->myu, C->d_evs,
+                           C->d_par, C->d_boff, C->d_blist, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
     }
     const unsigned ge = (unsigned)C->g_ev;
@@ -2809,7 +2764,7 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     HIPCHK(dalloc(&C->d_boff, (size_t)C->htot + 1));
     HIPCHK(dalloc(&C->d_blist, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_qbucket, (size_t)C->n_ni));
-    HIPCHK(dalloc(&C->d_ni_map, 3 * (size_t)C->n_ni));
+    HIPCHK(dalloc(&C->d_qrec, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_tile_cnt, (size_t)C->ntile));
     HIPCHK(dalloc(&C->d_tile_off, (size_t)C->ntile + 1));
     HIPCHK(dalloc(&C->d_dlist, (size_t)nE));
