@@ -177,7 +177,7 @@ struct Contact {
     // per-step kernels are not dominated by dispatching idle workgroups); every loop is grid-stride
     int g_seg = 256, g_ev = 1024, g_tri = 4096, g_node = 256, g_del = 1024, g_reset = 64;
     int g_box = 32;  // bounding boxes: blocks per segment (each block ends in 6 atomics on the pair's
-                     // 6 bounds, so fewer, longer blocks: ~16 entries per thread)
+                     // 6 bounds, so fewer, longer blocks: ~4 entries per thread, one unrolled pass)
     // hash grid over i-nodes
     int htot = 0;
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_qbucket = nullptr;
@@ -2651,7 +2651,7 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         }
         for (int q = 0; q < C->nseg; ++q) maxseg = std::max<long long>(maxseg, seg[8 * q + 1] - seg[8 * q]);
         C->g_seg = clampi((maxseg + kB - 1) / kB, 1, kSegBlocks);
-        C->g_box = clampi((maxseg + 16 * kB - 1) / (16 * kB), 1, 32);
+        C->g_box = clampi((maxseg + 4 * kB - 1) / (4 * kB), 1, 128);  // ~4 entries per thread: one unrolled pass
         C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
         // >= 64 waves (every event shard); one pass over every live triangle as a candidate (32
         // lanes each) up to the 4096-block cap -- small self-contact decks keep half their triangles
