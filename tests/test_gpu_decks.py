@@ -141,3 +141,35 @@ def test_charpy_deck_two_ranks_bitexact():
         assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + loc.nElement])
         sv.close()
     assert sorted(dels) == gdel and len(gdel) > 0
+
+
+@pytest.mark.parametrize("name,world", [("car_crash_N2k", 2), ("car_wall_N2k", 3)])
+def test_car_deck_ranks_bitexact(name, world):
+    """The v0.0.2 car decks (multi-instance contact, self-contact on car-wall, mass scaling 100)
+    range-partitioned over an in-process group with the divided contact search and the
+    reference-order element arithmetic: 20 000 steps bit-identical to one context."""
+    z, glob = _deck(name)
+    steps = 20000
+    with Solver(glob) as sv:
+        sv.set_tuning("elem_exact", 1)
+        sv.step(1, steps)
+        g = sv.download()
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_tuning("elem_exact", 1)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, world, 5200 + world)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        svs.append(sv)
+    step_group(svs, 1, steps)
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
+        assert np.array_equal(st.velo.reshape(-1, 3), g.velo.reshape(-1, 3)[l2g - 1])
+        e0 = loc.global_element_offset
+        assert np.array_equal(st.integ_stress, g.integ_stress[8 * e0:8 * (e0 + loc.nElement)])
+        sv.close()
