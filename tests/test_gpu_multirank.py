@@ -366,3 +366,43 @@ def test_contact_group_divided_window_vs_oracle():
         new += [tuple(int(v) for v in x) for x in sv.deleted() if x[0] > t0]
         sv.close()
     assert sorted(new) == sorted(tuple(int(v) for v in x) for x in o.deletions)
+
+
+def test_divided_contact_overflow_poisons_every_rank():
+    """An event-buffer overflow on any rank in the divided search is seen by every rank in the
+    exchanged counts: the same step is poisoned on all of them (device-side, no host round trip),
+    every rank's call fails, and every rank's state is the last good step's."""
+    from hakai import mesh
+    from hakai._abi import HakaiError
+    glob = mesh.two_body_model(plate=(12, 12, 1), impactor=(8, 8, 1), v=-1e5, perturb=0.03, seed=4, n_steps=60)
+    gdiag, _ = glob.lumped_mass()
+
+    def group(cap, key):
+        parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+        svs = []
+        for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+            sv = Solver(loc, diag_M=diag)
+            sv.set_element_offset(loc.global_element_offset)
+            sv.comm_init_local(r, 2, key)
+            sv.set_interface(*iface)
+            sv.set_contact_global(glob, l2g, off, gdiag)
+            sv.set_tuning("contact_event_cap", cap)
+            svs.append(sv)
+        return parts, svs
+
+    parts, svs = group(1, 9191)
+    with pytest.raises(HakaiError) as ei:
+        step_group(svs, 1, glob.n_steps)
+    import re
+    p = int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
+    assert 1 < p < glob.n_steps
+    after = [sv.download() for sv in svs]
+    for sv in svs:
+        sv.close()
+    _, good_svs = group(1 << 12, 9192)
+    step_group(good_svs, 1, p - 1)
+    for a, sv in zip(after, good_svs):
+        g = sv.download()
+        assert np.array_equal(a.disp, g.disp) and np.array_equal(a.velo, g.velo)
+        assert np.array_equal(a.integ_stress, g.integ_stress)
+        sv.close()
