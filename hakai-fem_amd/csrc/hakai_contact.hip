@@ -134,12 +134,17 @@ struct Mirror {
     long long div_seq = 0;            // divided phase A calls (equal on the ranks of a lockstep group)
 };
 
-// A hash-bucket entry: the i-node's cell and node id, written by the fill so the triangle search
-// reads one 32-B record per entry instead of an index and then its cell and node.
-struct BEnt {
+// A hash-bucket entry: the i-node's cell, node id and position (coord + u of this step, the value
+// the triangle test would gather: the same expression, so the same bits), written by the binning
+// and moved into the bucket list by the fill, so the triangle search reads one 64-B record per
+// entry and has no dependent gather of the node's position behind it.
+struct alignas(16) BEnt {
     long long m[3];
     int node, pad;
+    double p[3];
+    double pad2;
 };
+static_assert(sizeof(BEnt) == 64, "BEnt: four 16-B vectors");
 
 struct Contact {
     // node / element space of the kernels: the context's own (one GPU) or the global mirror
@@ -187,6 +192,7 @@ struct Contact {
     // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
     bool small = false;
     int fuse_small = 1;
+    int tri_w64 = 0;  // tuning "contact_tri_wave": one candidate triangle per wave (k_ct_tri64)
 
     // events and per-node gather over the touched nodes
     long long cap = 0;
@@ -667,6 +673,8 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
         for (int d = 0; d < 3; ++d) e.m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
         e.node = nd;
         e.pad = 0;
+        for (int d = 0; d < 3; ++d) e.p[d] = p[d];
+        e.pad2 = 0.0;
         qrec[base + q] = e;  // coalesced by live position; the fill moves it into the bucket list
         const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
         qbucket[base + q] = b;
@@ -947,31 +955,68 @@ __device__ __forceinline__ void ev_write(int* ev_nodes, double* ev_f, long long 
     ef[2] = fz;
 }
 
+// one bucket entry: its four 16-B vectors are issued together and pinned (the asm), so the
+// compiler cannot split the record into per-field loads sunk behind the tests that use them --
+// that made every entry a chain of four dependent round trips
+__device__ __forceinline__ long long ll2(unsigned lo, unsigned hi) {
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ BEnt ld_bent(const BEnt* e) {
+    const uint4* q = reinterpret_cast<const uint4*>(e);
+    const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    asm volatile("" ::"v"(w0.x), "v"(w1.x), "v"(w2.x), "v"(w3.x));
+    BEnt r;
+    r.m[0] = ll2(w0.x, w0.y);
+    r.m[1] = ll2(w0.z, w0.w);
+    r.m[2] = ll2(w1.x, w1.y);
+    r.node = (int)w1.z;
+    r.pad = (int)w1.w;
+    r.p[0] = __longlong_as_double(ll2(w2.x, w2.y));
+    r.p[1] = __longlong_as_double(ll2(w2.z, w2.w));
+    r.p[2] = __longlong_as_double(ll2(w3.x, w3.y));
+    r.pad2 = __longlong_as_double(ll2(w3.z, w3.w));
+    return r;
+}
+
 // one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
 // i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
-                                         int b, const PairParam* par, const int* boff, const BEnt* blist,
-                                         double d_lim, double myu,
+                                         int b, int part, int stride, const PairParam* par, const int* boff,
+                                         const BEnt* __restrict__ blist, double d_lim, double myu,
                                          unsigned int* evn, long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
 #pragma clang fp contract(off)
     const int pr = rec->pr;
     const int sl0 = boff[b], sl1 = boff[b + 1];
-    for (int sl = sl0; sl < sl1; ++sl) {
-        const BEnt be = blist[sl];
-        if (llabs(mj[0] - be.m[0]) > 1 || llabs(mj[1] - be.m[1]) > 1 || llabs(mj[2] - be.m[2]) > 1) continue;
+    // self contact: the triangle's element's own nodes are skipped (:2496-2507); loaded once
+    const bool self = rec->self;
+    int own8[8];
+    if (self) {
+        const int* cn = s.conn + 8 * (long long)rec->eleid;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) own8[a] = cn[a];
+    }
+    // the point-independent part of the test, held in registers for the whole bucket (scalar
+    // registers when the record is wave-uniform, k_ct_tri64)
+    const double c0 = rec->c[0], c1 = rec->c[1], c2 = rec->c[2], Rmax = rec->Rmax;
+    const double q00 = rec->q0[0], q01 = rec->q0[1], q02 = rec->q0[2], vdet = rec->vdet;
+    double im[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) im[k] = rec->im[k];
+    for (int sl = sl0 + part; sl < sl1; sl += stride) {
+        const BEnt be = ld_bent(blist + sl);
         const int i = be.node;
-        if (rec->self) {
-            bool own = false;
-            for (int a = 0; a < 8; ++a) own |= (i == s.conn[8 * (long long)rec->eleid + a]);
-            if (own) continue;
+        // branch-free cell and self tests: no load waits behind a branch
+        bool skip = ((int)(llabs(mj[0] - be.m[0]) > 1) | (int)(llabs(mj[1] - be.m[1]) > 1) |
+                     (int)(llabs(mj[2] - be.m[2]) > 1)) != 0;
+        if (self) {
+#pragma unroll
+            for (int a = 0; a < 8; ++a) skip |= (i == own8[a]);
         }
-        double p[3];
-        pos(s, i, p);
-        const double dpc = my3norm(p[0] - rec->c[0], p[1] - rec->c[1], p[2] - rec->c[2]);
-        if (dpc >= rec->Rmax) continue;
-        const double bx = p[0] - rec->q0[0], by = p[1] - rec->q0[1], bz = p[2] - rec->q0[2];
-        const double* im = rec->im;
-        const double vdet = rec->vdet;
+        if (skip) continue;
+        const double p[3] = {be.p[0], be.p[1], be.p[2]};
+        const double dpc = my3norm(p[0] - c0, p[1] - c1, p[2] - c2);
+        if (dpc >= Rmax) continue;
+        const double bx = p[0] - q00, by = p[1] - q01, bz = p[2] - q02;
         const double x1 = (im[0] * bx + im[1] * by + im[2] * bz) / vdet;
         const double x2 = (im[3] * bx + im[4] * by + im[5] * bz) / vdet;
         const double d = (im[6] * bx + im[7] * by + im[8] * bz) / vdet;
@@ -1028,6 +1073,25 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
     }
 }
 
+// the wave's buffered events -> its event shard, one atomic per wave (every lane calls it)
+__device__ __forceinline__ void ev_flush(const EvBuf& eb, int lane, unsigned int* evn, long long shard_cap,
+                                         int* sh_nodes, double* sh_f) {
+    const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
+    int x = c;  // wave inclusive scan of the buffered counts
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (__builtin_amdgcn_readlane(x, 63) == 0) return;  // wave-uniform: no events
+    unsigned base = 0;
+    if (lane == 63) base = atomicAdd(evn, (unsigned)x);
+    base = __shfl(base, 63) + (unsigned)(x - c);
+#pragma unroll
+    for (int u = 0; u < kEvLocal; ++u)
+        if (u < c && (long long)(base + u) < shard_cap)
+            ev_write(sh_nodes, sh_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+}
+
 // 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
 __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
                                                 const TriRec* cand, long long cshard_cap,
@@ -1078,21 +1142,55 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
             dup |= c2 < cell && (half ? hi : lo) == hb;
         }
         if (valid && !dup)
-            tri_cell(s, rec, mj, hoff + (int)hb, par, boff, blist, d_lim, myu, evn, shard_cap, sh_nodes, sh_f, eb);
-        const int c = eb.n < kEvLocal ? eb.n : kEvLocal;
-        int x = c;  // wave inclusive scan of the buffered counts
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (__builtin_amdgcn_readlane(x, 63) == 0) continue;  // wave-uniform: no events this iteration
-        unsigned base = 0;
-        if (lane == 63) base = atomicAdd(evn, (unsigned)x);
-        base = __shfl(base, 63) + (unsigned)(x - c);
+            tri_cell(s, rec, mj, hoff + (int)hb, 0, 1, par, boff, blist, d_lim, myu, evn, shard_cap, sh_nodes, sh_f,
+                         eb);
+        ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
+    }
+}
+
+// One candidate triangle per WAVE: the record address is wave-uniform (scalar loads, no VGPRs for
+// the triangle's constants), lane c and lane 32 + c both take cell c and split its bucket (even /
+// odd entries), so a wave's longest serial chain is half a bucket. The events are the same set
+// as k_ct_tri's (their order in the shards differs; the per-node sums do not depend on it).
+__global__ __launch_bounds__(128) void k_ct_tri64(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
+                                                  const TriRec* __restrict__ cand, long long cshard_cap,
+                                                  const PairParam* par, const int* boff, const BEnt* blist,
+                                                  double d_lim, double myu, unsigned int* evs, long long shard_cap,
+                                                  int* ev_nodes, double* ev_f) {
+    __shared__ unsigned s_cpre[kCandShards + 4];
+    const long long nt = shard_scan(ccnt, cshard_cap, s_cpre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl[kNcand] = s_cpre[kCandShards + 2];
+        atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
+        atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
+        ctl[kCandOver] = s_cpre[kCandShards + 1];
+    }
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wpb = (int)(blockDim.x >> 6);
+    const int shard = (int)(((long long)blockIdx.x * wpb + wv) % kEvShards);
+    unsigned int* evn = evs + shard * kShardStride;
+    int* sh_nodes = ev_nodes + 4 * (long long)shard * shard_cap;
+    double* sh_f = ev_f + 3 * (long long)shard * shard_cap;
+    const int cell = lane & 31, part = lane >> 5;
+    const bool valid = cell < 27;
+    for (long long t = (long long)blockIdx.x * wpb + wv; t < nt; t += (long long)gridDim.x * wpb) {
+        EvBuf eb;
+        eb.n = 0;
+        eb.j0 = eb.j1 = eb.j2 = 0;
+        const TriRec* rec = cand + shard_slot(s_cpre, cshard_cap, t);
+        const long long mj[3] = {rec->mj[0], rec->mj[1], rec->mj[2]};
+        unsigned hb = 0x80000000u | (unsigned)lane;
+        if (valid)
+            hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
+                 (unsigned)rec->hmask;
+        bool dup = false;
 #pragma unroll
-        for (int u = 0; u < kEvLocal; ++u)
-            if (u < c && (long long)(base + u) < shard_cap)
-                ev_write(sh_nodes, sh_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
+        for (int c2 = 0; c2 < 26; ++c2) dup |= c2 < cell && (unsigned)__builtin_amdgcn_readlane((int)hb, c2) == hb;
+        if (valid && !dup)
+            tri_cell(s, rec, mj, rec->hoff + (int)hb, part, 2, par, boff, blist, d_lim, myu, evn, shard_cap,
+                         sh_nodes, sh_f, eb);
+        ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
 }
 
@@ -2095,7 +2193,9 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                                C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
                                C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
-        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
+        auto tri = C->tri_w64 ? k_ct_tri64 : k_ct_tri;
+        const int gt = C->tri_w64 ? std::min(2 * C->g_tri, 8192) : C->g_tri;
+        hipLaunchKernelGGL(tri, dim3(gt), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
                            C->cshard_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
@@ -2259,6 +2359,12 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     if (!std::strcmp(key, "contact_fuse_small")) {  // small decks: fused single-workgroup phases
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_small must be 0 or 1");
         C->fuse_small = (int)value;
+        graph_invalidate(c);
+        return 0;
+    }
+    if (!std::strcmp(key, "contact_tri_wave")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_tri_wave must be 0 or 1");
+        C->tri_w64 = (int)value;
         graph_invalidate(c);
         return 0;
     }

@@ -185,6 +185,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
  *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy;
  *   "contact_divide"    multi-GPU contact: 1 (default) divided search, 0 replicated search;
+ *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
+ *   "contact_tri_wave"  1: one wave per candidate triangle in the triangle test (default 0: 32 lanes);
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0). */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);

@@ -29,7 +29,9 @@ def main():
     ap.add_argument("--serial", type=int, default=1,
                     help="multi-rank: drain each rank's phase before the next rank's (tuning group_serial), so "
                          "the per-rank kernel timings are not inflated by the ranks sharing this one GPU")
+    ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_tri_wave=1")
     a = ap.parse_args()
+    a.tuning = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in a.tuning.split(",") if kv]
     if a.ranks > 1:
         return group(a)
     import numpy as np
@@ -40,6 +42,8 @@ def main():
     m = mesh.config_c4(a.scale)
     t1 = time.time()
     sv = Solver(m)
+    for k, v in a.tuning:
+        sv.set_tuning(k, v)
     t2 = time.time()
     pairs, sizes = sv.contact_info()
     sv.step(1, a.preload)
@@ -59,7 +63,8 @@ def main():
     st = sv.download(element_flag=True)
     n_active = int(st.element_flag.sum())
     out = {
-        "workload": f"C4 two-body impact, scale 1/{a.scale}", "elements": m.nElement, "nodes": m.nNode,
+        "workload": f"C4 two-body impact, scale 1/{a.scale}", "tuning": dict(a.tuning),
+        "elements": m.nElement, "nodes": m.nNode,
         "pairs": pairs, "element_size": sizes, "steps": a.steps, "preload": a.preload,
         "value_M_element_updates_per_s": round(n_active * a.steps / el / 1e6, 3),
         "ms_per_step": round(el / a.steps * 1e3, 4),
@@ -93,6 +98,8 @@ def group(a):
         sv.set_contact_global(m, l2g, off, gdiag)
         sv.set_tuning("contact_divide", a.divide)
         sv.set_tuning("group_serial", a.serial)
+        for k, v in a.tuning:
+            sv.set_tuning(k, v)
         svs.append(sv)
     t1 = time.time()
     step_group(svs, 1, a.preload)
