@@ -153,19 +153,23 @@ def main():
     import torch
     import torch.distributed as dist
     from hakai._abi import K_ELEMENT, K_EXCHANGE, K_NODAL, K_BC
+    from hakai.dist import rank_device
     from hakai.solver import Solver, comm_unique_id, step_group
     R = a.local_ranks if a.local_ranks > 1 else 0
     if R and world > 1:
         raise SystemExit("--local-ranks is a one-process rehearsal")
     nparts = R or world                      # subdomains of the workload
     multi = world > 1 or a.dist_path
+    device = 0
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29571")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal) the ranks share them
+        device = rank_device(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+        torch.cuda.set_device(device)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     # this process's subdomains: one per rank, or R in-process ranks on one device
     ids = list(range(R)) if R else [rank]
     built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong) for r in ids]
@@ -173,7 +177,7 @@ def main():
     preload = built[0][4] if a.preload < 0 else a.preload
     svs = []
     for r, (model, diag, iface, _, _) in zip(ids, built):
-        sv = Solver(model, device=local_rank if multi else 0, diag_M=diag)
+        sv = Solver(model, device=device, diag_M=diag)
         # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region is
         # stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
         sv.set_tuning("graph", 0)

@@ -229,8 +229,9 @@ def main(argv=None):
     import torch
     import torch.distributed as tdist
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = _dist.rank_device(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+    torch.cuda.set_device(device)
+    tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
     try:
         hakai_multi(argv[0], argv[1] if len(argv) > 1 else "temp", verbose=True)
     finally:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""The N-GPU driver (python -m hakai.run under torch.distributed.run) at world size 1 on the GPU box
-(RCCL refuses two ranks on one device): writes a contact deck with deletions, runs the one-GPU
-driver (hakai.hakai) and the torchrun driver, and compares their VTK files byte for byte."""
+"""The N-GPU driver (python -m hakai.run under torch.distributed.run, --nproc ranks; on a one-GPU box
+the ranks share the device and RCCL connects them over loopback, hakai.dist.rank_device): writes a
+contact deck with deletions, runs the one-GPU driver (hakai.hakai) and the torchrun driver, and
+compares their VTK files byte for byte."""
 import os
 import subprocess
 import sys
@@ -12,6 +13,10 @@ sys.path[:0] = [os.path.join(ROOT, "hakai-fem_amd"), os.path.join(ROOT, "tests")
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nproc", type=int, default=2)
+    args = ap.parse_args()
     import hakai
     from hakai import mesh
     from inp_writer import write_inp
@@ -20,7 +25,7 @@ def main():
     deck = write_inp(os.path.join(tmp, "impact.inp"), m)
     hakai.hakai(deck, os.path.join(tmp, "one"), verbose=False)
     env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "hakai-fem_amd") + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.nproc),
                         "--master-addr", "127.0.0.1", "--master-port", "29561", "-m", "hakai.run", deck,
                         os.path.join(tmp, "multi")], env=env, capture_output=True, text=True, timeout=300)
     print(r.stdout[-2000:], r.stderr[-2000:])
@@ -29,7 +34,7 @@ def main():
     a, b = sorted(os.listdir(os.path.join(tmp, "one"))), sorted(os.listdir(os.path.join(tmp, "multi")))
     same = a == b and all(open(os.path.join(tmp, "one", f), "rb").read() == open(os.path.join(tmp, "multi", f), "rb").read()
                           for f in a)
-    print(f"torchrun driver (world 1) vs one-GPU driver: {len(a)} files, byte-identical: {same}")
+    print(f"torchrun driver (world {args.nproc}) vs one-GPU driver: {len(a)} files, byte-identical: {same}")
     return 0 if same else 1
 
 

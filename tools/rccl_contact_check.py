@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """RCCL check of the multi-GPU contact path (hakai_set_contact_global over hakai_comm_init): 2 ranks
-(both on device 0 when only one GPU is visible), a range-partitioned two-body impact with contact
+(both on device 0 when only one GPU is visible: hakai.dist.rank_device makes them separate hosts to
+RCCL, which then runs its socket transport over loopback), a range-partitioned two-body impact with contact
 deletions, the divided contact search (events all-gathered with ncclAllGather, exact sizes) and the
 replicated one, each compared bit for bit with a single-context run. Launch:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \\
@@ -18,12 +19,12 @@ def main():
     import torch
     import torch.distributed as dist
     from hakai import dist as hdist
-    from hakai import device_count, mesh
+    from hakai import mesh
     from hakai.solver import Solver, comm_unique_id
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = hdist.rank_device(int(os.environ.get("LOCAL_RANK", rank)), int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     dist.init_process_group("gloo")
-    dev = rank % max(device_count(), 1)
     glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
     gdiag, _ = glob.lumped_mass()
     loc, diag, iface, l2g, off = hdist.range_partition(glob, rank, world, gdiag)
