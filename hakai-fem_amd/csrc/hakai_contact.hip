@@ -268,7 +268,15 @@ struct Range {
     bool empty;
 };
 
-__device__ __forceinline__ Range pair_range(const unsigned long long* bb) {
+__device__ __forceinline__ Range pair_range(const unsigned long long* bb_) {
+    // the pair's 12 words as six 16-B loads, all in flight together (bbox + 12 * pair is 16-B aligned)
+    unsigned long long bb[12];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) {
+        const ulonglong2 v = reinterpret_cast<const ulonglong2*>(bb_)[w];
+        bb[2 * w] = v.x;
+        bb[2 * w + 1] = v.y;
+    }
     Range r;
     r.empty = false;
 #pragma unroll
@@ -661,6 +669,7 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
         const int pr = ni_pair[k];
         const Range r = pair_range(bbox + 12 * pr);
         const int nd = ni_node[k];
+        const PairParam pp = par[pr];  // loaded with the box, not behind the range test
         double p[3];
         pos(s, nd, p);
         if (r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] || p[1] > r.mx[1] ||
@@ -668,7 +677,6 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
             qbucket[base + q] = -1;
             continue;
         }
-        const PairParam pp = par[pr];
         BEnt e;
         for (int d = 0; d < 3; ++d) e.m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
         e.node = nd;
@@ -825,9 +833,9 @@ struct TriRec {
     int hoff, hmask, self;  // the pair's hash region and self-contact flag (no parameter load in the search)
 };
 
-__device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const Range& r, const PairParam& pp,
-                                         const int* tri_nodes, const int* tri_ele, const double q0[3],
-                                         const double q1[3], const double q2[3], TriRec& T) {
+__device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam& pp, int nd0, int nd1, int nd2,
+                                         int ele, const double q0[3], const double q1[3], const double q2[3],
+                                         TriRec& T) {
 #pragma clang fp contract(off)
     const double cx = (q0[0] + q1[0] + q2[0]) / 3.0, cy = (q0[1] + q1[1] + q2[1]) / 3.0,
                  cz = (q0[2] + q1[2] + q2[2]) / 3.0;
@@ -870,10 +878,10 @@ __device__ __forceinline__ void tri_geom(const StepIn& s, int j, int pr, const R
     T.n[0] = nx;
     T.n[1] = ny;
     T.n[2] = nz;
-    T.j0 = tri_nodes[3 * j];
-    T.j1 = tri_nodes[3 * j + 1];
-    T.j2 = tri_nodes[3 * j + 2];
-    T.eleid = tri_ele[j];
+    T.j0 = nd0;
+    T.j1 = nd1;
+    T.j2 = nd2;
+    T.eleid = ele;
     T.pr = pr;
     T.hoff = pp.hash_off;
     T.hmask = pp.hash_size - 1;
@@ -892,33 +900,30 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
     __shared__ unsigned s_app[2];
     for (int q0 = bid * blockDim.x; q0 < n; q0 += nb * blockDim.x) {  // block-uniform trip count
         const int q = q0 + (int)threadIdx.x;
-        bool keep = false;
-        int j = 0, pr = 0;
+        // every load unconditional (lanes past the end re-read the last entry), so the chain is
+        // three round trips -- live entry; its element, pair and nodes; flag, pair box, positions
+        // and pair parameters -- instead of one per test
+        const int j = tri_live[q < n ? q : n - 1];
+        const int ele = tri_ele[j], pr = tri_pair[j];
+        const int nd0 = tri_nodes[3 * j], nd1 = tri_nodes[3 * j + 1], nd2 = tri_nodes[3 * j + 2];
+        const int fl = s.flag[ele];
+        const Range r = pair_range(bbox + 12 * pr);
+        const PairParam pp = par[pr];
         double p0[3], p1[3], p2[3];
-        Range r;
-        if (q < n) {
-            j = tri_live[q];
-            keep = (own_n <= 1 || j % own_n == own_r) && s.flag[tri_ele[j]] == 1;  // own triangles only
-            if (keep) {
-                pr = tri_pair[j];
-                r = pair_range(bbox + 12 * pr);
-                keep = !r.empty;
-                if (keep) {
-                    pos(s, tri_nodes[3 * j], p0);
-                    pos(s, tri_nodes[3 * j + 1], p1);
-                    pos(s, tri_nodes[3 * j + 2], p2);
-                    for (int d = 0; d < 3; ++d) {
-                        if (p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]) keep = false;
-                        if (p0[d] > r.mx[d] && p1[d] > r.mx[d] && p2[d] > r.mx[d]) keep = false;
-                    }
-                }
-            }
+        pos(s, nd0, p0);
+        pos(s, nd1, p1);
+        pos(s, nd2, p2);
+        bool keep = q < n && (own_n <= 1 || j % own_n == own_r) && fl == 1 && !r.empty;  // own triangles only
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            keep &= !(p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]);
+            keep &= !(p0[d] > r.mx[d] && p1[d] > r.mx[d] && p2[d] > r.mx[d]);
         }
         const int shard = bid % kCandShards;
         const unsigned slot = block_append(&ccnt[shard * kShardStride], keep, s_app);
         if (keep && (long long)slot < cshard_cap) {
             TriRec T;
-            tri_geom(s, j, pr, r, par[pr], tri_nodes, tri_ele, p0, p1, p2, T);
+            tri_geom(pr, r, pp, nd0, nd1, nd2, ele, p0, p1, p2, T);
             cand[shard * cshard_cap + slot] = T;
         }
     }
