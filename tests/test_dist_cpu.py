@@ -168,3 +168,22 @@ def test_range_partition_two_body():
             assert np.array_equal(ups[r], dns[r + 1])
     with pytest.raises(ValueError):  # a cut that makes ranks 0 and 2 share nodes
         dist.range_partition(mesh.two_body_model(plate=(6, 6, 2), impactor=(3, 3, 3)), 0, 3)
+
+
+def test_rank_device_shares_scarce_gpus(monkeypatch):
+    """One GPU per local rank when there are enough (nothing set); fewer GPUs than local ranks (a
+    one-GPU rehearsal) wrap the ranks around the devices and give each rank its own RCCL host id,
+    so RCCL's duplicate-GPU check does not refuse the communicator."""
+    for k in ("NCCL_HOSTID", "NCCL_SOCKET_IFNAME", "NCCL_IB_DISABLE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert dist.rank_device(5, 8) == 5
+    assert "NCCL_HOSTID" not in os.environ
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert dist.rank_device(3, 4) == 0
+    h3 = os.environ["NCCL_HOSTID"]
+    assert dist.rank_device(2, 4) == 0
+    assert os.environ["NCCL_HOSTID"] != h3 and h3.endswith("rank3")
+    assert os.environ["NCCL_SOCKET_IFNAME"] == "lo"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    assert [dist.rank_device(r, 4) for r in range(4)] == [0, 1, 0, 1]
