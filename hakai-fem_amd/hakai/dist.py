@@ -152,20 +152,24 @@ def slab_partition(glob: Model, rank: int, world: int, nx: int, ny: int):
 
 
 def rank_device(local_rank: int, local_world: int) -> int:
-    """The HIP device of a local rank: one GPU per rank (device = local rank) on a node with enough
-    GPUs. With fewer visible GPUs than local ranks (a one-GPU rehearsal of an N-rank run) the ranks
-    wrap around the devices, and ranks that share a device are made to look like separate hosts to
-    RCCL (NCCL_HOSTID), whose duplicate-GPU check would otherwise refuse the communicator: RCCL then
-    connects them with its socket transport over loopback. The RCCL calls, their order, sizes and
-    buffers are the ones an N-GPU node runs; only the transport and the timings differ. Must run
-    before the first RCCL call of the process (torch's process group or hakai_comm_unique_id)."""
+    """The HIP device of a local rank: device = local rank on a node with a GPU per rank; with fewer
+    visible GPUs than local ranks, local rank mod the visible count (e.g. one visible GPU per process
+    under per-rank HIP_VISIBLE_DEVICES: device 0 of each).
+
+    HAKAI_RCCL_SHARED_GPU=1 (tests and rehearsals only) declares that the ranks really share GPUs,
+    as on the one-GPU test box: RCCL's duplicate-GPU check would refuse such a communicator, so each
+    rank gets its own NCCL_HOSTID, RCCL sees separate hosts and connects them with its socket
+    transport over loopback. The RCCL calls, their order, sizes and buffers are the ones an N-GPU
+    node runs; only the transport and the timings differ. Never set on a production node: it would
+    take xGMI out of the path. Must run before the first RCCL call of the process."""
     import os
     import socket
     import torch
     n = max(torch.cuda.device_count(), 1)  # counts devices without initialising the GPU
     if n >= local_world:
         return local_rank
-    os.environ["NCCL_HOSTID"] = f"{socket.gethostname()}-rank{local_rank}"
-    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    if os.environ.get("HAKAI_RCCL_SHARED_GPU") == "1":
+        os.environ["NCCL_HOSTID"] = f"{socket.gethostname()}-rank{local_rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     return local_rank % n

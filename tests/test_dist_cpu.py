@@ -171,15 +171,17 @@ def test_range_partition_two_body():
 
 
 def test_rank_device_shares_scarce_gpus(monkeypatch):
-    """One GPU per local rank when there are enough (nothing set); fewer GPUs than local ranks (a
-    one-GPU rehearsal) wrap the ranks around the devices and give each rank its own RCCL host id,
-    so RCCL's duplicate-GPU check does not refuse the communicator."""
-    for k in ("NCCL_HOSTID", "NCCL_SOCKET_IFNAME", "NCCL_IB_DISABLE"):
+    """One GPU per local rank when there are enough (nothing set); fewer visible GPUs than local
+    ranks wrap the ranks around the devices, and only HAKAI_RCCL_SHARED_GPU=1 (a one-GPU
+    rehearsal) gives each rank its own RCCL host id, so RCCL's duplicate-GPU check lets them share."""
+    for k in ("NCCL_HOSTID", "NCCL_SOCKET_IFNAME", "NCCL_IB_DISABLE", "HAKAI_RCCL_SHARED_GPU"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     assert dist.rank_device(5, 8) == 5
-    assert "NCCL_HOSTID" not in os.environ
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert dist.rank_device(3, 8) == 0  # e.g. per-rank HIP_VISIBLE_DEVICES: each rank's device 0
+    assert "NCCL_HOSTID" not in os.environ
+    monkeypatch.setenv("HAKAI_RCCL_SHARED_GPU", "1")
     assert dist.rank_device(3, 4) == 0
     h3 = os.environ["NCCL_HOSTID"]
     assert dist.rank_device(2, 4) == 0

@@ -1,9 +1,9 @@
 """RCCL with more than one rank (hakai_comm_init: grouped ncclSend/ncclRecv interface exchange,
 ncclAllReduce / ncclAllGather at setup, the divided contact search's per-step event all-gather),
 one process per rank under torch.distributed.run, against one context bit for bit. On a one-GPU box
-the ranks share the device: hakai.dist.rank_device makes them separate hosts to RCCL, which then
-connects them with its socket transport over loopback -- the same RCCL calls, sizes and buffers as
-on an N-GPU node, another transport."""
+the ranks share the device (HAKAI_RCCL_SHARED_GPU=1: hakai.dist.rank_device makes them separate
+hosts to RCCL, which then connects them with its socket transport over loopback) -- the same RCCL
+calls, sizes and buffers as on an N-GPU node, another transport."""
 import os
 import socket
 import subprocess
@@ -24,10 +24,14 @@ def _port():
     return p
 
 
+def _env():
+    return dict(os.environ, HAKAI_RCCL_SHARED_GPU="1")
+
+
 def _torchrun(script, n, *args, timeout=300):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, script), *args]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=_env())
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     return r.stdout
 
@@ -49,6 +53,6 @@ def test_rccl_contact_bitexact():
 def test_torchrun_driver_writes_the_same_vtk():
     """python -m hakai.run deck.inp over 2 RCCL ranks: 101 VTK files byte-identical to one GPU's."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "driver_torchrun_smoke.py"), "--nproc", "2"],
-                       capture_output=True, text=True, timeout=400, cwd=ROOT)
+                       capture_output=True, text=True, timeout=400, cwd=ROOT, env=_env())
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     assert "byte-identical: True" in r.stdout

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """The N-GPU driver (python -m hakai.run under torch.distributed.run, --nproc ranks; on a one-GPU box
-the ranks share the device and RCCL connects them over loopback, hakai.dist.rank_device): writes a
+the ranks share the device and RCCL connects them over loopback, hakai.dist.rank_device; this
+script sets HAKAI_RCCL_SHARED_GPU=1 for its ranks): writes a
 contact deck with deletions, runs the one-GPU driver (hakai.hakai) and the torchrun driver, and
 compares their VTK files byte for byte."""
 import os
@@ -24,7 +25,7 @@ def main():
     m = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
     deck = write_inp(os.path.join(tmp, "impact.inp"), m)
     hakai.hakai(deck, os.path.join(tmp, "one"), verbose=False)
-    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "hakai-fem_amd") + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    env = dict(os.environ, HAKAI_RCCL_SHARED_GPU="1", PYTHONPATH=os.path.join(ROOT, "hakai-fem_amd") + os.pathsep + os.environ.get("PYTHONPATH", ""))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.nproc),
                         "--master-addr", "127.0.0.1", "--master-port", "29561", "-m", "hakai.run", deck,
                         os.path.join(tmp, "multi")], env=env, capture_output=True, text=True, timeout=300)

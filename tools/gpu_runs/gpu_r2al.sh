@@ -6,6 +6,7 @@
 # and bench.py's N-rank line at N = 2 and 4 (timings meaningless: one GPU, socket transport)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+export HAKAI_RCCL_SHARED_GPU=1  # the ranks share the one GPU (hakai.dist.rank_device)
 mkdir -p gpurun_out
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 timeout -k 10 400 $TR --nproc-per-node 2 --master-port 29534 tools/rccl_contact_check.py > gpurun_out/r2al_rccl_contact.log 2>&1

@@ -3,6 +3,7 @@
 # loopback, hakai.dist.rank_device), each bit-exact against one context on the whole bar
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+export HAKAI_RCCL_SHARED_GPU=1  # the ranks share the one GPU (hakai.dist.rank_device)
 mkdir -p gpurun_out
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 for n in 2 3 4; do

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """RCCL check of the multi-GPU contact path (hakai_set_contact_global over hakai_comm_init): 2 ranks
-(both on device 0 when only one GPU is visible: hakai.dist.rank_device makes them separate hosts to
-RCCL, which then runs its socket transport over loopback), a range-partitioned two-body impact with contact
+(both on device 0 when only one GPU is visible and HAKAI_RCCL_SHARED_GPU=1: hakai.dist.rank_device
+makes them separate hosts to RCCL, which then runs its socket transport over loopback), a range-partitioned two-body impact with contact
 deletions, the divided contact search (events all-gathered with ncclAllGather, exact sizes) and the
 replicated one, each compared bit for bit with a single-context run. Launch:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \\

@@ -3,7 +3,8 @@
 ncclSend/ncclRecv per step, an ncclAllReduce at setup) at any world size: a deleting elastoplastic
 bar split into z-slabs (hakai.dist.slab_partition; middle ranks exchange with both neighbours),
 every rank's final displacements, stresses, flags and deletions compared bit for bit with one
-context on the whole bar. On a one-GPU box the ranks share the device (hakai.dist.rank_device).
+context on the whole bar. On a one-GPU box the ranks share the device (HAKAI_RCCL_SHARED_GPU=1,
+hakai.dist.rank_device).
 Launch:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 \\
       --master-port 29537 tools/rccl_exchange_check.py
