@@ -531,6 +531,7 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     c->h_young.resize((size_t)nMat);
     for (int i = 0; i < nMat; ++i) c->h_young[i] = mats[i].young;
     c->model_ok = true;
+    c->tb_built_mb = -1;  // two-step schedule: rebuilt for this mesh on first use
     c->state_ok = false;
     return hakai_reset_state(c, 0, nullptr, nullptr, 1.0);
 }
@@ -593,7 +594,7 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
     // per-node table: the first resolved entry of each node (entries are sorted by dof, a node's
     // up-to-3 entries are consecutive) or -1, so the nodal kernel applies the BCs itself
     // (hakai_step; 4 B per node)
-    if (!dof.empty() && c->nN <= kFuseBcMaxNodes) {
+    if (!dof.empty()) {  // (used by k_nodal up to kFuseBcMaxNodes, and by the two-step schedule)
         std::vector<int> of((size_t)c->nN, -1);
         for (size_t i = dof.size(); i-- > 0;) of[(size_t)dof[i] / 3] = (int)i;
         HIPCHK(dalloc(&c->d_bc_of_node, of.size()));
@@ -821,6 +822,9 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.nN = c->nN;
     na.dt = d_time;
     na.bc_of_node = nullptr;
+    na.two_step = 0;
+    na.r1_lo = na.r1_hi = na.r2_lo = na.r2_hi = 0;
+    na.ct2 = 0.0;
     hk::BCArgs ba;
     ba.dof = c->d_bc_dof;
     ba.grp = c->d_bc_grp;
@@ -838,7 +842,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.poison = c->d_poison;
     // one GPU, small mesh: the nodal kernel applies the BCs (multi-GPU redoes interface nodes
     // after the nodal kernel, so the BCs must come after that)
-    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm;
+    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm && c->nN <= kFuseBcMaxNodes;
     if (fuse_bc) {
         na.bc_of_node = c->d_bc_of_node;
         na.bc = ba;
@@ -887,6 +891,142 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     if (rc) return rc;
     c->steps_done++;
     c->last_dt = d_time;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-step chunked schedule (tuning "tblock_mb"). Steps s and s+1 are the same computations as two
+// step_once calls, reordered: element chunk it of step s, then the nodes of step s+1 whose incident
+// elements have all finished step s, then the elements of step s+1 whose nodes all have. Every
+// node still sums its incidences in element order and every element runs the same code, so the
+// result is bit-identical to stream mode; the gain is that step s+1 meets its Gauss-point state
+// (stored by step s one chunk earlier), the element forces and the node rows in the 256 MB Infinity
+// Cache. Iteration it launches
+//   nodal:   step s on nodes [A[it], A[it+1])  +  step s+1 on nodes [B[it-1], B[it])
+//   element: step s on batches [E[it], E[it+1]) + step s+1 on batches [D[it-1], D[it])
+// (it = 0..C; missing neighbours are empty ranges). Hazards, for any numbering:
+//  * step s on element e needs u_s of its nodes: they are < A[it+1] (A = 1 + max node of the
+//    elements so far), and overwriting fe_{s-1}(e) is safe because every node of e has gathered;
+//  * step s+1 on node n needs fe_s of every incident element: max incident element < E[it]·32;
+//    it overwrites u_{s-1}(n), which only the (finished) step-s elements around n read;
+//  * step s+1 on element e needs u_{s+1} of its nodes (< B[it]) and its own state_s.
+// Contiguous ranges come from prefix maxima, so a badly numbered mesh only loses the overlap (the
+// whole pair ends up in the last iteration), never correctness.
+static void tblock_build(hakai_ctx* c) {
+    const long long nE = c->nE, nN = c->nN, nb = c->nEp / 32;
+    const long long per_el = 8LL * 8 * (c->any_plastic ? 14 : 12);  // Gauss-point state bytes per element
+    const long long cb = std::max(1LL, ((long long)c->tblock_mb << 20) / per_el / 32);
+    const long long C = (nb + cb - 1) / cb;
+    std::vector<long long> pm_node(nE), pm_inc(nN, -1);  // prefix max of max node per element; of max incident element
+    long long run = -1;
+    for (long long e = 0; e < nE; ++e) {
+        for (int k = 0; k < 8; ++k) {
+            const long long n = c->h_conn[8 * e + k];
+            run = std::max(run, n);
+            pm_inc[n] = std::max(pm_inc[n], e);
+        }
+        pm_node[e] = run;
+    }
+    for (long long n = 1; n < nN; ++n) pm_inc[n] = std::max(pm_inc[n], pm_inc[n - 1]);
+    c->tb_E.assign(C + 1, 0);
+    c->tb_A.assign(C + 1, 0);
+    c->tb_B.assign(C + 1, 0);
+    c->tb_D.assign(C + 1, 0);
+    for (long long it = 1; it <= C; ++it) {
+        if (it == C) {
+            c->tb_E[it] = nb;
+            c->tb_A[it] = c->tb_B[it] = nN;
+            c->tb_D[it] = nb;
+            break;
+        }
+        const long long eb = it * cb, ebound = std::min(nE, 32 * eb);  // elements [0, ebound) done at step s
+        c->tb_E[it] = eb;
+        c->tb_A[it] = ebound > 0 ? std::min(nN, pm_node[ebound - 1] + 1) : 0;
+        // nodes [0, B): every incident element < ebound (and already updated for step s)
+        const long long b = std::lower_bound(pm_inc.begin(), pm_inc.end(), ebound) - pm_inc.begin();
+        c->tb_B[it] = std::min(b, c->tb_A[it]);
+        // elements [0, D): every node < B; whole batches only
+        const long long d = std::lower_bound(pm_node.begin(), pm_node.end(), c->tb_B[it]) - pm_node.begin();
+        c->tb_D[it] = std::min(d / 32, eb);
+    }
+    for (long long it = 1; it <= C; ++it) {  // monotone by construction; keep it explicit
+        c->tb_A[it] = std::max(c->tb_A[it], c->tb_A[it - 1]);
+        c->tb_B[it] = std::max(c->tb_B[it], c->tb_B[it - 1]);
+        c->tb_D[it] = std::max(c->tb_D[it], c->tb_D[it - 1]);
+    }
+    c->tb_built_mb = c->tblock_mb;
+}
+
+static bool tblock_eligible(const hakai_ctx* c) {
+    return c->tblock_mb > 0 && !c->comm && !c->contact && !c->q_from_buf && !c->diag_atomic_q &&
+           !c->diag_no_assembly && c->nE > 0 && c->nN > 0 && (c->nbc == 0 || c->d_bc_of_node);
+}
+
+// Steps t and t+1 with the chunked schedule (stream mode). last: the call ends with step t+1.
+static int step_pair(hakai_ctx* c, double t, double d_time, bool last) {
+    if (c->tb_built_mb != c->tblock_mb) tblock_build(c);
+    hipStream_t s = c->stream;
+    const int cur0 = c->cur;
+    const long long C = (long long)c->tb_E.size() - 1;
+    hk::NodalArgs na;
+    std::memset(&na, 0, sizeof na);
+    na.u = c->d_u[cur0];               // step s: u_{s-1}; out: u_{s-2} -> u_s (range 2 swaps them)
+    na.u_pre_out = c->d_u[1 - cur0];
+    na.mass = c->d_mass;
+    na.inc_ptr = c->d_inc_ptr;
+    na.inc = c->d_inc;
+    na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
+    na.cstride = c->fe_layout == 1 ? c->nEp : 1;
+    na.early = c->nodal_early;
+    na.fe_nt = c->nodal_fe_nt;
+    na.reverse = c->nodal_reverse;
+    na.fe = c->d_fe;
+    na.nN = c->nN;
+    na.dt = d_time;
+    na.poison = c->d_poison;
+    na.two_step = 1;
+    if (c->nbc > 0) {
+        na.bc_of_node = c->d_bc_of_node;
+        na.bc.dof = c->d_bc_dof;
+        na.bc.grp = c->d_bc_grp;
+        na.bc.val = c->d_bc_val;
+        na.bc.n = c->nbc;
+        na.bc.amp_n = c->d_amp_n;
+        na.bc.amp_off = c->d_amp_off;
+        na.bc.amp_t = c->d_amp_t;
+        na.bc.amp_v = c->d_amp_v;
+        na.bc.dt = d_time;
+        na.bc.poison = c->d_poison;
+    }
+    na.bc.ct = t * d_time;
+    na.ct2 = (t + 1.0) * d_time;
+    hk::ElemArgs ea = elem_args(c);
+    ea.u = c->d_u[1 - cur0];           // step s: u_s, u_{s-1} (range 2: u_{s+1}, u_s)
+    ea.u_pre = c->d_u[cur0];
+    ea.step_i = (int)t;
+    ea.two_step = 1;
+    EventPair ep;
+    for (long long it = 0; it <= C; ++it) {
+        const bool has1 = it < C, has2 = it > 0;
+        na.r1_lo = has1 ? c->tb_A[it] : 0;
+        na.r1_hi = has1 ? c->tb_A[it + 1] : 0;
+        na.r2_lo = has2 ? c->tb_B[it - 1] : 0;
+        na.r2_hi = has2 ? c->tb_B[it] : 0;
+        hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
+        HIPCHK(hk::launch_nodal(na, s));
+        hkc::prof_end(c, &ep);
+        ea.r1_lo = has1 ? c->tb_E[it] : 0;
+        ea.r1_hi = has1 ? c->tb_E[it + 1] : 0;
+        ea.r2_lo = has2 ? c->tb_D[it - 1] : 0;
+        ea.r2_hi = has2 ? c->tb_D[it] : 0;
+        hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
+        HIPCHK(hk::launch_element(ea, c->has_ductile, last, s));
+        hkc::prof_end(c, &ep);
+    }
+    c->q_from_buf = false;
+    c->steps_done += 2;
+    c->last_dt = d_time;
+    c->tb_pairs++;
     return 0;
 }
 
@@ -989,6 +1129,13 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     while (it < n_steps) {
         const double t = t_first + (double)it;
         int rc;
+        if (it + 2 <= n_steps && tblock_eligible(c)) {
+            rc = step_pair(c, t, d_time, it + 2 == n_steps);
+            c->tdev_next = -1;
+            it += 2;
+            if (rc) return rc;
+            continue;
+        }
         // the call's last step stays in stream mode: it also stores triaxiality for downloads
         // (eligibility of step t implies it for the steps after it: step t clears every one-off
         // condition)
@@ -1169,6 +1316,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
             return 0;
         }
         return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
+    }
+    if (!std::strcmp(key, "tblock_mb")) {  // two-step chunked schedule, MB of Gauss-point state per chunk
+        if (value < 0 || value > (1 << 20)) return fail(HAKAI_ERR_ARG, "tblock_mb must be 0 (off) .. 2^20");
+        c->tblock_mb = (int)value;
+        return 0;
     }
     if (!std::strcmp(key, "graph")) {
         if (value < 0 || value > 1024 || (value & 1)) return fail(HAKAI_ERR_ARG, "graph must be 0 or an even step count <= 1024");

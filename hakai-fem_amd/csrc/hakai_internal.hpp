@@ -135,6 +135,16 @@ struct hakai_ctx {
     long long tdev_next = -1;          // the step the device counter is valid for (-1: unknown)
     int graph = 16;                    // tuning "graph": steps per graph (even), 0 = no capture
     long long graph_steps = 0;         // steps run from graphs (tests, stats)
+    // Two-step chunked schedule (tuning "tblock_mb", hakai_step on one GPU without contact): steps s
+    // and s+1 are interleaved chunk by chunk so that step s+1 of a chunk re-reads its Gauss-point
+    // state, element forces and node rows while they are still in the Infinity Cache. Boundaries,
+    // per iteration it = 0..C (see tblock_build): element batches tb_E[it] (step s chunks), node
+    // counts tb_A[it] (nodes step s's chunk it needs), tb_B[it] (nodes whose step-s forces are all
+    // in after chunks < it) and element batches tb_D[it] (elements whose nodes are all < tb_B[it]).
+    int tblock_mb = 0;                 // MB of Gauss-point state per chunk, 0 = off
+    long long tb_built_mb = -1;        // chunk size the schedule below was built for (-1: none)
+    std::vector<long long> tb_E, tb_A, tb_B, tb_D;
+    long long tb_pairs = 0;            // step pairs run with the chunked schedule (tests, stats)
     // multi-GPU
     hkc::Comm* comm = nullptr;
 };

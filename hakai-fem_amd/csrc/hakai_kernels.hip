@@ -654,12 +654,31 @@ __device__ __forceinline__ void graph_step(ElemArgs& a) {
     }
 }
 
+// Two-step chunked schedule (ElemArgs::two_step): virtual batch v < n1 is batch r1_lo + v of step s,
+// the others batch r2_lo + v - n1 of step s+1, whose displacement buffers are swapped. A batch lies
+// in one range, so the selection is uniform over the block.
+__device__ __forceinline__ long long two_step_batch(const ElemArgs& a, long long v) {
+    const long long n1 = a.r1_hi - a.r1_lo;
+    return v < n1 ? a.r1_lo + v : a.r2_lo + (v - n1);
+}
+__device__ __forceinline__ ElemArgs two_step_args(const ElemArgs& a, long long v) {
+    ElemArgs b = a;
+    if (v >= a.r1_hi - a.r1_lo) {
+        b.u = a.u_pre;
+        b.u_pre = a.u;
+        b.step_i = a.step_i + 1;
+    }
+    return b;
+}
+
 // One batch of 32 elements per block (simple form; small meshes, the literal drop-in, A/B).
-template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW, bool EXACT>
-__global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
+template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW, bool EXACT, bool TWO = false>
+__global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
+    const long long vb = xcd_remap(blockIdx.x, gridDim.x);
+    ElemArgs a = TWO ? two_step_args(a0, vb) : a0;
     if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
     const int k = threadIdx.x & 7;
@@ -668,7 +687,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
         stage_pusai(a, s_pus);
         __syncthreads();
     }
-    const long long e = (long long)xcd_remap(blockIdx.x, gridDim.x) * kEPB + grp;
+    const long long e = (TWO ? two_step_batch(a0, vb) : vb) * kEPB + grp;
     ElemIn in;
     load_stage_a<EXACT>(a, e, k, in);
     load_stage_b<true>(a, e, k, in);
@@ -683,7 +702,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a) {
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO = false>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
@@ -704,7 +723,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     const DevMat* mats = LDS_MATS ? s_mats : a.mats;
     double* nd8 = s_nd + grp * kLdsStride;
     double* xb = s_xb + (EXACT ? grp * kXbStride : 0);
-    const long long nb = a.nEp / kEPB;
+    const long long nb = TWO ? (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo) : a.nEp / kEPB;
     // Batch schedule, as (first, stride, count):
     //  map 0: each block walks a contiguous run of batches;
     //  map 1: each XCD owns a contiguous run and its blocks stride through it together, so the
@@ -725,111 +744,126 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     }
     if (count <= 0) return;  // block-uniform
     // iterations past the end are clamped to the last batch (loaded, never computed)
-    auto elem_of = [&](long long i) { return (first + (i < count ? i : count - 1) * stride) * kEPB + grp; };
+    // (TWO: virtual batches, mapped to the two ranges; each call site takes its batch's step args)
+    auto vb_of = [&](long long i) { return first + (i < count ? i : count - 1) * stride; };
+    auto elem_of = [&](long long i) { return (TWO ? two_step_batch(a, vb_of(i)) : vb_of(i)) * kEPB + grp; };
 
     ElemIn cur, nxt;
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
-    load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
+    load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(0)) : a, elem_of(0), k, cur);
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
-        load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
+        load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(i + 1)) : a, elem_of(i + 1), k, nxt);
+        const ElemArgs ai = TWO ? two_step_args(a, vb_of(i)) : a;
         if (EXACT)
-            elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, xb, s_pus,
+            elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                             cur);
         else
-            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(a, mats, elem_of(i), k, nd8, cur);
+            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, cur);
         cur = nxt;
         nxt = nn;
     }
 }
 
 // Runtime flags -> template instantiations.
-template <int MINW, bool EXACT>
+template <int MINW, bool EXACT, bool TWO>
 static void launch_element_w(const ElemArgs& a, bool do_delete, bool store_triax, bool with_vol, unsigned grid,
                              hipStream_t s) {
     if (with_vol) {
-        hipLaunchKernelGGL((k_element<false, false, true, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_element<false, false, true, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     } else if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<true, true, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, true, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<true, false, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, false, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<false, true, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, true, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<false, false, false, MINW, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, false, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     }
 }
 
-template <bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT>
+template <bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO>
 static void launch_pipe(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
     if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid), dim3(kBlock),
-                               0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
                                dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
                                dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS, NT, EXACT>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
                                dim3(kBlock), 0, s, a);
     }
 }
 
-template <bool ANY_PLASTIC, bool LDS_MATS>
+template <bool ANY_PLASTIC, bool LDS_MATS, bool TWO>
 static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
     if (a.exact) {  // reference-order kernel: Gauss-point state nontemporal when any is requested
         if (a.gp_nt)
-            launch_pipe<ANY_PLASTIC, LDS_MATS, 3, true>(a, do_delete, store_triax, grid, s);
+            launch_pipe<ANY_PLASTIC, LDS_MATS, 3, true, TWO>(a, do_delete, store_triax, grid, s);
         else
-            launch_pipe<ANY_PLASTIC, LDS_MATS, 0, true>(a, do_delete, store_triax, grid, s);
+            launch_pipe<ANY_PLASTIC, LDS_MATS, 0, true, TWO>(a, do_delete, store_triax, grid, s);
         return;
     }
     if (ANY_PLASTIC && LDS_MATS && a.gp_nt) {
         switch (a.gp_nt) {
-            case 1: launch_pipe<true, true, 1, false>(a, do_delete, store_triax, grid, s); break;
-            case 2: launch_pipe<true, true, 2, false>(a, do_delete, store_triax, grid, s); break;
-            default: launch_pipe<true, true, 3, false>(a, do_delete, store_triax, grid, s); break;
+            case 1: launch_pipe<true, true, 1, false, TWO>(a, do_delete, store_triax, grid, s); break;
+            case 2: launch_pipe<true, true, 2, false, TWO>(a, do_delete, store_triax, grid, s); break;
+            default: launch_pipe<true, true, 3, false, TWO>(a, do_delete, store_triax, grid, s); break;
         }
         return;
     }
-    launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false>(a, do_delete, store_triax, grid, s);
+    launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false, TWO>(a, do_delete, store_triax, grid, s);
 }
 
-hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
-    if (a.nE <= 0) return hipSuccess;
-    if (a.exact && !a.pusai) return hipErrorInvalidValue;
-    const long long nb = a.nEp / kEPB;
+template <bool TWO>
+static hipError_t launch_element_t(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
+    const long long nb = TWO ? (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo) : a.nEp / kEPB;
+    if (nb <= 0) return hipSuccess;
     if (a.pipe_blocks > 0 && !a.vol) {
         const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
         const bool lds = a.nmat <= kMaxLdsMats;
         if (a.any_plastic) {
-            if (lds) launch_element_p<true, true>(a, do_delete, store_triax, grid, s);
-            else launch_element_p<true, false>(a, do_delete, store_triax, grid, s);
+            if (lds) launch_element_p<true, true, TWO>(a, do_delete, store_triax, grid, s);
+            else launch_element_p<true, false, TWO>(a, do_delete, store_triax, grid, s);
         } else {
-            if (lds) launch_element_p<false, true>(a, do_delete, store_triax, grid, s);
-            else launch_element_p<false, false>(a, do_delete, store_triax, grid, s);
+            if (lds) launch_element_p<false, true, TWO>(a, do_delete, store_triax, grid, s);
+            else launch_element_p<false, false, TWO>(a, do_delete, store_triax, grid, s);
         }
         return hipGetLastError();
     }
     const unsigned grid = (unsigned)nb;
     if (a.exact) {
-        launch_element_w<2, true>(a, do_delete, store_triax, a.vol != nullptr, grid, s);
+        launch_element_w<2, true, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s);
         return hipGetLastError();
     }
     switch (a.variant) {
-        case 3: launch_element_w<3, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        case 4: launch_element_w<4, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        default: launch_element_w<2, false>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        case 3: launch_element_w<3, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        case 4: launch_element_w<4, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
+        default: launch_element_w<2, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
+    if (a.nE <= 0) return hipSuccess;
+    if (a.exact && !a.pusai) return hipErrorInvalidValue;
+    if (a.two_step) {
+        if (a.vol || a.t_rd || a.r1_lo < 0 || a.r2_lo < 0 || a.r1_hi < a.r1_lo || a.r2_hi < a.r2_lo ||
+            a.r1_hi * kEPB > a.nEp || a.r2_hi * kEPB > a.nEp)
+            return hipErrorInvalidValue;
+        return launch_element_t<true>(a, do_delete, store_triax, s);
+    }
+    return launch_element_t<false>(a, do_delete, store_triax, s);
 }
 
 // Negative-Jacobian diagnostic (the reference prints a warning, v2/HAKAI_j.jl:1736-1739): counts
@@ -944,13 +978,30 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
 // MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer. Compile-time modes keep the
 // kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
 // which serialises the early node loads with the gather again.
-template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false, bool BCF = false>
-__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
+// TWO (NodalArgs::two_step): thread index v < n1 updates node r1_lo + v for step s, the others node
+// r2_lo + v - n1 for step s+1 (displacement buffers swapped, BC time ct2).
+template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false, bool BCF = false, bool TWO = false>
+__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
 #pragma clang fp contract(off)
-    if (poisoned(a.poison)) return;
-    const unsigned lb = a.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
-    const long long n = (long long)lb * kBlock + threadIdx.x;
-    if (n >= a.nN) return;
+    if (poisoned(a0.poison)) return;
+    const unsigned lb = a0.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
+    const long long v = (long long)lb * kBlock + threadIdx.x;
+    NodalArgs a = a0;
+    long long n = v;
+    if (TWO) {
+        const long long n1 = a0.r1_hi - a0.r1_lo, n2 = a0.r2_hi - a0.r2_lo;
+        if (v >= n1 + n2) return;
+        if (v < n1) {
+            n = a0.r1_lo + v;
+        } else {
+            n = a0.r2_lo + (v - n1);
+            a.u = a0.u_pre_out;
+            a.u_pre_out = const_cast<double*>(a0.u);
+            a.bc.ct = a0.ct2;
+        }
+    } else if (n >= a.nN) {
+        return;
+    }
     NodeIn in;
     if (EARLY) nodal_load<FEXT>(a, n, in);
     const long long cs = AOS ? 1 : a.cstride;  // compile-time 1: a row's 3 loads merge into 2
@@ -990,47 +1041,60 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
     nodal_update<BCF>(a, n, in, Q0, Q1, Q2);
 }
 
-template <bool FEXT, bool AOS, bool EARLY, bool BCF>
+template <bool FEXT, bool AOS, bool EARLY, bool BCF, bool TWO>
 static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.qbuf)
-        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8 && a.fe_nt)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY, false, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
-template <bool FEXT, bool AOS, bool BCF>
+template <bool FEXT, bool AOS, bool BCF, bool TWO>
 static void launch_nodal_f(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.early)
-        launch_nodal_e<FEXT, AOS, true, BCF>(a, grid, s);
+        launch_nodal_e<FEXT, AOS, true, BCF, TWO>(a, grid, s);
     else
-        launch_nodal_e<FEXT, AOS, false, BCF>(a, grid, s);
+        launch_nodal_e<FEXT, AOS, false, BCF, TWO>(a, grid, s);
 }
 
-template <bool FEXT, bool BCF>
+template <bool FEXT, bool BCF, bool TWO>
 static void launch_nodal_a(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.cstride == 1)
-        launch_nodal_f<FEXT, true, BCF>(a, grid, s);
+        launch_nodal_f<FEXT, true, BCF, TWO>(a, grid, s);
     else
-        launch_nodal_f<FEXT, false, BCF>(a, grid, s);
+        launch_nodal_f<FEXT, false, BCF, TWO>(a, grid, s);
 }
 
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
     if (a.nN <= 0) return hipSuccess;
+    if (a.two_step) {  // chunked two-step schedule: no external force, no uploaded Q, no graph counter
+        if (a.fext || a.qbuf || a.bc.t_rd || a.r1_lo < 0 || a.r2_lo < 0 || a.r1_hi < a.r1_lo ||
+            a.r2_hi < a.r2_lo || a.r1_hi > a.nN || a.r2_hi > a.nN)
+            return hipErrorInvalidValue;
+        const long long nv = (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo);
+        if (nv <= 0) return hipSuccess;
+        const unsigned grid = (unsigned)((nv + kBlock - 1) / kBlock);
+        if (a.bc_of_node)
+            launch_nodal_a<false, true, true>(a, grid, s);
+        else
+            launch_nodal_a<false, false, true>(a, grid, s);
+        return hipGetLastError();
+    }
     const unsigned grid = (unsigned)((a.nN + kBlock - 1) / kBlock);
     if (a.bc_of_node) {
         if (a.fext)
-            launch_nodal_a<true, true>(a, grid, s);
+            launch_nodal_a<true, true, false>(a, grid, s);
         else
-            launch_nodal_a<false, true>(a, grid, s);
+            launch_nodal_a<false, true, false>(a, grid, s);
     } else {
         if (a.fext)
-            launch_nodal_a<true, false>(a, grid, s);
+            launch_nodal_a<true, false, false>(a, grid, s);
         else
-            launch_nodal_a<false, false>(a, grid, s);
+            launch_nodal_a<false, false, false>(a, grid, s);
     }
     return hipGetLastError();
 }

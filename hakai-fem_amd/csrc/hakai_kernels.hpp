@@ -46,6 +46,12 @@ struct ElemArgs {
                             // rows land on one dummy row: no fe traffic, results invalid)
     const int* poison;      // [0] != 0: a contact buffer overflowed in this call; every state-writing
                             // kernel is a no-op from then on (the state stays the last good step's)
+    // Two-step chunked schedule (tuning "tblock_mb", hakai_step): when two_step is set the launch
+    // covers batches [r1_lo, r1_hi) of step step_i (u, u_pre as above) and batches [r2_lo, r2_hi)
+    // of step step_i + 1, whose displacement buffers are the other way round (u_pre holds u_{s+1},
+    // u holds u_s). Batch ranges are element batches of kEPB.
+    int two_step;
+    long long r1_lo, r1_hi, r2_lo, r2_hi;
 };
 
 struct BCArgs {
@@ -83,6 +89,11 @@ struct NodalArgs {
     const int* bc_of_node; // one GPU: [nN] first entry of `bc` of each node (-1 none); the nodal
     BCArgs bc;             // kernel then applies the BCs itself (no k_bc launch)
     const int* poison;     // see ElemArgs::poison
+    // Two-step chunked schedule (see ElemArgs): nodes [r1_lo, r1_hi) get step s's update (u, u_pre_out,
+    // bc.ct) and nodes [r2_lo, r2_hi) step s+1's, with u and u_pre_out swapped and BC time ct2.
+    int two_step;
+    long long r1_lo, r1_hi, r2_lo, r2_hi;
+    double ct2;
 };
 
 
