@@ -67,6 +67,17 @@ static void dfree(T*& p) {
 
 namespace hkc {
 
+static void own_free(hakai_ctx* c) {
+    dfree(c->d_own_off);
+    dfree(c->d_own_list);
+    dfree(c->d_own_q);
+    dfree(c->d_own_rp);
+    dfree(c->d_own_rows);
+    dfree(c->d_own_dump);
+    c->own_built_g = -1;
+    c->own_valid = false;
+}
+
 static void free_model(hakai_ctx* c) {
     contact_destroy(c);
     dfree(c->d_coord);
@@ -90,6 +101,7 @@ static void free_model(hakai_ctx* c) {
     dfree(c->d_del_step);
     dfree(c->d_qbuf);
     dfree(c->d_fext);
+    own_free(c);
     c->model_ok = false;
     c->state_ok = false;
 }
@@ -606,6 +618,7 @@ int hakai_set_bc(hakai_ctx* c, const hakai_bc_t* bc) {
 
 int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const double* ic_values, double d_time) {
     if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
+    if (c) c->own_valid = false;  // the next nodal update gathers fe (or the uploaded Q)
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "reset_state before upload_model");
     HIPCHK(hipSetDevice(c->device));
@@ -644,6 +657,7 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
 
 int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
+    if (c) c->own_valid = false;  // the next nodal update gathers fe (or the uploaded Q)
     if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "upload_state before upload_model");
     HIPCHK(hipSetDevice(c->device));
@@ -788,6 +802,181 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Owner-computed assembly (tuning "own_assembly"). Logical block lb of the persistent element
+// kernel (grid G) walks batches [lb*nb/G, (lb+1)*nb/G) in order. A node's incidences, in ascending
+// element order (the reference's serial sum, v2/HAKAI_j.jl:668-675), split into consecutive
+// per-block segments. The block holding the FIRST segment sums it in an LDS slot, starting from
+// 0.0 exactly like the nodal gather, and stores the result into own_q[n] (the whole Q when the
+// segment is all of them). Every contribution of a later segment is copied unchanged to its own
+// row, rows of a node consecutive in element order, and the nodal kernel forms
+// ((own_q[n] + row) + row) ... -- the same additions in the same order as the gather of fe, so the
+// result is bit-identical. One 16-B entry per node segment piece (or exported
+// contribution) per super-batch of kOwnS batches, one thread each (layout: hakai_kernels.hip
+// own_pass). Slots are allocated per block over the super-batches a sum is open; a mesh needing more than kOwnSlots open
+// sums in one block, or a node with > 8 incidences, does not use the mode.
+// ---------------------------------------------------------------------------------------------
+static constexpr int kOwnSlotsHost = 1024;  // = kOwnSlots in hakai_kernels.hip
+static constexpr int kOwnSHost = 2;         // = kOwnS: batches per super-batch
+static constexpr int kOwnExpRowsHost = 4;   // = kOwnExpRows: contributions per exported entry
+enum { kOwnInitH = 1, kOwnFinH = 2, kOwnExpH = 4, kOwnNopH = 8 };
+
+static bool own_build(hakai_ctx* c, long long G) {
+    hkc::own_free(c);
+    const long long nb = c->nEp / 32, nN = c->nN;
+    c->own_built_g = -2;
+    if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
+    struct Ent { int target, slot, flags, n; int lanes[8]; };
+    // super-batches: runs of kOwnS batches from each block's first batch (the last one may be short);
+    // sb_first[b] = first batch of b's super-batch, which also indexes the entry lists
+    std::vector<long long> bstart(G + 1);
+    for (long long lb = 0; lb <= G; ++lb) bstart[lb] = lb * nb / G;
+    std::vector<int> block_of(nb);
+    std::vector<long long> sb_first(nb);
+    for (long long lb = 0; lb < G; ++lb)
+        for (long long b = bstart[lb]; b < bstart[lb + 1]; ++b) {
+            block_of[b] = (int)lb;
+            sb_first[b] = bstart[lb] + (b - bstart[lb]) / kOwnSHost * kOwnSHost;
+        }
+    std::vector<std::vector<Ent>> per(nb);
+    std::vector<int> rp(nN + 1, 0);
+    long long rows = 0;
+    // open-sum intervals per block in super-batch units: (first, last, entry refs to patch the slot)
+    struct Seg { long long s0, s1; std::vector<std::pair<long long, int>> refs; };
+    std::vector<std::vector<Seg>> segs(G);
+    auto batch_of = [&](int j) { return (long long)(c->h_inc0[j] / 8) / 32; };
+    for (long long n = 0; n < nN; ++n) {
+        rp[n] = (int)rows;
+        const int j0 = c->h_ptr[n], j1 = c->h_ptr[n + 1];
+        if (j0 == j1) continue;
+        const int hb = block_of[batch_of(j0)];
+        int j = j0;
+        Seg sg;
+        sg.s0 = -1;
+        while (j < j1 && block_of[batch_of(j)] == hb) {  // the head segment, super-batch by super-batch
+            const long long sb = sb_first[batch_of(j)];
+            Ent en{(int)n, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+            while (j < j1 && sb_first[batch_of(j)] == sb) {
+                const long long e = c->h_inc0[j] / 8;
+                const int k = c->h_inc0[j] % 8;
+                if (en.n == 8) return false;
+                en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + k);
+                ++j;
+            }
+            if (sg.s0 < 0) {
+                sg.s0 = sb;
+                en.flags |= kOwnInitH;
+            }
+            sg.s1 = sb;
+            per[sb].push_back(en);
+            sg.refs.emplace_back(sb, (int)per[sb].size() - 1);
+        }
+        per[sg.s1][sg.refs.back().second].flags |= kOwnFinH;
+        if (sg.s1 > sg.s0) segs[hb].push_back(std::move(sg));
+        while (j < j1) {  // later segments: each contribution to its own row, up to 4 per entry
+            const long long sb = sb_first[batch_of(j)];
+            Ent en{(int)rows, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+            while (j < j1 && sb_first[batch_of(j)] == sb && en.n < kOwnExpRowsHost) {
+                const long long e = c->h_inc0[j] / 8;
+                en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + c->h_inc0[j] % 8);
+                ++rows;
+                ++j;
+            }
+            per[sb].push_back(en);
+        }
+    }
+    rp[nN] = (int)rows;
+    if (rows > (1LL << 31) - 1) return false;
+    // slots: a sum open over super-batches [s0, s1] holds its slot through s1; reuse strictly after
+    for (long long lb = 0; lb < G; ++lb) {
+        auto& v = segs[lb];
+        std::sort(v.begin(), v.end(), [](const Seg& x, const Seg& y) { return x.s0 < y.s0; });
+        std::vector<std::pair<long long, int>> busy;  // (s1, slot) min-heap
+        std::vector<int> free_slots;
+        int next = 0;
+        auto cmp = [](const std::pair<long long, int>& x, const std::pair<long long, int>& y) { return x.first > y.first; };
+        for (auto& sg : v) {
+            while (!busy.empty() && busy.front().first < sg.s0) {
+                free_slots.push_back(busy.front().second);
+                std::pop_heap(busy.begin(), busy.end(), cmp);
+                busy.pop_back();
+            }
+            int slot;
+            if (!free_slots.empty()) {
+                slot = free_slots.back();
+                free_slots.pop_back();
+            } else {
+                slot = next++;
+            }
+            if (slot >= kOwnSlotsHost) return false;
+            for (auto& r : sg.refs) per[r.first][r.second].slot = slot;
+            busy.emplace_back(sg.s1, slot);
+            std::push_heap(busy.begin(), busy.end(), cmp);
+        }
+    }
+    std::vector<int> off(nb + 1, 0);
+    for (long long b = 0; b < nb; ++b) {
+        if (per[b].size() > 256) return false;  // one entry per thread
+        off[b + 1] = off[b] + (int)per[b].size();
+    }
+    const long long ne = off[nb];
+    std::vector<int> list(4 * (size_t)(ne + 1), 0);
+    for (long long b = 0; b < nb; ++b)
+        for (size_t i = 0; i < per[b].size(); ++i) {
+            const Ent& en = per[b][i];
+            unsigned long long lo = 0;
+            for (int q = 0; q < 7; ++q) lo |= (unsigned long long)en.lanes[q] << (9 * q);
+            int* w = &list[4 * ((size_t)off[b] + i)];
+            w[0] = en.target;
+            w[1] = (int)((unsigned)en.slot | (unsigned)en.flags << 10 | (unsigned)en.n << 14 |
+                         (unsigned)en.lanes[7] << 18);
+            w[2] = (int)(unsigned)(lo & 0xffffffffu);
+            w[3] = (int)(unsigned)(lo >> 32);
+        }
+    int* nop = &list[4 * (size_t)ne];  // padding entry: reads lane 0, stores to the dump line
+    nop[1] = kOwnNopH << 10;
+    hipStream_t s = c->stream;
+    HIPCHK(dalloc(&c->d_own_off, off.size()));
+    HIPCHK(dalloc(&c->d_own_list, list.size()));
+    HIPCHK(dalloc(&c->d_own_q, 3 * (size_t)nN));
+    HIPCHK(dalloc(&c->d_own_rp, rp.size()));
+    HIPCHK(dalloc(&c->d_own_rows, 3 * (size_t)std::max(rows, 1LL)));
+    HIPCHK(dalloc(&c->d_own_dump, 8 * (size_t)G));
+    HIPCHK(hipMemcpyAsync(c->d_own_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_own_list, list.data(), list.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_own_rp, rp.data(), rp.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->d_own_q, 0, 3 * (size_t)nN * sizeof(double), s));  // nodes without elements
+    HIPCHK(hipStreamSynchronize(s));
+    c->own_nop = (int)ne;
+    c->own_rows = rows;
+    c->own_entries = ne;
+    c->own_built_g = G;
+    return true;
+}
+
+// Grid of the persistent kernel for this context (0: the one-batch kernel runs).
+static long long own_grid(const hakai_ctx* c) {
+    const long long nb = c->nEp / 32;
+    const bool pipe = nb >= (long long)c->pipe_min * c->pipe_blocks && c->pipe_blocks > 0;
+    return pipe ? std::min<long long>(nb, c->pipe_blocks) : 0;
+}
+
+// This step's element update uses owner-computed assembly (builds the lists on first use).
+static bool own_use(hakai_ctx* c) {
+    if (!c->own_assembly || c->comm || c->elem_exact || c->fe_layout != 0 || c->diag_atomic_q || c->diag_no_assembly ||
+        c->tblock_mb || c->nmat > hk::kMaxLdsMats || (c->gp_nt != 0 && c->gp_nt != 3) || c->nE <= 0)
+        return false;
+    const long long G = own_grid(c);
+    if (G <= 0) return false;
+    if (c->own_built_g != G && c->own_built_g != -2 - G) {
+        if (!own_build(c, G)) {
+            c->own_built_g = -2 - G;  // not suitable for this grid: remembered, fe mode
+            return false;
+        }
+    }
+    return c->own_built_g == G;
+}
+
 // One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take
 // the step number from the device counter and the element kernel advances it. phase: 1 = the
 // contact search (phase A), 2 = the rest (contact phase B, nodal, BCs, element, exchange), 3 = both;
@@ -825,6 +1014,12 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.two_step = 0;
     na.r1_lo = na.r1_hi = na.r2_lo = na.r2_hi = 0;
     na.ct2 = 0.0;
+    // owner-computed assembly: Q from the previous element step's sums (else the fe gather)
+    const bool own = own_use(c);
+    const bool own_q = c->own_valid && !na.qbuf;
+    na.own_q = own_q ? c->d_own_q : nullptr;
+    na.own_rp = own_q ? c->d_own_rp : nullptr;
+    na.own_rows = own_q ? c->d_own_rows : nullptr;
     hk::BCArgs ba;
     ba.dof = c->d_bc_dof;
     ba.grp = c->d_bc_grp;
@@ -878,6 +1073,15 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
+    if (own) {
+        ea.own = 1;
+        ea.own_off = c->d_own_off;
+        ea.own_list = reinterpret_cast<const int4*>(c->d_own_list);
+        ea.own_nop = c->own_nop;
+        ea.own_q = c->d_own_q;
+        ea.own_rows = c->d_own_rows;
+        ea.own_dump = c->d_own_dump;
+    }
     if (c->g_trd) {
         ea.t_rd = c->g_trd;
         ea.t_wr = c->d_tstep + par;
@@ -885,6 +1089,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
     HIPCHK(hk::launch_element(ea, c->has_ductile, last, s));
     hkc::prof_end(c, &ep);
+    c->own_valid = own;
+    c->own_steps += own ? 1 : 0;
     rc = hkc::comm_post_element(c, (long long)t);
     if (rc) return rc;
     rc = hkc::contact_post_step(c);
@@ -1024,6 +1230,7 @@ static int step_pair(hakai_ctx* c, double t, double d_time, bool last) {
         hkc::prof_end(c, &ep);
     }
     c->q_from_buf = false;
+    c->own_valid = false;
     c->steps_done += 2;
     c->last_dt = d_time;
     c->tb_pairs++;
@@ -1036,7 +1243,10 @@ static int step_pair(hakai_ctx* c, double t, double d_time, bool last) {
 // argument is fixed for a given starting parity (cur), so one graph per parity serves the whole
 // run. A failed capture leaves the context's host state advanced: the call returns the error.
 static bool graph_eligible(const hakai_ctx* c, double t) {
-    return c->graph && !c->comm && !c->prof && !c->q_from_buf && c->nE > 0 && hkc::contact_graph_ok(c, t);
+    // (owner-computed assembly: only once the previous step left its sums, so every captured nodal
+    // update reads them)
+    return c->graph && !c->comm && !c->prof && !c->q_from_buf && c->nE > 0 && hkc::contact_graph_ok(c, t) &&
+           c->own_valid == own_use(const_cast<hakai_ctx*>(c));
 }
 
 static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
@@ -1079,6 +1289,7 @@ static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
     } else {  // replay the host-side state changes of the captured steps
         hkc::contact_graph_advance(c, t + len - 1);
         c->q_from_buf = false;
+        c->own_steps += c->own_valid ? len : 0;  // captured in the steady state: every step or none
         c->steps_done += len;
         c->last_dt = d_time;
     }
@@ -1123,6 +1334,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         return fail(HAKAI_ERR_STATE, "step: a multi-GPU contact buffer overflowed; the state is that of the last good "
                     "step -- raise the capacity and hakai_upload_state / hakai_reset_state on every rank");
     HIPCHK(hipSetDevice(c->device));
+    (void)own_use(c);  // owner-assembly lists are built here, never inside a graph capture
     const int cur0 = c->cur;
     const long long done0 = c->steps_done;
     int64_t it = 0;
@@ -1198,6 +1410,17 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
 int hakai_graph_steps(hakai_ctx* c, int64_t* n) {
     if (!c || !n) return fail(HAKAI_ERR_ARG, "null");
     *n = c->graph_steps;
+    return 0;
+}
+
+int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
+    if (!c || !key || !value) return fail(HAKAI_ERR_ARG, "null");
+    if (!std::strcmp(key, "graph_steps")) *value = c->graph_steps;
+    else if (!std::strcmp(key, "tblock_pairs")) *value = c->tb_pairs;
+    else if (!std::strcmp(key, "own_steps")) *value = c->own_steps;
+    else if (!std::strcmp(key, "own_rows")) *value = c->own_built_g > 0 ? c->own_rows : -1;
+    else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
+    else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
 
@@ -1316,6 +1539,11 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
             return 0;
         }
         return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
+    }
+    if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "own_assembly must be 0 or 1");
+        c->own_assembly = (int)value;
+        return 0;
     }
     if (!std::strcmp(key, "tblock_mb")) {  // two-step chunked schedule, MB of Gauss-point state per chunk
         if (value < 0 || value > (1 << 20)) return fail(HAKAI_ERR_ARG, "tblock_mb must be 0 (off) .. 2^20");

@@ -145,6 +145,21 @@ struct hakai_ctx {
     long long tb_built_mb = -1;        // chunk size the schedule below was built for (-1: none)
     std::vector<long long> tb_E, tb_A, tb_B, tb_D;
     long long tb_pairs = 0;            // step pairs run with the chunked schedule (tests, stats)
+    // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): the persistent
+    // element kernel sums node forces in LDS in element order and stores Q (or a prefix partial plus
+    // the later contributions as rows) instead of the per-element fe array.
+    int own_assembly = 0;              // tuning value (1 = use when eligible)
+    long long own_built_g = -1;        // grid the lists were built for (-1 none, -2 mesh not suitable)
+    bool own_valid = false;            // d_own_q/d_own_rows hold the last element step's sums
+    int* d_own_off = nullptr;          // [nb+1] per-batch entry offsets
+    int* d_own_list = nullptr;         // 4 ints per entry (+ one no-op entry at own_nop)
+    int own_nop = 0;
+    double* d_own_q = nullptr;         // [nN][3]
+    int* d_own_rp = nullptr;           // [nN+1]
+    double* d_own_rows = nullptr;      // [rows][3]
+    double* d_own_dump = nullptr;      // [grid][8]
+    long long own_rows = 0, own_entries = 0;
+    long long own_steps = 0;           // element steps run with owner-computed assembly
     // multi-GPU
     hkc::Comm* comm = nullptr;
 };

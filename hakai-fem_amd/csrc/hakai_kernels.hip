@@ -105,12 +105,24 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
 
 // Unconditional write-back of one lane (selects, no branches): its node's force fk, its Gauss
 // point's state, the element flag and the deletion log.
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false, bool OWN = false>
 __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, int k, const ElemIn& in, bool active,
                                                bool kill, const double (&fk)[3], const double (&fin)[6],
-                                               const double (&eps)[6], double eqp, double ys, double tri) {
+                                               const double (&eps)[6], double eqp, double ys, double tri,
+                                               double* sfe = nullptr) {
     const long long gp = 8 * e + k, ld = a.ld;
-    if (a.qatomic) {  // timing diagnostic: atomics into Q instead of the fe round trip
+    if (OWN) {  // owner-computed assembly: the batch's forces go to LDS [element][local node][3]
+        double* fo = sfe + 3 * ((threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k)));
+        fo[0] = active ? fk[0] : 0.0;
+        fo[1] = active ? fk[1] : 0.0;
+        fo[2] = active ? fk[2] : 0.0;
+        if (STORE_TRIAX) {  // a call's last step also keeps fe (Q / Qe downloads, mode switches)
+            double* fg = a.fe + in.fb;
+            fg[0] = active ? fk[0] : 0.0;
+            fg[a.cstride] = active ? fk[1] : 0.0;
+            fg[2 * a.cstride] = active ? fk[2] : 0.0;
+        }
+    } else if (a.qatomic) {  // timing diagnostic: atomics into Q instead of the fe round trip
         const int src = (int)(threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k));
         const int node = __shfl(in.n, src);
         if (active)
@@ -160,9 +172,9 @@ __device__ __forceinline__ double ductile_fr(const DevMat* M, int nd, double t_e
 // is stored):  flag 1 -> full update;  flag 2 (deleted in the previous step) -> Qe and triaxiality
 // become 0 and the flag 0 (the reference skips deleted elements, :1116, and their stress is zero);
 // flag 0 -> state written back unchanged, Qe 0.
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0, bool OWN = false>
 __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __restrict__ mats, long long e, int k,
-                                          double* nd8, const ElemIn& in) {
+                                          double* nd8, const ElemIn& in, double* sfe = nullptr) {
     const DevMat* M = mats + in.mt;
     const bool active = in.fl == 1;
     const int npp = M->npp;
@@ -350,7 +362,8 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     fk[1] += S * bb1;
     fk[2] += S * bb2;
     if (WITH_VOL) a.vol[e] = V;
-    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, false, OWN>(a, e, k, in, active, kill, fk, fin, eps, eqp,
+                                                                         ys, tri, sfe);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -698,13 +711,98 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
         elem_step<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride, in);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Owner-computed assembly (ElemArgs::own). The block sums node forces per SUPER-BATCH of kOwnS
+// consecutive batches of its range (the last one may be shorter), one 16-B entry per thread:
+//   x = target (node for ACC entries, row for EXP), y = slot | flags << 10 | n << 14 | lane7 << 18,
+//   z | w << 32 = lanes 0-6, 9 bits each; a lane is (element - 32 * super-batch's first batch) * 8
+//   + local node, in ascending element order.
+// An ACC entry continues node `target`'s running sum in LDS slot `slot` (INIT: from 0.0, the nodal
+// gather's own start) with the super-batch's contributions in element order; FIN stores the sum to
+// own_q (the node's Q, or its prefix partial when later blocks hold more incidences); EXP copies one
+// up to kOwnExpRows contributions of one node unchanged to consecutive own_rows. Every thread issues
+// the same kOwnExpRows x 24 B of stores (unused ones to a per-block dump line, which a wave's lanes
+// share), so the pipeline's load accounting stays exact. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
+// ---------------------------------------------------------------------------------------------
+constexpr int kOwnSlots = 1024;            // LDS running sums per block (24 KB)
+constexpr int kOwnS = 2;                   // batches per super-batch
+constexpr int kOwnFe = kOwnS * kEPB * 24;  // staged forces per super-batch (doubles)
+constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
+enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
+
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS only: prefetches stay in flight
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ int4 own_load(const ElemArgs& a, long long b) {
+    const int o0 = a.own_off[b], o1 = a.own_off[b + 1];
+    const int idx = o0 + (int)threadIdx.x;
+    return a.own_list[idx < o1 ? idx : a.own_nop];
+}
+
+__device__ __forceinline__ int own_lane(int4 en, int j) {
+    const unsigned long long lo = (unsigned long long)(unsigned)en.z | ((unsigned long long)(unsigned)en.w << 32);
+    return j < 7 ? (int)((lo >> (9 * j)) & 511) : (int)(((unsigned)en.y >> 18) & 511);
+}
+
+__device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, const double* s_fe, double* s_part) {
+#pragma clang fp contract(off)
+    lds_barrier();  // the super-batch's forces are in s_fe, the previous pass is done with s_part
+    const int slot = en.y & 1023, flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;
+    double* dump = a.own_dump + 8 * (long long)blockIdx.x;
+    double v[3];
+    if (flags & (kOwnExp | kOwnNop)) {  // EXP: up to kOwnExpRows contributions -> rows target, target+1, ...
+#pragma unroll
+        for (int j = 0; j < kOwnExpRows; ++j) {
+            const int l = own_lane(en, j);
+            double* dst = ((flags & kOwnExp) && j < n) ? a.own_rows + 3 * ((long long)en.x + j) : dump;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dst[c] = s_fe[3 * l + c];
+        }
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = (flags & kOwnInit) ? 0.0 : s_part[3 * slot + c];
+    for (int j = 0; j < n; ++j) {
+        const int l = own_lane(en, j);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] += s_fe[3 * l + c];
+    }
+    if (!(flags & kOwnFin)) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s_part[3 * slot + c] = v[c];
+    }
+    double* dst = (flags & kOwnFin) ? a.own_q + 3 * (long long)en.x : dump;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dst[c] = v[c];
+#pragma unroll
+    for (int j = 1; j < kOwnExpRows; ++j)  // same store count as an EXP entry
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dump[c] = 0.0;
+}
+
+// Between passes: the same stores to the dump line, so both sides of the (block-uniform) pass
+// branch leave the same number of memory operations in flight.
+__device__ __forceinline__ void own_idle(const ElemArgs& a) {
+    double* dump = a.own_dump + 8 * (long long)blockIdx.x;
+#pragma unroll
+    for (int j = 0; j < kOwnExpRows; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dump[c] = 0.0;
+}
+
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO = false>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO = false,
+          bool OWN = false>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
+    __shared__ __attribute__((aligned(16))) double s_fe[OWN ? 2 * kOwnFe : 1];
+    __shared__ __attribute__((aligned(16))) double s_part[OWN ? kOwnSlots * 3 : 1];
     __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
@@ -730,7 +828,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     //         batches that share a node layer (one element layer apart) are processed close in
     //         time on the same L2 (blocks are dealt round-robin over the 8 XCDs).
     long long first, stride, count;
-    if (a.pipe_map == 1 && gridDim.x % 8 == 0) {
+    if (OWN) {  // contiguous batch range per block, in order (own_build's partition)
+        first = (long long)blockIdx.x * nb / gridDim.x;
+        stride = 1;
+        count = ((long long)blockIdx.x + 1) * nb / gridDim.x - first;
+    } else if (a.pipe_map == 1 && gridDim.x % 8 == 0) {
         const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, per = gridDim.x >> 3;
         const long long r0 = x * nb / 8, r1 = (x + 1) * nb / 8;
         first = r0 + j;
@@ -749,19 +851,33 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     auto elem_of = [&](long long i) { return (TWO ? two_step_batch(a, vb_of(i)) : vb_of(i)) * kEPB + grp; };
 
     ElemIn cur, nxt;
+    int4 ent_cur = {0, 0, 0, 0}, ent_nxt = {0, 0, 0, 0};
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
     load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(0)) : a, elem_of(0), k, cur);
+    // (OWN: super-batch of iteration i starts at iteration i - i % kOwnS; its entries are listed under
+    // its first batch)
+    auto sb_of = [&](long long i) { return vb_of((i < count ? i : count - 1) / kOwnS * kOwnS); };
+    if (OWN) ent_cur = own_load(a, sb_of(0));
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
         load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(i + 1)) : a, elem_of(i + 1), k, nxt);
+        if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
+        double* sfe = s_fe + ((i / kOwnS) & 1) * kOwnFe + (i % kOwnS) * (kEPB * 24);
         const ElemArgs ai = TWO ? two_step_args(a, vb_of(i)) : a;
         if (EXACT)
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                             cur);
         else
-            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, cur);
+            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(ai, mats, elem_of(i), k, nd8, cur, sfe);
+        if (OWN) {
+            if ((i + 1) % kOwnS == 0 || i + 1 == count)  // block-uniform
+                own_pass(a, ent_cur, s_fe + ((i / kOwnS) & 1) * kOwnFe, s_part);
+            else
+                own_idle(a);
+            ent_cur = ent_nxt;
+        }
         cur = nxt;
         nxt = nn;
     }
@@ -825,6 +941,25 @@ static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax
     launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false, TWO>(a, do_delete, store_triax, grid, s);
 }
 
+template <bool ANY_PLASTIC, int NT>
+static void launch_own(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (do_delete) {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
+    } else {
+        if (store_triax)
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+                               dim3(kBlock), 0, s, a);
+    }
+}
+
 template <bool TWO>
 static hipError_t launch_element_t(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
     const long long nb = TWO ? (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo) : a.nEp / kEPB;
@@ -857,6 +992,21 @@ static hipError_t launch_element_t(const ElemArgs& a, bool do_delete, bool store
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
     if (a.nE <= 0) return hipSuccess;
     if (a.exact && !a.pusai) return hipErrorInvalidValue;
+    if (a.own) {  // owner-computed assembly: fused persistent kernel only (own_build sized its lists for it)
+        const long long nb = a.nEp / kEPB;
+        if (a.exact || a.two_step || a.vol || a.qatomic || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats ||
+            (a.gp_nt != 0 && a.gp_nt != 3) || !a.own_off || !a.own_list || !a.own_q || !a.own_dump)
+            return hipErrorInvalidValue;
+        const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
+        if (a.any_plastic) {
+            if (a.gp_nt) launch_own<true, 3>(a, do_delete, store_triax, grid, s);
+            else launch_own<true, 0>(a, do_delete, store_triax, grid, s);
+        } else {
+            if (a.gp_nt) launch_own<false, 3>(a, do_delete, store_triax, grid, s);
+            else launch_own<false, 0>(a, do_delete, store_triax, grid, s);
+        }
+        return hipGetLastError();
+    }
     if (a.two_step) {
         if (a.vol || a.t_rd || a.r1_lo < 0 || a.r2_lo < 0 || a.r1_hi < a.r1_lo || a.r2_hi < a.r2_lo ||
             a.r1_hi * kEPB > a.nEp || a.r2_hi * kEPB > a.nEp)
@@ -975,7 +1125,7 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
     }
 }
 
-// MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer. Compile-time modes keep the
+// MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer; 3: owner-computed Q + rows. Compile-time modes keep the
 // kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
 // which serialises the early node loads with the gather again.
 // TWO (NodalArgs::two_step): thread index v < n1 updates node r1_lo + v for step s, the others node
@@ -1010,6 +1160,16 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
         Q0 = a.qbuf[3 * n + 0];
         Q1 = a.qbuf[3 * n + 1];
         Q2 = a.qbuf[3 * n + 2];
+    } else if (MODE == 3) {  // owner-computed assembly: Q (or prefix partial) + later rows, in order
+        Q0 = a.own_q[3 * n + 0];
+        Q1 = a.own_q[3 * n + 1];
+        Q2 = a.own_q[3 * n + 2];
+        const int j0 = a.own_rp[n], j1 = a.own_rp[n + 1];
+        for (int j = j0; j < j1; ++j) {
+            Q0 += a.own_rows[3LL * j + 0];
+            Q1 += a.own_rows[3LL * j + 1];
+            Q2 += a.own_rows[3LL * j + 2];
+        }
     } else if (MODE == 0) {
         const int4 lo = reinterpret_cast<const int4*>(a.inc8)[2 * n];
         const int4 hi = reinterpret_cast<const int4*>(a.inc8)[2 * n + 1];
@@ -1045,6 +1205,8 @@ template <bool FEXT, bool AOS, bool EARLY, bool BCF, bool TWO>
 static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.qbuf)
         hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (a.own_q)
+        hipLaunchKernelGGL((k_nodal<3, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8 && a.fe_nt)
         hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8)

@@ -52,6 +52,20 @@ struct ElemArgs {
     // u holds u_s). Batch ranges are element batches of kEPB.
     int two_step;
     long long r1_lo, r1_hi, r2_lo, r2_hi;
+    // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): logical block lb of
+    // the persistent kernel walks batches [lb*nb/G, (lb+1)*nb/G) in order and sums every node force
+    // it holds in LDS, in element order, from a per-batch list of 16-B entries
+    // (own_list[own_off[b] .. own_off[b+1]), see OwnEntry in hakai_kernels.hip). It stores each
+    // node's complete Q, or the prefix partial P of a node whose later incidences belong to later
+    // blocks, into own_q, and those later contributions one by one into own_rows. No fe traffic
+    // except on a call's last step (STORE_TRIAX), which also stores fe so Q/Qe downloads stay valid.
+    int own;
+    const int* own_off;
+    const int4* own_list;
+    int own_nop;            // index of a no-op entry (list padding)
+    double* own_q;          // [nN][3]
+    double* own_rows;       // [rows][3]
+    double* own_dump;       // [grid][8] target of the no-op entries' stores
 };
 
 struct BCArgs {
@@ -94,6 +108,10 @@ struct NodalArgs {
     int two_step;
     long long r1_lo, r1_hi, r2_lo, r2_hi;
     double ct2;
+    // Owner-computed assembly (ElemArgs::own): Q = own_q[n] + own_rows[own_rp[n]] + ... in order
+    const double* own_q;
+    const int* own_rp;
+    const double* own_rows;
 };
 
 

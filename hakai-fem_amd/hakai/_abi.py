@@ -124,6 +124,7 @@ def lib() -> ctypes.CDLL:
                                     PD, PD]),
         "hakai_run_inp": (c_int, [c_char_p, c_char_p, c_int, c_int]),
         "hakai_graph_steps": (c_int, [c_void_p, PI64]),
+        "hakai_stat": (c_int, [c_void_p, c_char_p, PI64]),
         "hakai_vtk_writer_create": (c_int, [POINTER(c_void_p), c_char_p, c_int64, PD, c_int64, PI64, c_int]),
         "hakai_vtk_writer_submit": (c_int, [c_void_p, c_int, PI64, PD, PD, PD, PD, PD, PD, PD]),
         "hakai_vtk_writer_acquire": (c_int, [c_void_p, c_void_p]),
@@ -149,7 +150,7 @@ def exported_symbols() -> list[str]:
         "hakai_profile_enable", "hakai_profile_mask", "hakai_profile_read", "hakai_set_tuning", "hakai_set_contact",
         "hakai_set_contact_cp", "hakai_set_contact_global", "hakai_set_contact_params", "hakai_contact_info", "hakai_contact_stats", "hakai_contact_force", "hakai_comm_unique_id", "hakai_comm_init",
         "hakai_comm_init_local", "hakai_set_interface", "hakai_set_element_offset", "hakai_inp_read", "hakai_inp_free", "hakai_write_vtk", "hakai_run_inp",
-        "hakai_graph_steps", "hakai_vtk_writer_create", "hakai_vtk_writer_submit", "hakai_vtk_writer_acquire", "hakai_vtk_writer_commit",
+        "hakai_graph_steps", "hakai_stat", "hakai_vtk_writer_create", "hakai_vtk_writer_submit", "hakai_vtk_writer_acquire", "hakai_vtk_writer_commit",
         "hakai_vtk_writer_wait", "hakai_vtk_writer_destroy",
     ]
 

@@ -190,6 +190,12 @@ class Solver:
     def set_tuning(self, key: str, value: int):
         check(self.L.hakai_set_tuning(self.ctx, key.encode(), int(value)))
 
+    def stat(self, key: str) -> int:
+        """Step-loop counter (hakai_stat): graph_steps, tblock_pairs, own_steps, own_rows, own_entries."""
+        n = I64(0)
+        check(self.L.hakai_stat(self.ctx, key.encode(), ctypes.byref(n)))
+        return n.value
+
     def graph_steps(self) -> int:
         """Steps run from captured hipGraphs so far (hakai_graph_steps)."""
         n = I64(0)

@@ -165,6 +165,12 @@ function graph_steps(c::Ctx)
     check(ccall((:hakai_graph_steps, lib), Cint, (Ptr{Cvoid}, Ref{Int64}), c.p, n))
     return n[]
 end
+# step-loop counters: "graph_steps", "tblock_pairs", "own_steps", "own_rows", "own_entries"
+function stat(c::Ctx, key::AbstractString)
+    n = Ref{Int64}(0)
+    check(ccall((:hakai_stat, lib), Cint, (Ptr{Cvoid}, Cstring, Ref{Int64}), c.p, key, n))
+    return n[]
+end
 # (step, element) of every deletion so far, in the order the reference prints them (:733-736)
 function deleted(c::Ctx; cap::Integer = 1 << 16)
     n = Ref{Int64}(0)

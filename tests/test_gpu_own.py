@@ -1,0 +1,121 @@
+"""Owner-computed assembly (tuning key "own_assembly"): the persistent element kernel sums node
+forces in LDS, in element order, and hands the nodal update each node's Q -- or its prefix partial
+plus the later blocks' contributions as individual rows -- instead of the 24-B-per-element-node fe
+array. The additions are the nodal gather's own, in the same order
+(v2/HAKAI_j.jl:668-675 serial sum), so every run here must be BIT-identical to the fe path: the same
+tuning with own_assembly 0. Block ranges are forced small so node sums straddle 2-3 blocks (prefix
+partial + exported rows), and meshes that need more LDS sums than a block holds fall back.
+"""
+import numpy as np
+import pytest
+
+from hakai import mesh
+from hakai.solver import Solver
+from test_gpu_tblock import _same, _shuffled
+from util import fast_deletion_bar, small_bar
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(m, calls, tune, own, graph=None):
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("own_assembly", own)
+        if graph is not None:
+            sv.set_tuning("graph", graph)
+        for t0, n in calls:
+            sv.step(t0, n)
+        g = sv.download()
+        dels = [tuple(x) for x in sv.deleted()]
+        st = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_entries", "graph_steps")}
+    return g, dels, st
+
+
+PIPE = {"elem_pipe_min": 0}
+
+
+@pytest.mark.parametrize("blocks", [3, 16, 200])
+def test_own_deletion_bar_bitexact(blocks):
+    """Deleting bar, 6 400 hex = 200 batches over 3 / 16 / 200 persistent blocks (200: one batch per
+    block, most nodes straddle blocks); odd step counts, several calls, graphs on."""
+    m = fast_deletion_bar(4, 4, 400)
+    calls = [(1, 301), (302, 1000), (1302, 1699)]
+    tune = {**PIPE, "elem_pipe_blocks": blocks}
+    g0, d0, s0 = _run(m, calls, tune, 0)
+    g1, d1, s1 = _run(m, calls, tune, 1)
+    assert s0["own_steps"] == 0 and s1["own_steps"] == 3000, (s0, s1)
+    assert s1["own_rows"] > 0 and s1["graph_steps"] > 0
+    assert len(d0) > 0 and d1 == d0
+    _same(g1, g0)
+
+
+def test_own_stream_mode_and_toggle():
+    """Stream mode (graph 0), and own_assembly switched off and on between calls."""
+    m = small_bar(6, 5, 300, n_steps=600, v_end=5e5)
+    tune = {**PIPE, "elem_pipe_blocks": 32}
+    g0, _, _ = _run(m, [(1, 600)], tune, 0, graph=0)
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("graph", 0)
+        for t0, n, own in ((1, 150, 1), (151, 151, 0), (302, 99, 1), (401, 200, 1)):
+            sv.set_tuning("own_assembly", own)
+            sv.step(t0, n)
+        g1 = sv.download()
+        assert sv.stat("own_steps") == 449
+    assert np.any(g0.integ_eq_plastic_strain > 0)
+    _same(g1, g0)
+
+
+def test_own_shuffled_numbering_bitexact():
+    """Random element and node numbering (long-lived LDS sums, many rows) or a fallback: bit-identical."""
+    m = _shuffled(fast_deletion_bar(3, 3, 200), seed=11)
+    tune = {**PIPE, "elem_pipe_blocks": 8}
+    g0, d0, _ = _run(m, [(1, 3000)], tune, 0)
+    g1, d1, s1 = _run(m, [(1, 3000)], tune, 1)
+    assert d1 == d0 and len(d0) > 0
+    _same(g1, g0)
+    # the sums of a shuffled mesh stay open for most of a block's range: more than a block's LDS slots
+    assert s1["own_steps"] in (0, 3000)
+
+
+def test_own_too_many_open_sums_falls_back():
+    """A 40x40 cross-section in one block needs > 1024 open LDS sums: fe path, same results."""
+    m = small_bar(40, 40, 6, n_steps=200, v_end=5e5)
+    tune = {**PIPE, "elem_pipe_blocks": 1}
+    g0, _, _ = _run(m, [(1, 200)], tune, 0)
+    g1, _, s1 = _run(m, [(1, 200)], tune, 1)
+    assert s1["own_steps"] == 0 and s1["own_rows"] == -1
+    _same(g1, g0)
+
+
+def test_own_contact_two_bodies_bitexact():
+    """External (contact) force beside the owner-computed Q: impactor on a plate, with deletions."""
+    m = mesh.two_body_model(plate=(12, 12, 3), impactor=(4, 4, 6), gap=0.05, v=-2e5)
+    n = 1500
+    tune = {**PIPE, "elem_pipe_blocks": 2}
+    g0, d0, _ = _run(m, [(1, 701), (702, n - 701)], tune, 0)
+    g1, d1, s1 = _run(m, [(1, 701), (702, n - 701)], tune, 1)
+    assert s1["own_steps"] == n
+    assert d1 == d0
+    assert np.max(np.abs(g0.disp)) > 0
+    _same(g1, g0)
+
+
+def test_own_upload_state_mid_run():
+    """An uploaded state (Q from the upload, then fe gathers on the first owner step) matches."""
+    m = fast_deletion_bar(3, 3, 120)
+    with Solver(m) as sv:
+        sv.step(1, 500)
+        mid = sv.download()
+    outs = []
+    for own in (0, 1):
+        with Solver(m) as sv:
+            for k, v in {**PIPE, "elem_pipe_blocks": 5}.items():
+                sv.set_tuning(k, v)
+            sv.set_tuning("own_assembly", own)
+            sv.upload(mid)
+            sv.step(501, 800)
+            outs.append(sv.download())
+    _same(outs[1], outs[0])
