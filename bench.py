@@ -252,6 +252,7 @@ def main():
         plastic.append(float(np.mean(st.integ_eq_plastic_strain > 0)))
         n_active += int(st.element_flag.sum())
     plastic_frac = float(np.mean(plastic))
+    own_steps = sum(sv.stat("own_steps") for sv in svs)
     n_elem_local = sum(b[0].nElement for b in built)
     n_node_local = sum(b[0].nNode for b in built)
     if multi:
@@ -324,6 +325,8 @@ def main():
                        whole_step_roofline_frac=round(whole_bytes * a.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)
                        if nparts == 1 else None,
                        kernel_ms_per_step=k_ms, **extra,
+                       assembly=("owner-computed node sums in LDS (own_assembly), element order" if own_steps
+                                 else "fe round trip (element forces gathered by the nodal kernel)"),
                        parallelism=(f"dp{world}" if world > 1 else
                                     (f"rehearsal: {R} in-process ranks on one GPU (device-copy exchange)"
                                      if R else "single"))),

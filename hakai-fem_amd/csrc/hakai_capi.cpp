@@ -408,6 +408,7 @@ int hakai_create(hakai_ctx** out, int device) {
         }
     }
     if (const char* v = std::getenv("HAKAI_ELEM_EXACT")) c->elem_exact = std::atoi(v) ? 1 : 0;
+    if (const char* v = std::getenv("HAKAI_OWN_ASSEMBLY")) c->own_assembly = std::atoi(v) ? 1 : 0;
     *out = c;
     return 0;
 }

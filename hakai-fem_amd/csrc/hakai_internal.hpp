@@ -148,7 +148,7 @@ struct hakai_ctx {
     // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): the persistent
     // element kernel sums node forces in LDS in element order and stores Q (or a prefix partial plus
     // the later contributions as rows) instead of the per-element fe array.
-    int own_assembly = 0;              // tuning value (1 = use when eligible)
+    int own_assembly = 1;              // tuning value (1 = use when eligible; env HAKAI_OWN_ASSEMBLY)
     long long own_built_g = -1;        // grid the lists were built for (-1 none, -2 mesh not suitable)
     bool own_valid = false;            // d_own_q/d_own_rows hold the last element step's sums
     int* d_own_off = nullptr;          // [nb+1] per-batch entry offsets

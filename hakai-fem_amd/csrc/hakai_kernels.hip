@@ -720,9 +720,9 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
 // An ACC entry continues node `target`'s running sum in LDS slot `slot` (INIT: from 0.0, the nodal
 // gather's own start) with the super-batch's contributions in element order; FIN stores the sum to
 // own_q (the node's Q, or its prefix partial when later blocks hold more incidences); EXP copies one
-// up to kOwnExpRows contributions of one node unchanged to consecutive own_rows. Every thread issues
-// the same kOwnExpRows x 24 B of stores (unused ones to a per-block dump line, which a wave's lanes
-// share), so the pipeline's load accounting stays exact. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
+// up to kOwnExpRows contributions of one node unchanged to consecutive own_rows. Stores are issued
+// unconditionally (unused ones to a per-block dump line, which a wave's lanes share) so the loads of
+// the pipeline stay in flight across the pass. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
 // ---------------------------------------------------------------------------------------------
 constexpr int kOwnSlots = 1024;            // LDS running sums per block (24 KB)
 constexpr int kOwnS = 2;                   // batches per super-batch
@@ -777,20 +777,6 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, const doubl
     double* dst = (flags & kOwnFin) ? a.own_q + 3 * (long long)en.x : dump;
 #pragma unroll
     for (int c = 0; c < 3; ++c) dst[c] = v[c];
-#pragma unroll
-    for (int j = 1; j < kOwnExpRows; ++j)  // same store count as an EXP entry
-#pragma unroll
-        for (int c = 0; c < 3; ++c) dump[c] = 0.0;
-}
-
-// Between passes: the same stores to the dump line, so both sides of the (block-uniform) pass
-// branch leave the same number of memory operations in flight.
-__device__ __forceinline__ void own_idle(const ElemArgs& a) {
-    double* dump = a.own_dump + 8 * (long long)blockIdx.x;
-#pragma unroll
-    for (int j = 0; j < kOwnExpRows; ++j)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) dump[c] = 0.0;
 }
 
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
@@ -872,10 +858,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         else
             elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(ai, mats, elem_of(i), k, nd8, cur, sfe);
         if (OWN) {
-            if ((i + 1) % kOwnS == 0 || i + 1 == count)  // block-uniform
+            // block-uniform branch; the compiler's load accounting is the same on both sides
+            // (checked in the ISA: identical vmcnt waits with or without balancing stores)
+            if ((i + 1) % kOwnS == 0 || i + 1 == count)
                 own_pass(a, ent_cur, s_fe + ((i / kOwnS) & 1) * kOwnFe, s_part);
-            else
-                own_idle(a);
             ent_cur = ent_nxt;
         }
         cur = nxt;

@@ -3,13 +3,13 @@
 # Env switches (pass inline in the gpurun command): SWEEP="variants", PROF=1, NOTEST=1.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-export HAKAI_GRAPH=0  # rocprofv3 cannot trace hipGraph launches
 mkdir -p gpurun_out
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ -z "$NOTEST" ]; then
 timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
 fi
+export HAKAI_GRAPH=0  # rocprofv3 cannot trace hipGraph launches; the tests keep the default
 if [ -n "$SWEEP" ]; then
 timeout -k 10 600 python tools/sweep.py --variants "$SWEEP" > gpurun_out/sweep.log 2>&1
 rc=$?; echo "sweep rc=$rc"; tail -8 gpurun_out/sweep.log; ok $rc || exit $rc
