@@ -185,6 +185,12 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *   "nodal_reverse"     1 (default): each XCD walks its node chunk from its end;
  *   "nodal_fe_nt"       1: element forces gathered with nontemporal loads;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
+ *   "own_assembly"      1 (default; env HAKAI_OWN_ASSEMBLY): one GPU, fused persistent kernel: the
+ *                       element kernel sums node forces in LDS in element order and hands the nodal
+ *                       update Q (+ the rows of nodes shared between blocks) instead of the per-element
+ *                       force array; meshes it does not fit use that array (hakai_stat "own_steps");
+ *   "tblock_mb"         > 0: two-step chunked schedule with chunks of this many MB of Gauss-point
+ *                       state (one GPU, no contact; default 0 = off: measured slower on C3);
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
  *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
  *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy;
