@@ -73,6 +73,7 @@ static void own_free(hakai_ctx* c) {
     dfree(c->d_own_q);
     dfree(c->d_own_rp);
     dfree(c->d_own_rows);
+    dfree(c->d_own_ridx);
     dfree(c->d_own_dump);
     c->own_built_g = -1;
     c->own_valid = false;
@@ -812,23 +813,25 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 // segment is all of them). Every contribution of a later segment is copied unchanged to its own
 // row, rows of a node consecutive in element order, and the nodal kernel forms
 // ((own_q[n] + row) + row) ... -- the same additions in the same order as the gather of fe, so the
-// result is bit-identical. One 16-B entry per node segment piece (or exported
-// contribution) per super-batch of kOwnS batches, one thread each (layout: hakai_kernels.hip
+// result is bit-identical. Rows are numbered by super-batch (an export entry carries up to 4
+// contributions of any nodes to consecutive rows); own_ridx lists each node's rows in element order.
+// One 16-B entry per node segment piece (or exported
+// contribution) per super-batch of S = 2 batches (1 when 2 would need more than 256 entries),
+// one thread each (layout: hakai_kernels.hip
 // own_pass). Slots are allocated per block over the super-batches a sum is open; a mesh needing more than kOwnSlots open
 // sums in one block, or a node with > 8 incidences, does not use the mode.
 // ---------------------------------------------------------------------------------------------
 static constexpr int kOwnSlotsHost = 1024;  // = kOwnSlots in hakai_kernels.hip
-static constexpr int kOwnSHost = 2;         // = kOwnS: batches per super-batch
 static constexpr int kOwnExpRowsHost = 4;   // = kOwnExpRows: contributions per exported entry
 enum { kOwnInitH = 1, kOwnFinH = 2, kOwnExpH = 4, kOwnNopH = 8 };
 
-static bool own_build(hakai_ctx* c, long long G) {
+static bool own_build(hakai_ctx* c, long long G, int S) {
     hkc::own_free(c);
     const long long nb = c->nEp / 32, nN = c->nN;
     c->own_built_g = -2;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
     struct Ent { int target, slot, flags, n; int lanes[8]; };
-    // super-batches: runs of kOwnS batches from each block's first batch (the last one may be short);
+    // super-batches: runs of S batches from each block's first batch (the last one may be short);
     // sb_first[b] = first batch of b's super-batch, which also indexes the entry lists
     std::vector<long long> bstart(G + 1);
     for (long long lb = 0; lb <= G; ++lb) bstart[lb] = lb * nb / G;
@@ -837,7 +840,7 @@ static bool own_build(hakai_ctx* c, long long G) {
     for (long long lb = 0; lb < G; ++lb)
         for (long long b = bstart[lb]; b < bstart[lb + 1]; ++b) {
             block_of[b] = (int)lb;
-            sb_first[b] = bstart[lb] + (b - bstart[lb]) / kOwnSHost * kOwnSHost;
+            sb_first[b] = bstart[lb] + (b - bstart[lb]) / S * S;
         }
     std::vector<std::vector<Ent>> per(nb);
     std::vector<int> rp(nN + 1, 0);
@@ -846,8 +849,10 @@ static bool own_build(hakai_ctx* c, long long G) {
     struct Seg { long long s0, s1; std::vector<std::pair<long long, int>> refs; };
     std::vector<std::vector<Seg>> segs(G);
     auto batch_of = [&](int j) { return (long long)(c->h_inc0[j] / 8) / 32; };
+    // contributions of later segments: (super-batch, incidence index j); their rows are numbered
+    // in super-batch order so that one entry exports up to 4 of them (any nodes) to consecutive rows
+    std::vector<std::pair<long long, int>> exports;
     for (long long n = 0; n < nN; ++n) {
-        rp[n] = (int)rows;
         const int j0 = c->h_ptr[n], j1 = c->h_ptr[n + 1];
         if (j0 == j1) continue;
         const int hb = block_of[batch_of(j0)];
@@ -874,19 +879,33 @@ static bool own_build(hakai_ctx* c, long long G) {
         }
         per[sg.s1][sg.refs.back().second].flags |= kOwnFinH;
         if (sg.s1 > sg.s0) segs[hb].push_back(std::move(sg));
-        while (j < j1) {  // later segments: each contribution to its own row, up to 4 per entry
-            const long long sb = sb_first[batch_of(j)];
-            Ent en{(int)rows, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
-            while (j < j1 && sb_first[batch_of(j)] == sb && en.n < kOwnExpRowsHost) {
-                const long long e = c->h_inc0[j] / 8;
-                en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + c->h_inc0[j] % 8);
-                ++rows;
-                ++j;
-            }
-            per[sb].push_back(en);
-        }
+        for (; j < j1; ++j) exports.emplace_back(sb_first[batch_of(j)], j);
     }
-    rp[nN] = (int)rows;
+    // rows: grouped by super-batch (stable: node order, then element order within a node)
+    std::stable_sort(exports.begin(), exports.end(),
+                     [](const std::pair<long long, int>& x, const std::pair<long long, int>& y) { return x.first < y.first; });
+    std::vector<int> row_of_inc(c->h_inc0.size(), -1);
+    for (size_t q = 0; q < exports.size();) {
+        const long long sb = exports[q].first;
+        Ent en{(int)rows, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+        while (q < exports.size() && exports[q].first == sb && en.n < kOwnExpRowsHost) {
+            const int j = exports[q].second;
+            const long long e = c->h_inc0[j] / 8;
+            en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + c->h_inc0[j] % 8);
+            row_of_inc[j] = (int)rows++;
+            ++q;
+        }
+        per[sb].push_back(en);
+    }
+    // per node: its rows in element order (CSR rp / ridx)
+    std::vector<int> ridx;
+    ridx.reserve(exports.size());
+    for (long long n = 0; n < nN; ++n) {
+        rp[n] = (int)ridx.size();
+        for (int j = c->h_ptr[n]; j < c->h_ptr[n + 1]; ++j)
+            if (row_of_inc[j] >= 0) ridx.push_back(row_of_inc[j]);
+    }
+    rp[nN] = (int)ridx.size();
     if (rows > (1LL << 31) - 1) return false;
     // slots: a sum open over super-batches [s0, s1] holds its slot through s1; reuse strictly after
     for (long long lb = 0; lb < G; ++lb) {
@@ -942,16 +961,20 @@ static bool own_build(hakai_ctx* c, long long G) {
     HIPCHK(dalloc(&c->d_own_q, 3 * (size_t)nN));
     HIPCHK(dalloc(&c->d_own_rp, rp.size()));
     HIPCHK(dalloc(&c->d_own_rows, 3 * (size_t)std::max(rows, 1LL)));
+    HIPCHK(dalloc(&c->d_own_ridx, std::max<size_t>(ridx.size(), 1)));
     HIPCHK(dalloc(&c->d_own_dump, 8 * (size_t)G));
     HIPCHK(hipMemcpyAsync(c->d_own_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_own_list, list.data(), list.size() * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->d_own_rp, rp.data(), rp.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!ridx.empty())
+        HIPCHK(hipMemcpyAsync(c->d_own_ridx, ridx.data(), ridx.size() * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->d_own_q, 0, 3 * (size_t)nN * sizeof(double), s));  // nodes without elements
     HIPCHK(hipStreamSynchronize(s));
     c->own_nop = (int)ne;
     c->own_rows = rows;
     c->own_entries = ne;
     c->own_built_g = G;
+    c->own_s = S;
     return true;
 }
 
@@ -962,20 +985,24 @@ static long long own_grid(const hakai_ctx* c) {
     return pipe ? std::min<long long>(nb, c->pipe_blocks) : 0;
 }
 
-// This step's element update uses owner-computed assembly (builds the lists on first use).
+// This step's element update uses owner-computed assembly (builds the lists on first use). The
+// grid is the persistent kernel's, or 8x that (blocks then run in waves) when the default ranges
+// span so much of a wide cross-section that too many sums stay open in a block.
 static bool own_use(hakai_ctx* c) {
     if (!c->own_assembly || c->comm || c->elem_exact || c->fe_layout != 0 || c->diag_atomic_q || c->diag_no_assembly ||
         c->tblock_mb || c->nmat > hk::kMaxLdsMats || (c->gp_nt != 0 && c->gp_nt != 3) || c->nE <= 0)
         return false;
-    const long long G = own_grid(c);
-    if (G <= 0) return false;
-    if (c->own_built_g != G && c->own_built_g != -2 - G) {
-        if (!own_build(c, G)) {
-            c->own_built_g = -2 - G;  // not suitable for this grid: remembered, fe mode
-            return false;
-        }
+    const long long G0 = own_grid(c);
+    if (G0 <= 0) return false;
+    if (c->own_built_g > 0) return true;
+    if (c->own_built_g == -2 - G0) return false;  // tried for this grid: the mesh does not fit
+    const long long nb = c->nEp / 32;
+    for (long long G : {G0, 8 * G0}) {
+        if (G > nb) break;
+        if (own_build(c, G, 2) || own_build(c, G, 1)) return true;
     }
-    return c->own_built_g == G;
+    c->own_built_g = -2 - G0;
+    return false;
 }
 
 // One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take
@@ -1021,6 +1048,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.own_q = own_q ? c->d_own_q : nullptr;
     na.own_rp = own_q ? c->d_own_rp : nullptr;
     na.own_rows = own_q ? c->d_own_rows : nullptr;
+    na.own_ridx = own_q ? c->d_own_ridx : nullptr;
     hk::BCArgs ba;
     ba.dof = c->d_bc_dof;
     ba.grp = c->d_bc_grp;
@@ -1038,7 +1066,9 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.poison = c->d_poison;
     // one GPU, small mesh: the nodal kernel applies the BCs (multi-GPU redoes interface nodes
     // after the nodal kernel, so the BCs must come after that)
-    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm && c->nN <= kFuseBcMaxNodes;
+    // (fuse_bc 2: at any size; large meshes measured slower with the fe gather, see kFuseBcMaxNodes)
+    const bool fuse_bc = c->nbc > 0 && c->d_bc_of_node && c->fuse_bc && !c->comm &&
+                         (c->nN <= kFuseBcMaxNodes || c->fuse_bc == 2);
     if (fuse_bc) {
         na.bc_of_node = c->d_bc_of_node;
         na.bc = ba;
@@ -1075,7 +1105,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
     if (own) {
-        ea.own = 1;
+        ea.own = c->own_s;
+        ea.own_grid = (int)c->own_built_g;
         ea.own_off = c->d_own_off;
         ea.own_list = reinterpret_cast<const int4*>(c->d_own_list);
         ea.own_nop = c->own_nop;
@@ -1421,6 +1452,7 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     else if (!std::strcmp(key, "own_steps")) *value = c->own_steps;
     else if (!std::strcmp(key, "own_rows")) *value = c->own_built_g > 0 ? c->own_rows : -1;
     else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
+    else if (!std::strcmp(key, "own_superbatch")) *value = c->own_built_g > 0 ? c->own_s : 0;
     else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1492,7 +1524,7 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         return 0;
     }
     if (!std::strcmp(key, "fuse_bc")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fuse_bc must be 0 or 1");
+        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "fuse_bc must be 0, 1 or 2 (any mesh size)");
         c->fuse_bc = (int)value;
         return 0;
     }

@@ -156,10 +156,12 @@ struct hakai_ctx {
     int own_nop = 0;
     double* d_own_q = nullptr;         // [nN][3]
     int* d_own_rp = nullptr;           // [nN+1]
-    double* d_own_rows = nullptr;      // [rows][3]
+    double* d_own_rows = nullptr;      // [rows][3], numbered by super-batch
+    int* d_own_ridx = nullptr;         // rows of node n: own_ridx[own_rp[n] .. own_rp[n+1]), element order
     double* d_own_dump = nullptr;      // [grid][8]
     long long own_rows = 0, own_entries = 0;
     long long own_steps = 0;           // element steps run with owner-computed assembly
+    int own_s = 2;                     // batches per super-batch of the built lists (2, or 1)
     // multi-GPU
     hkc::Comm* comm = nullptr;
 };

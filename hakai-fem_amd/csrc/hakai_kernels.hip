@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Owner-computed assembly (ElemArgs::own). The block sums node forces per SUPER-BATCH of kOwnS
+// Owner-computed assembly (ElemArgs::own). The block sums node forces per SUPER-BATCH of OS
 // consecutive batches of its range (the last one may be shorter), one 16-B entry per thread:
 //   x = target (node for ACC entries, row for EXP), y = slot | flags << 10 | n << 14 | lane7 << 18,
 //   z | w << 32 = lanes 0-6, 9 bits each; a lane is (element - 32 * super-batch's first batch) * 8
@@ -720,13 +720,13 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
 // An ACC entry continues node `target`'s running sum in LDS slot `slot` (INIT: from 0.0, the nodal
 // gather's own start) with the super-batch's contributions in element order; FIN stores the sum to
 // own_q (the node's Q, or its prefix partial when later blocks hold more incidences); EXP copies one
-// up to kOwnExpRows contributions of one node unchanged to consecutive own_rows. Stores are issued
+// up to kOwnExpRows contributions (of any nodes) unchanged to consecutive own_rows. Stores are issued
 // unconditionally (unused ones to a per-block dump line, which a wave's lanes share) so the loads of
 // the pipeline stay in flight across the pass. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
 // ---------------------------------------------------------------------------------------------
 constexpr int kOwnSlots = 1024;            // LDS running sums per block (24 KB)
-constexpr int kOwnS = 2;                   // batches per super-batch
-constexpr int kOwnFe = kOwnS * kEPB * 24;  // staged forces per super-batch (doubles)
+// batches per super-batch: 2, or 1 for meshes whose 64-element super-batches need more than 256
+// entries (wide cross-sections); the host picks (own_build), the kernel is instantiated for both
 constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
 enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
 
@@ -784,8 +784,10 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, const doubl
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO = false,
-          bool OWN = false>
+          int OS = 0>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
+    constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
+    constexpr int kOwnFe = OS * kEPB * 24;       // staged forces per super-batch (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_fe[OWN ? 2 * kOwnFe : 1];
     __shared__ __attribute__((aligned(16))) double s_part[OWN ? kOwnSlots * 3 : 1];
@@ -841,16 +843,17 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
     load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(0)) : a, elem_of(0), k, cur);
-    // (OWN: super-batch of iteration i starts at iteration i - i % kOwnS; its entries are listed under
+    // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // its first batch)
-    auto sb_of = [&](long long i) { return vb_of((i < count ? i : count - 1) / kOwnS * kOwnS); };
+    constexpr int S = OS > 0 ? OS : 1;
+    auto sb_of = [&](long long i) { return vb_of((i < count ? i : count - 1) / S * S); };
     if (OWN) ent_cur = own_load(a, sb_of(0));
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
         load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(i + 1)) : a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
-        double* sfe = s_fe + ((i / kOwnS) & 1) * kOwnFe + (i % kOwnS) * (kEPB * 24);
+        double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         const ElemArgs ai = TWO ? two_step_args(a, vb_of(i)) : a;
         if (EXACT)
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, xb, s_pus,
@@ -860,8 +863,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         if (OWN) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
-            if ((i + 1) % kOwnS == 0 || i + 1 == count)
-                own_pass(a, ent_cur, s_fe + ((i / kOwnS) & 1) * kOwnFe, s_part);
+            if ((i + 1) % S == 0 || i + 1 == count)
+                own_pass(a, ent_cur, s_fe + ((i / S) & 1) * kOwnFe, s_part);
             ent_cur = ent_nxt;
         }
         cur = nxt;
@@ -927,23 +930,31 @@ static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax
     launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false, TWO>(a, do_delete, store_triax, grid, s);
 }
 
-template <bool ANY_PLASTIC, int NT>
+template <bool ANY_PLASTIC, int NT, int OS>
 static void launch_own(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
     if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
                                dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
                                dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
                                dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, true, NT, false, false, true>), dim3(grid),
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
                                dim3(kBlock), 0, s, a);
     }
+}
+
+template <bool ANY_PLASTIC, int NT>
+static void launch_own_s(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (a.own == 1)
+        launch_own<ANY_PLASTIC, NT, 1>(a, do_delete, store_triax, grid, s);
+    else
+        launch_own<ANY_PLASTIC, NT, 2>(a, do_delete, store_triax, grid, s);
 }
 
 template <bool TWO>
@@ -980,16 +991,17 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
     if (a.exact && !a.pusai) return hipErrorInvalidValue;
     if (a.own) {  // owner-computed assembly: fused persistent kernel only (own_build sized its lists for it)
         const long long nb = a.nEp / kEPB;
-        if (a.exact || a.two_step || a.vol || a.qatomic || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats ||
+        if (a.own > 2 || a.exact || a.two_step || a.vol || a.qatomic || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats ||
             (a.gp_nt != 0 && a.gp_nt != 3) || !a.own_off || !a.own_list || !a.own_q || !a.own_dump)
             return hipErrorInvalidValue;
-        const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
+        if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;
+        const unsigned grid = (unsigned)a.own_grid;
         if (a.any_plastic) {
-            if (a.gp_nt) launch_own<true, 3>(a, do_delete, store_triax, grid, s);
-            else launch_own<true, 0>(a, do_delete, store_triax, grid, s);
+            if (a.gp_nt) launch_own_s<true, 3>(a, do_delete, store_triax, grid, s);
+            else launch_own_s<true, 0>(a, do_delete, store_triax, grid, s);
         } else {
-            if (a.gp_nt) launch_own<false, 3>(a, do_delete, store_triax, grid, s);
-            else launch_own<false, 0>(a, do_delete, store_triax, grid, s);
+            if (a.gp_nt) launch_own_s<false, 3>(a, do_delete, store_triax, grid, s);
+            else launch_own_s<false, 0>(a, do_delete, store_triax, grid, s);
         }
         return hipGetLastError();
     }
@@ -1152,9 +1164,10 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
         Q2 = a.own_q[3 * n + 2];
         const int j0 = a.own_rp[n], j1 = a.own_rp[n + 1];
         for (int j = j0; j < j1; ++j) {
-            Q0 += a.own_rows[3LL * j + 0];
-            Q1 += a.own_rows[3LL * j + 1];
-            Q2 += a.own_rows[3LL * j + 2];
+            const long long r = a.own_ridx[j];
+            Q0 += a.own_rows[3 * r + 0];
+            Q1 += a.own_rows[3 * r + 1];
+            Q2 += a.own_rows[3 * r + 2];
         }
     } else if (MODE == 0) {
         const int4 lo = reinterpret_cast<const int4*>(a.inc8)[2 * n];

@@ -59,7 +59,8 @@ struct ElemArgs {
     // node's complete Q, or the prefix partial P of a node whose later incidences belong to later
     // blocks, into own_q, and those later contributions one by one into own_rows. No fe traffic
     // except on a call's last step (STORE_TRIAX), which also stores fe so Q/Qe downloads stay valid.
-    int own;
+    int own;                // 0 off; 1 or 2: batches per super-batch
+    int own_grid;           // blocks of the owner-assembly launch (the lists' partition)
     const int* own_off;
     const int4* own_list;
     int own_nop;            // index of a no-op entry (list padding)
@@ -108,9 +109,11 @@ struct NodalArgs {
     int two_step;
     long long r1_lo, r1_hi, r2_lo, r2_hi;
     double ct2;
-    // Owner-computed assembly (ElemArgs::own): Q = own_q[n] + own_rows[own_rp[n]] + ... in order
+    // Owner-computed assembly (ElemArgs::own): Q = own_q[n] + own_rows[own_ridx[own_rp[n]]] + ...
+    // in element order
     const double* own_q;
     const int* own_rp;
+    const int* own_ridx;
     const double* own_rows;
 };
 

@@ -121,7 +121,8 @@ int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
 int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
 /* Step-loop counters (tests, tools; no reference counterpart): "graph_steps", "tblock_pairs" (step
  * pairs run with the two-step chunked schedule), "own_steps" (element steps with owner-computed
- * assembly), "own_rows" / "own_entries" (its exported rows / per-batch entries for this mesh). */
+ * assembly), "own_rows" / "own_entries" (its exported rows / per-batch entries for this mesh),
+ * "own_superbatch" (batches of 32 elements per LDS summing pass: 2, or 1 for wide meshes). */
 int hakai_stat(hakai_ctx* ctx, const char* key, int64_t* value);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */

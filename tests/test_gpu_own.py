@@ -80,13 +80,35 @@ def test_own_shuffled_numbering_bitexact():
     assert s1["own_steps"] in (0, 3000)
 
 
-def test_own_too_many_open_sums_falls_back():
-    """A 40x40 cross-section in one block needs > 1024 open LDS sums: fe path, same results."""
+def test_own_wide_section_finer_grid_or_fallback():
+    """A 40x40 cross-section on 1 block: too many open sums, so the lists are built for 8 blocks
+    (blocks then run in waves) -- or the fe path; either way bit-identical. A shuffled wide mesh
+    cannot fit at all."""
     m = small_bar(40, 40, 6, n_steps=200, v_end=5e5)
     tune = {**PIPE, "elem_pipe_blocks": 1}
     g0, _, _ = _run(m, [(1, 200)], tune, 0)
     g1, _, s1 = _run(m, [(1, 200)], tune, 1)
+    assert s1["own_steps"] == 200, s1
+    _same(g1, g0)
+    ms = _shuffled(m, seed=3)
+    g0, _, _ = _run(ms, [(1, 60)], tune, 0)
+    g1, _, s1 = _run(ms, [(1, 60)], tune, 1)
     assert s1["own_steps"] == 0 and s1["own_rows"] == -1
+    _same(g1, g0)
+
+
+@pytest.mark.parametrize("layers", [12])
+def test_own_wide_section_single_batch_passes(layers):
+    """100x100 cross-section (C5's): 64-element super-batches would need more than 256 entries, so
+    the lists use one batch per summing pass; bit-identical to the fe path."""
+    m = small_bar(100, 100, layers, n_steps=100, v_end=5e5)
+    g0, _, _ = _run(m, [(1, 100)], {}, 0)
+    with Solver(m) as sv:
+        sv.set_tuning("own_assembly", 1)
+        sv.step(1, 100)
+        g1 = sv.download()
+        assert sv.stat("own_steps") == 100
+        assert sv.stat("own_superbatch") == 1
     _same(g1, g0)
 
 

@@ -30,6 +30,7 @@ def run(name, m, preload, steps):
         k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
                                                 (K_CONTACT, "contact"))}
         st = sv.download(element_flag=True, integ_eq_plastic_strain=True)
+        own = sv.stat("own_steps") > 0
     import numpy as np
     act = int(st.element_flag.sum())
     print(json.dumps({"config": name, "elements": m.nElement, "nodes": m.nNode, "steps": steps, "preload": preload,
@@ -38,7 +39,8 @@ def run(name, m, preload, steps):
                       "element_ms_timed": round(e_ms / max(e_n, 1), 4),
                       "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
                       "plastic_gp_frac": round(float(np.mean(st.integ_eq_plastic_strain > 0)), 4),
-                      "deleted": int(m.nElement - act)}), flush=True)
+                      "deleted": int(m.nElement - act),
+                      "assembly": "owner-computed (LDS)" if own else "fe round trip"}), flush=True)
 
 
 def main():
