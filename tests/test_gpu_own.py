@@ -141,3 +141,40 @@ def test_own_upload_state_mid_run():
             sv.step(501, 800)
             outs.append(sv.download())
     _same(outs[1], outs[0])
+
+
+def test_own_tensile5e_padded_batch_vs_oracle():
+    """Tensile5e.inp (5 hex: one batch, 27 padding elements; amplitude BCs; element 3 deleted at
+    step 15 153) on the persistent kernel with owner assembly: the fused kernel's oracle parity
+    (1e-6) and bit-identity with the fe path."""
+    import oracle as O
+    m = mesh.tensile5e_model()
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    g0, d0, _ = _run(m, [(1, m.n_steps)], PIPE, 0)
+    g1, d1, s1 = _run(m, [(1, m.n_steps)], PIPE, 1)
+    assert s1["own_steps"] == m.n_steps
+    assert d1 == d0 == o.deletions == [(15153, 3)]
+    _same(g1, g0)
+    assert np.max(np.abs(g1.disp - o.s["disp"])) / np.max(np.abs(o.s["disp"])) < 1e-6
+
+
+def test_own_isolated_node_and_ragged_batch():
+    """63 hex (last batch ragged) plus a node no element uses (Q = 0, its own sum never written)."""
+    from hakai.model import Model
+    base = small_bar(3, 3, 7, n_steps=300, v_end=5e5)
+    coord = np.vstack([base.coordmat, [[50.0, 50.0, 50.0]]])
+    extra = coord.shape[0]
+    m = Model(coord, base.elementmat, base.element_material, base.materials, bc=base.bc,
+              ic_dofs=np.concatenate([base.ic_dofs, [3 * extra]]),
+              ic_values=np.concatenate([np.asarray(base.ic_values), [1e3]]), d_time=base.d_time,
+              end_time=base.end_time, name="ragged_isolated")
+    g0, _, _ = _run(m, [(1, 151), (152, 149)], PIPE, 0)
+    g1, _, s1 = _run(m, [(1, 151), (152, 149)], PIPE, 1)
+    assert s1["own_steps"] == 300
+    # the isolated node has no mass (the reference's update divides by it): compare NaN as equal
+    from test_gpu_tblock import STATE
+    for k in STATE:
+        assert np.array_equal(getattr(g1, k), getattr(g0, k), equal_nan=True), k
+    assert np.all(g1.Q[3 * extra - 3:] == 0.0)
+    assert np.all(np.isfinite(g1.disp[:3 * extra - 3]))
