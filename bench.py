@@ -284,7 +284,8 @@ def main():
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("elements") == n_elem_local:
+            # measured on the one-GPU C3 workload (tools/gpu_prof.sh): attached to that workload only
+            if pm.get("elements") == n_elem_local and world == 1 and cfg["workload"].startswith("C3"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
