@@ -852,9 +852,18 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
     // contributions of later segments: (super-batch, incidence index j); their rows are numbered
     // in super-batch order so that one entry exports up to 4 of them (any nodes) to consecutive rows
     std::vector<std::pair<long long, int>> exports;
+    // multi-GPU: the nodes shared with rank-1 send their contributions one by one (hakai_comm.cpp
+    // k_pack_own), so all of them are rows
+    std::vector<char> all_rows(nN, 0);
+    if (const std::vector<int>* dn = hkc::comm_dn_nodes(c))
+        for (int n : *dn) all_rows[n] = 1;
     for (long long n = 0; n < nN; ++n) {
         const int j0 = c->h_ptr[n], j1 = c->h_ptr[n + 1];
         if (j0 == j1) continue;
+        if (all_rows[n]) {
+            for (int j = j0; j < j1; ++j) exports.emplace_back(sb_first[batch_of(j)], j);
+            continue;
+        }
         const int hb = block_of[batch_of(j0)];
         int j = j0;
         Seg sg;
@@ -989,7 +998,7 @@ static long long own_grid(const hakai_ctx* c) {
 // grid is the persistent kernel's, or 8x that (blocks then run in waves) when the default ranges
 // span so much of a wide cross-section that too many sums stay open in a block.
 static bool own_use(hakai_ctx* c) {
-    if (!c->own_assembly || c->comm || c->elem_exact || c->fe_layout != 0 || c->diag_atomic_q || c->diag_no_assembly ||
+    if (!c->own_assembly || c->elem_exact || c->fe_layout != 0 || c->diag_atomic_q || c->diag_no_assembly ||
         c->tblock_mb || c->nmat > hk::kMaxLdsMats || (c->gp_nt != 0 && c->gp_nt != 3) || c->nE <= 0)
         return false;
     const long long G0 = own_grid(c);

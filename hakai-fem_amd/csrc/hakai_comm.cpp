@@ -46,6 +46,7 @@ struct Comm {
     double* d_dn_sendC[2] = {nullptr, nullptr};  // [n_dn][nslot][3]
     double* d_dn_recvP = nullptr;                // [n_dn][3]
     double* d_saved = nullptr;                   // u_pre of interface nodes [n_up+n_dn][3]
+    std::vector<int> h_dn;                       // host copy of d_dn (owner-computed assembly)
     bool pending = false;
     int pending_par = 0;
     // all-gather of equal-size blocks (the contact mirror, hakai_contact.hip): per-parity send
@@ -167,6 +168,66 @@ __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const in
         const double uc = u[3 * n + c];
         const double up_ = saved[3 * j + c];
         const double f = fext ? fext[3 * n + c] : 0.0;  // contact force (external_force, :500-564)
+        out[3 * n + c] = inv * (f - Q[c] + mdt2 * (2.0 * uc - up_) + dC / 2.0 / dt * up_);
+    }
+}
+
+// Owner-computed assembly (hakai_capi.cpp own_build): a node's local Q is own_q[n] plus its rows
+// (own_ridx[own_rp[n]..]) in element order, and every local contribution of a dn node is a row of
+// its own -- so the partial sums and single contributions below are those k_pack / k_fix take
+// from fe, in the same order.
+__global__ void k_pack_own(const int* up, int n_up, const int* dn, int n_dn, const int* rp, const int* ridx,
+                           const double* rows, const double* own_q, int nslot, double* up_sendP, double* dn_sendC) {
+#pragma clang fp contract(off)
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_up) {
+        const int n = up[j];
+        double q[3] = {own_q[3LL * n], own_q[3LL * n + 1], own_q[3LL * n + 2]};
+        for (int i = rp[n]; i < rp[n + 1]; ++i)
+            for (int c = 0; c < 3; ++c) q[c] += rows[3LL * ridx[i] + c];
+        for (int c = 0; c < 3; ++c) up_sendP[3 * j + c] = q[c];
+    } else if (j < n_up + n_dn) {
+        const int jj = j - n_up;
+        const int n = dn[jj];
+        const int b = rp[n], m = rp[n + 1] - b;
+        double* o = dn_sendC + (long long)3 * nslot * jj;
+        for (int s = 0; s < nslot; ++s)
+            for (int c = 0; c < 3; ++c) o[3 * s + c] = s < m ? rows[3LL * ridx[b + s] + c] : 0.0;
+    }
+}
+
+__global__ void k_fix_own(const int* up, int n_up, const int* dn, int n_dn, const int* rp, const int* ridx,
+                          const double* rows, int nslot, const double* up_sendP, const double* up_recvC,
+                          const double* dn_recvP, const double* saved, const double* u, double* out, const double* mass,
+                          const double* fext, double dt, const int* poison) {
+#pragma clang fp contract(off)
+    if (*poison) return;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_up + n_dn) return;
+    double Q[3];
+    long long n;
+    if (j < n_up) {
+        n = up[j];
+        for (int c = 0; c < 3; ++c) Q[c] = up_sendP[3 * j + c];
+        const double* r = up_recvC + (long long)3 * nslot * j;
+        for (int s = 0; s < nslot; ++s)
+            for (int c = 0; c < 3; ++c) Q[c] += r[3 * s + c];
+    } else {
+        const int jj = j - n_up;
+        n = dn[jj];
+        for (int c = 0; c < 3; ++c) Q[c] = dn_recvP[3 * jj + c];
+        const int b = rp[n], m = rp[n + 1] - b;
+        for (int s = 0; s < nslot; ++s)
+            for (int c = 0; c < 3; ++c) Q[c] += s < m ? rows[3LL * ridx[b + s] + c] : 0.0;
+    }
+    const double m_ = mass[n];
+    const double dC = 0.0 * m_;
+    const double mdt2 = m_ / (dt * dt);
+    const double inv = 1.0 / (mdt2 + dC / 2.0 / dt);
+    for (int c = 0; c < 3; ++c) {
+        const double uc = u[3 * n + c];
+        const double up_ = saved[3 * j + c];
+        const double f = fext ? fext[3 * n + c] : 0.0;
         out[3 * n + c] = inv * (f - Q[c] + mdt2 * (2.0 * uc - up_) + dC / 2.0 / dt * up_);
     }
 }
@@ -361,6 +422,8 @@ int comm_reset(hakai_ctx* c) {
     return 0;
 }
 
+const std::vector<int>* comm_dn_nodes(const hakai_ctx* c) { return c->comm ? &c->comm->h_dn : nullptr; }
+
 int comm_pre_nodal(hakai_ctx* c) {
     Comm* m = c->comm;
     if (!m || m->n_up + m->n_dn == 0 || !m->pending) return 0;
@@ -396,7 +459,14 @@ int comm_post_nodal(hakai_ctx* c, double d_time) {
                                   hipMemcpyDeviceToDevice, c->stream));
         }
     }
-    if (!c->q_from_buf) {  // an uploaded Q already holds the global sum
+    if (!c->q_from_buf && c->own_valid) {  // the previous element step summed node forces itself
+        const int n = m->n_up + m->n_dn;
+        hipLaunchKernelGGL(k_fix_own, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn,
+                           m->n_dn, c->d_own_rp, c->d_own_ridx, c->d_own_rows, m->nslot, m->d_up_sendP[par],
+                           m->d_up_recvC, m->d_dn_recvP, m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass,
+                           c->contact ? c->d_fext : nullptr, d_time, c->d_poison);
+        HIPCHK(hipGetLastError());
+    } else if (!c->q_from_buf) {  // an uploaded Q already holds the global sum
         const int n = m->n_up + m->n_dn;
         hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
                            c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
@@ -413,8 +483,13 @@ int comm_post_element(hakai_ctx* c, long long step) {
     if (!m || m->n_up + m->n_dn == 0) return 0;
     const int par = (int)(step & 1);
     const int n = m->n_up + m->n_dn;
-    hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
-                       c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_dn_sendC[par]);
+    if (c->own_valid)  // this step's element kernel summed the node forces (owner-computed assembly)
+        hipLaunchKernelGGL(k_pack_own, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn,
+                           m->n_dn, c->d_own_rp, c->d_own_ridx, c->d_own_rows, c->d_own_q, m->nslot,
+                           m->d_up_sendP[par], m->d_dn_sendC[par]);
+    else
+        hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
+                           c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_dn_sendC[par]);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(m->ev_packed[par], c->stream));
     if (m->mode == 0) {
@@ -543,6 +618,9 @@ int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_nod
     m->nslot = nslot;
     m->n_up = (int)up.size();
     m->n_dn = (int)dn.size();
+    m->h_dn = dn;
+    c->own_built_g = -1;  // owner-assembly lists export every dn node's contributions: rebuilt
+    c->own_valid = false;
     HIPCHK(dalloc(&m->d_up, up.size()));
     HIPCHK(dalloc(&m->d_dn, dn.size()));
     for (int p = 0; p < 2; ++p) {

@@ -177,6 +177,7 @@ int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface 
 int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
 int comm_post_element(hakai_ctx* c, long long step); // pack interface forces, start exchange
 bool comm_is_local(const hakai_ctx* c);              // in-process group stepped in lockstep
+const std::vector<int>* comm_dn_nodes(const hakai_ctx* c);  // nodes shared with rank-1 (or null)
 int comm_rank(const hakai_ctx* c);
 int comm_size(const hakai_ctx* c);
 // All-gather of equal-size device blocks, one per rank, from per-parity send buffers (RCCL

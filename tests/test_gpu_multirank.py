@@ -406,3 +406,54 @@ def test_divided_contact_overflow_poisons_every_rank():
         assert np.array_equal(a.disp, g.disp) and np.array_equal(a.velo, g.velo)
         assert np.array_equal(a.integ_stress, g.integ_stress)
         sv.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_group_owner_assembly_bitexact(world):
+    """Owner-computed assembly on ranks with a communicator (the persistent kernel forced with
+    elem_pipe_min 0, several blocks per rank): the lower side's partial sum is its local Q
+    (own_q + rows) and the upper side's single contributions are exported rows (hakai_comm.cpp
+    k_pack_own / k_fix_own). Every rank equals one context -- with and without the mode -- bit for bit."""
+    glob = fast_deletion_bar(4, 4, 120)
+    n = 1500
+    tune = {"elem_pipe_min": 0, "elem_pipe_blocks": 6}
+    ref = {}
+    for own in (0, 1):
+        with Solver(glob) as sv:
+            for k, v in tune.items():
+                sv.set_tuning(k, v)
+            sv.set_tuning("own_assembly", own)
+            sv.step(1, n)
+            ref[own] = (sv.download(), [tuple(x) for x in sv.deleted()])
+    g, gdel = ref[1]
+    assert len(gdel) > 0
+    for k in ("disp", "disp_pre", "integ_stress", "element_flag", "Qe"):
+        assert np.array_equal(getattr(ref[0][0], k), getattr(g, k)), k
+    parts = [dist.slab_partition(glob, r, world, 4, 4) for r in range(world)]
+    svs = []
+    for r, (loc, diag, iface) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, world, 900 + world)
+        sv.set_interface(*iface)
+        svs.append(sv)
+    step_group(svs, 1, n)
+    dels = []
+    for sv, (loc, _, _) in zip(svs, parts):
+        assert sv.stat("own_steps") == n
+        st = sv.download()
+        dels += [tuple(x) for x in sv.deleted()]
+        n0, nl = loc.global_node_offset, loc.nNode
+        e0, el = loc.global_element_offset, loc.nElement
+        sl = slice(3 * n0, 3 * (n0 + nl))
+        assert np.array_equal(st.disp, g.disp[sl])
+        assert np.array_equal(st.disp_pre, g.disp_pre[sl])
+        gp = slice(8 * e0, 8 * (e0 + el))
+        assert np.array_equal(st.integ_stress, g.integ_stress[gp])
+        assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
+        assert np.array_equal(st.Qe, g.Qe[e0:e0 + el])
+    for sv in svs:
+        sv.close()
+    assert sorted(dels) == gdel
