@@ -14,10 +14,12 @@ interface exchange). Inputs are resident in HBM before timing starts.
 Workloads (BASELINE.json):
   N = 1 (default)  C3, the 2 M-hex elastoplastic tensile bar 20x20x5000 (Tensile5e steel_Ductile,
                    ENCASTRE at z=0, linear v_z field) -- the configuration the north star is quoted on.
-  N > 1 (weak)     each rank owns a 2 M-hex z-slab of the C5 bar 100x100x(200N) (uniform
-                   v_z = -1e5 mm/s into the clamped face); N = 8 is C5 (16 M hex). The line carries
-                   `single_gpu_same_slab`: the same run's rate of one rank's slab on its GPU alone
-                   (no exchange), so value / (N x that) is the weak-scaling efficiency on ONE workload.
+  N > 1 (weak)     each rank owns one C3 bar: the 20x20x(5000N) bar in N z-slabs of 20x20x5000
+                   (2 M hex each, the same velocity gradient, preload and plastic share as N = 1),
+                   so value_N / (N x value_1) compares the same per-GPU work; N = 8 is 16 M hex.
+                   --weak-shape c5: 2 M-hex z-slabs of the C5 bar 100x100x(200N) instead (uniform
+                   v_z = -1e5 mm/s into the clamped face). The line carries `single_gpu_same_slab`:
+                   the same run's rate of one rank's slab on its GPU alone (no exchange).
   --strong         the whole C5 bar 100x100x1600 (16 M hex) split over N (N = 1 holds all 16 M),
                    so value_N / value_1 is the strong-scaling speed-up ("scaling": "strong").
 Before warm-up an untimed preload advances the bar into its plastic regime (the share of yielding
@@ -57,6 +59,8 @@ def parse():
     ap.add_argument("--preload", type=int, default=-1, help="untimed steps before warm-up (-1: config default)")
     ap.add_argument("--layers", type=int, default=0, help="override z layers (tests / quick runs)")
     ap.add_argument("--strong", action="store_true", help="strong scaling: C5 16 M hex split over the ranks")
+    ap.add_argument("--weak-shape", choices=("c3", "c5"), default="c3",
+                    help="N > 1 weak scaling: a C3 bar per rank (default) or 2 M-hex slabs of the C5 bar")
     ap.add_argument("--local-ranks", type=int, default=0,
                     help="rehearsal: the N-rank path as an in-process group of R contexts on one GPU")
     ap.add_argument("--same-slab-ref", type=int, default=1,
@@ -69,7 +73,7 @@ def parse():
     return ap.parse_args()
 
 
-def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=False):
+def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=False, weak_shape="c3"):
     """Returns (local Model, local diag_M, interface arrays or None, config dict, preload)."""
     from hakai import mesh
     from hakai.dist import slab_partition
@@ -93,6 +97,16 @@ def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=Fal
                "elements": m.nElement, "nodes": m.nNode, "partition": "single GPU"}
         diag, _ = m.lumped_mass()
         return m, diag, None, cfg, 400
+    if weak_shape == "c3":
+        per = layers_override or 5000
+        glob = mesh.bar_model(20, 20, per * world, mesh.steel_ductile(), lambda z, L: 5e5 * z / per,
+                              name="C3xN")
+        local, diag, iface = slab_partition(glob, rank, world, nx=20, ny=20)
+        cfg = {"workload": "C3 per rank: 20x20x%d elastoplastic tensile bar (steel_Ductile, deletion on, v_z = "
+               "5e5 z/%d mm/s), %d z-slabs of 20x20x%d (2 M hex each, the N = 1 workload)"
+               % (per * world, per, world, per), "elements": glob.nElement, "nodes": glob.nNode,
+               "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"}
+        return local, diag, iface, cfg, 400
     per = layers_override or 200
     glob = mesh.config_c5(layers=per * world)
     local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
@@ -172,7 +186,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     # this process's subdomains: one per rank, or R in-process ranks on one device
     ids = list(range(R)) if R else [rank]
-    built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong) for r in ids]
+    built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong, a.weak_shape) for r in ids]
     cfg = built[0][3]
     preload = built[0][4] if a.preload < 0 else a.preload
     svs = []

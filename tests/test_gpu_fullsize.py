@@ -7,7 +7,7 @@
   reference-order kernel (elem_exact) run from the same hand-off state equals the oracle bit for bit.
 * C3: size-independent properties of one full step: every element's 8 nodal forces sum to zero
   (sum_i dN_i/dx = 0, so B^T sigma has no net force), and the assembled Q obeys the same balance.
-* C5 family, the bench's N=2 weak-scaling case (100x100x400, 2 z-slabs of 2 M hex): the 2-rank
+* C5 family, the bench's --weak-shape c5 N=2 case (100x100x400, 2 z-slabs of 2 M hex): the 2-rank
   in-process group (same partition, pack / fix kernels and exchange protocol as the RCCL path) is
   bit-identical to one context holding all 4 M elements.
 """
