@@ -76,7 +76,7 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key, divide=1):
+def _run_contact_group(glob, world, n_steps, key, divide=1, tune=None):
     """Range-partitioned contact model on an in-process group, each rank mirroring the global
     contact model (hakai_set_contact_global); divide=1 (default): each rank searches its share of
     the triangles and the events are all-gathered."""
@@ -90,8 +90,12 @@ def _run_contact_group(glob, world, n_steps, key, divide=1):
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
         sv.set_tuning("contact_divide", divide)
+        for k, v in (tune or {}).items():
+            sv.set_tuning(k, v)
         svs.append(sv)
     step_group(svs, 1, n_steps)
+    if tune and tune.get("own_assembly"):
+        assert all(sv.stat("own_steps") == n_steps for sv in svs)
     out = [(loc, l2g, sv.download(), [tuple(x) for x in sv.deleted()], sv.contact_stats())
            for sv, (loc, _, _, l2g, _) in zip(svs, parts)]
     for sv in svs:
@@ -457,3 +461,21 @@ def test_local_group_owner_assembly_bitexact(world):
     for sv in svs:
         sv.close()
     assert sorted(dels) == gdel
+
+
+def test_contact_group_owner_assembly_bitexact():
+    """Contact on a communicator with owner-computed assembly (persistent kernel forced): the mirror's
+    contact force enters the nodal update and the interface fix beside the owner-computed Q;
+    every rank equals one context with the same mode, deletions included."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(8, 8, 2), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    tune = {"elem_pipe_min": 0, "own_assembly": 1}
+    with Solver(glob) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+        assert sv.stat("own_steps") == glob.n_steps
+    parts = _run_contact_group(glob, 2, glob.n_steps, key=5150, tune=tune)
+    _assert_group_equals_single(glob, parts, g, gdel)
