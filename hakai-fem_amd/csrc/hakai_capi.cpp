@@ -816,8 +816,8 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 // result is bit-identical. Rows are numbered by super-batch (an export entry carries up to 4
 // contributions of any nodes to consecutive rows); own_ridx lists each node's rows in element order.
 // One 16-B entry per node segment piece (or exported
-// contribution) per super-batch of S = 2 batches (1 when 2 would need more than 256 entries),
-// one thread each (layout: hakai_kernels.hip
+// contribution) per super-batch of S = 2 batches (1 when 2 would need more than 512 entries),
+// one or two per thread (layout: hakai_kernels.hip
 // own_pass). Slots are allocated per block over the super-batches a sum is open; a mesh needing more than kOwnSlots open
 // sums in one block, or a node with > 8 incidences, does not use the mode.
 // ---------------------------------------------------------------------------------------------
@@ -945,7 +945,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
     }
     std::vector<int> off(nb + 1, 0);
     for (long long b = 0; b < nb; ++b) {
-        if (per[b].size() > 256) return false;  // one entry per thread
+        if (per[b].size() > 512) return false;  // two entries per thread at most (own_pass)
         off[b + 1] = off[b] + (int)per[b].size();
     }
     const long long ne = off[nb];

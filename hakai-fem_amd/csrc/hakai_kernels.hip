@@ -725,8 +725,8 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
 // the pipeline stay in flight across the pass. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
 // ---------------------------------------------------------------------------------------------
 constexpr int kOwnSlots = 1024;            // LDS running sums per block (24 KB)
-// batches per super-batch: 2, or 1 for meshes whose 64-element super-batches need more than 256
-// entries (wide cross-sections); the host picks (own_build), the kernel is instantiated for both
+// batches per super-batch: 2, or 1 for meshes whose 64-element super-batches need more than 512
+// entries; the host picks (own_build), the kernel is instantiated for both
 constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
 enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
 
@@ -747,9 +747,8 @@ __device__ __forceinline__ int own_lane(int4 en, int j) {
     return j < 7 ? (int)((lo >> (9 * j)) & 511) : (int)(((unsigned)en.y >> 18) & 511);
 }
 
-__device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, const double* s_fe, double* s_part) {
+__device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const double* s_fe, double* s_part) {
 #pragma clang fp contract(off)
-    lds_barrier();  // the super-batch's forces are in s_fe, the previous pass is done with s_part
     const int slot = en.y & 1023, flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;
     double* dump = a.own_dump + 8 * (long long)blockIdx.x;
     double v[3];
@@ -777,6 +776,20 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, const doubl
     double* dst = (flags & kOwnFin) ? a.own_q + 3 * (long long)en.x : dump;
 #pragma unroll
     for (int c = 0; c < 3; ++c) dst[c] = v[c];
+}
+
+// One summing pass: the prefetched entry of this thread, then -- only for a super-batch with more
+// than kBlock entries (wide cross-sections) -- a second one, loaded here (that pass waits for it).
+// Entries of one pass touch distinct LDS slots, so the two rounds need no barrier between them.
+__device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long sb, const double* s_fe,
+                                         double* s_part) {
+    lds_barrier();  // the super-batch's forces are in s_fe, the previous pass is done with s_part
+    own_entry(a, en, s_fe, s_part);
+    const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
+    if (o1 - o0 > kBlock) {  // block-uniform
+        const int idx = o0 + kBlock + (int)threadIdx.x;
+        own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe, s_part);
+    }
 }
 
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
@@ -864,7 +877,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
             if ((i + 1) % S == 0 || i + 1 == count)
-                own_pass(a, ent_cur, s_fe + ((i / S) & 1) * kOwnFe, s_part);
+                own_pass(a, ent_cur, sb_of(i), s_fe + ((i / S) & 1) * kOwnFe, s_part);
             ent_cur = ent_nxt;
         }
         cur = nxt;

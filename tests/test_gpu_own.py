@@ -98,9 +98,9 @@ def test_own_wide_section_finer_grid_or_fallback():
 
 
 @pytest.mark.parametrize("layers", [12])
-def test_own_wide_section_single_batch_passes(layers):
-    """100x100 cross-section (C5's): 64-element super-batches would need more than 256 entries, so
-    the lists use one batch per summing pass; bit-identical to the fe path."""
+def test_own_wide_section_two_entry_passes(layers):
+    """100x100 cross-section (C5's): some 64-element super-batches need more than 256 entries, so
+    those passes take a second entry per thread; bit-identical to the fe path."""
     m = small_bar(100, 100, layers, n_steps=100, v_end=5e5)
     g0, _, _ = _run(m, [(1, 100)], {}, 0)
     with Solver(m) as sv:
@@ -108,7 +108,7 @@ def test_own_wide_section_single_batch_passes(layers):
         sv.step(1, 100)
         g1 = sv.download()
         assert sv.stat("own_steps") == 100
-        assert sv.stat("own_superbatch") == 1
+        assert sv.stat("own_superbatch") == 2
     _same(g1, g0)
 
 

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u bench.py --local-ranks 8 --steps 50 --warmup 5 > gpurun_out/s2k_local8.json 2> gpurun_out/s2k_local8.err
+timeout -k 10 500 python -u bench.py --local-ranks 8 --steps 50 --warmup 5 > gpurun_out/s2k_local8.json 2> gpurun_out/s2k_local8.err
 rc=$?; echo "local8 rc=$rc"; tail -1 gpurun_out/s2k_local8.json; [ $rc -eq 0 ] || exit $rc
 export HAKAI_RCCL_SHARED_GPU=1
 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 30 --warmup 5 > gpurun_out/s2k_rccl2.json 2> gpurun_out/s2k_rccl2.err
