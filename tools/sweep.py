@@ -36,7 +36,7 @@ sv.step(1, 400)
 sv.sync()
 t = 401
 res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
-DEFAULTS = {"elem_exact_pipe": 0, "elem_minw": 2, "elem_exact": 0, "diag_no_assembly": 0, "diag_atomic_q": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_map": 1, "fe_layout": 0, "nodal_early": 1, "elem_gp_nt": 3, "nodal_fe_nt": 0, "nodal_reverse": 1, "tblock_mb": 0, "own_assembly": 0}
+DEFAULTS = {"elem_exact_pipe": 0, "elem_minw": 2, "elem_exact": 0, "diag_no_assembly": 0, "diag_atomic_q": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_map": 1, "fe_layout": 0, "nodal_early": 1, "elem_gp_nt": 3, "nodal_fe_nt": 0, "nodal_reverse": 1, "tblock_mb": 0, "own_assembly": 1}
 for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
