@@ -76,6 +76,7 @@ static void own_free(hakai_ctx* c) {
     dfree(c->d_own_ridx);
     dfree(c->d_own_dump);
     c->own_built_g = -1;
+    c->own_for_g0 = -1;
     c->own_valid = false;
 }
 
@@ -1003,15 +1004,16 @@ static bool own_use(hakai_ctx* c) {
         return false;
     const long long G0 = own_grid(c);
     if (G0 <= 0) return false;
-    if (c->own_built_g > 0) return true;
-    if (c->own_built_g == -2 - G0) return false;  // tried for this grid: the mesh does not fit
+    if (c->own_for_g0 == G0) return c->own_built_g > 0;  // built (or found not to fit) for this grid
     const long long nb = c->nEp / 32;
+    bool ok = false;
     for (long long G : {G0, 8 * G0}) {
         if (G > nb) break;
-        if (own_build(c, G, 2) || own_build(c, G, 1)) return true;
+        if ((ok = own_build(c, G, 2) || own_build(c, G, 1))) break;
     }
-    c->own_built_g = -2 - G0;
-    return false;
+    c->own_for_g0 = G0;
+    if (!ok) c->own_built_g = -2;
+    return ok;
 }
 
 // One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take

@@ -620,6 +620,7 @@ int hakai_set_interface(hakai_ctx* c, int64_t n_shared, const int64_t* local_nod
     m->n_dn = (int)dn.size();
     m->h_dn = dn;
     c->own_built_g = -1;  // owner-assembly lists export every dn node's contributions: rebuilt
+    c->own_for_g0 = -1;
     c->own_valid = false;
     HIPCHK(dalloc(&m->d_up, up.size()));
     HIPCHK(dalloc(&m->d_dn, dn.size()));

@@ -150,6 +150,7 @@ struct hakai_ctx {
     // the later contributions as rows) instead of the per-element fe array.
     int own_assembly = 1;              // tuning value (1 = use when eligible; env HAKAI_OWN_ASSEMBLY)
     long long own_built_g = -1;        // grid the lists were built for (-1 none, -2 mesh not suitable)
+    long long own_for_g0 = -1;         // persistent-kernel grid that build was for (a change rebuilds)
     bool own_valid = false;            // d_own_q/d_own_rows hold the last element step's sums
     int* d_own_off = nullptr;          // [nb+1] per-batch entry offsets
     int* d_own_list = nullptr;         // 4 ints per entry (+ one no-op entry at own_nop)

@@ -178,3 +178,21 @@ def test_own_isolated_node_and_ragged_batch():
         assert np.array_equal(getattr(g1, k), getattr(g0, k), equal_nan=True), k
     assert np.all(g1.Q[3 * extra - 3:] == 0.0)
     assert np.all(np.isfinite(g1.disp[:3 * extra - 3]))
+
+
+def test_own_grid_change_between_calls_rebuilds():
+    """elem_pipe_blocks changed between calls: the owner lists are rebuilt for the new grid (the
+    call boundary leaves fe valid for the first step), results unchanged."""
+    m = small_bar(6, 5, 300, n_steps=600, v_end=5e5)
+    g0, _, _ = _run(m, [(1, 600)], PIPE, 0)
+    with Solver(m) as sv:
+        sv.set_tuning("elem_pipe_min", 0)
+        seen = []
+        for t0, n, blocks in ((1, 201, 32), (202, 200, 12), (402, 199, 40)):
+            sv.set_tuning("elem_pipe_blocks", blocks)
+            sv.step(t0, n)
+            seen.append(sv.stat("own_entries"))
+        g1 = sv.download()
+        assert sv.stat("own_steps") == 600
+    assert len(set(seen)) == 3  # three partitions, three list sets
+    _same(g1, g0)
