@@ -43,6 +43,13 @@ def test_rccl_interface_exchange_bitexact(n):
     assert f"RCCL {n}-rank interface exchange vs 1 context bit-exact: True" in out
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_rccl_interface_exchange_owner_assembly_bitexact(n):
+    """The same over RCCL with owner-computed assembly on every rank (k_pack_own / k_fix_own)."""
+    out = _torchrun("tools/rccl_exchange_check.py", n, "--own")
+    assert f"RCCL {n}-rank interface exchange (owner-computed assembly) vs 1 context bit-exact: True" in out
+
+
 def test_rccl_contact_bitexact():
     """Two-body impact with contact deletions over 2 RCCL ranks, divided and replicated search."""
     out = _torchrun("tools/rccl_contact_check.py", 2)
