@@ -260,67 +260,33 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.del_step = c->d_del_step;
     ea.step_i = 0;
     ea.any_plastic = c->any_plastic ? 1 : 0;
-    ea.variant = c->elem_variant;
     // nEp / 32 = batches of 32 elements (kEPB); small meshes take the one-batch-per-block kernel
     ea.pipe_blocks = (c->nEp / 32 >= (long long)c->pipe_min * c->pipe_blocks) ? c->pipe_blocks : 0;
-    // the reference-order arithmetic keeps ~50 more live registers: its pipelined form spills and
-    // runs slower than the one-batch kernel (C3: 1.49 vs 1.29 ms, profiles/r02_exact_kernel_variants.log)
-    if (c->elem_exact && !c->exact_pipe) ea.pipe_blocks = 0;
-    ea.pipe_map = c->pipe_map;
     ea.gp_nt = c->gp_nt;
-    ea.cstride = c->fe_layout == 1 ? c->nEp : 1;
     ea.nmat = c->nmat;
     ea.exact = c->elem_exact;
     ea.pusai = c->d_pusai;
-    ea.fe_mask = c->diag_no_assembly ? 0 : -1;
-    ea.qatomic = c->diag_atomic_q ? c->d_qbuf : nullptr;
     ea.poison = c->d_poison;
     return ea;
 }
 
-// Base offset and component stride of (element e, local node k) in a force layout.
-static inline long long fe_base(const hakai_ctx* c, int layout, long long e, int k) {
-    return layout == 1 ? 3LL * k * c->nEp + e : 24 * e + 3 * k;
-}
-static inline long long fe_cs(const hakai_ctx* c, int layout) { return layout == 1 ? c->nEp : 1; }
-
-// Element forces <-> the reference's Qe (24 x nE) whatever the device layout.
+// Element forces [nEp][8][3] <-> the reference's Qe (24 x nE): the same layout.
 static int fe_download_qe(hakai_ctx* c, double* Qe) {
-    if (c->fe_layout == 0) {
-        HIPCHK(hipMemcpyAsync(Qe, c->d_fe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        return 0;
-    }
-    std::vector<double> fe((size_t)c->fe_len);
-    HIPCHK(hipMemcpyAsync(fe.data(), c->d_fe, fe.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(Qe, c->d_fe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    const long long cs = fe_cs(c, c->fe_layout);
-    for (long long e = 0; e < c->nE; ++e)
-        for (int k = 0; k < 8; ++k)
-            for (int q = 0; q < 3; ++q) Qe[24 * e + 3 * k + q] = fe[fe_base(c, c->fe_layout, e, k) + q * cs];
     return 0;
 }
 
 static int fe_upload_qe(hakai_ctx* c, const double* Qe) {
-    if (c->fe_layout == 0) {
-        HIPCHK(hipMemcpyAsync(c->d_fe, Qe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        return 0;
-    }
-    std::vector<double> fe((size_t)c->fe_len, 0.0);
-    const long long cs = fe_cs(c, c->fe_layout);
-    for (long long e = 0; e < c->nE; ++e)
-        for (int k = 0; k < 8; ++k)
-            for (int q = 0; q < 3; ++q) fe[fe_base(c, c->fe_layout, e, k) + q * cs] = Qe[24 * e + 3 * k + q];
-    HIPCHK(hipMemcpyAsync(c->d_fe, fe.data(), fe.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_fe, Qe, 24 * (size_t)c->nE * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 
-// Incidence tables (CSR and padded) as bases of `layout`; padding -> the zero base 24nEp.
-static int fe_upload_incidence(hakai_ctx* c, int layout) {
+// Incidence tables (CSR and padded) as force row bases 24e + 3k; padding -> the zero base 24nEp.
+static int fe_upload_incidence(hakai_ctx* c) {
     std::vector<int> inc(c->h_inc0.size());
-    for (size_t j = 0; j < inc.size(); ++j) inc[j] = (int)fe_base(c, layout, c->h_inc0[j] >> 3, c->h_inc0[j] & 7);
+    for (size_t j = 0; j < inc.size(); ++j) inc[j] = 24 * (c->h_inc0[j] >> 3) + 3 * (c->h_inc0[j] & 7);
     if (!inc.empty())
         HIPCHK(hipMemcpyAsync(c->d_inc, inc.data(), inc.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     if (c->d_inc8) {
@@ -331,19 +297,6 @@ static int fe_upload_incidence(hakai_ctx* c, int layout) {
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
-}
-
-// Switch the element-force layout, converting the current forces (the next step's Q).
-static int fe_set_layout(hakai_ctx* c, int layout) {
-    if (layout == c->fe_layout) return 0;
-    std::vector<double> qe(24 * (size_t)c->nE);
-    int r = c->state_ok ? fe_download_qe(c, qe.data()) : 0;
-    if (r) return r;
-    if ((r = fe_upload_incidence(c, layout))) return r;
-    HIPCHK(hipMemsetAsync(c->d_fe, 0, (size_t)c->fe_len * sizeof(double), c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->fe_layout = layout;
-    return c->state_ok ? fe_upload_qe(c, qe.data()) : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -375,7 +328,6 @@ int hakai_create(hakai_ctx** out, int device) {
                     prop.gcnArchName);
     hakai_ctx* c = new hakai_ctx();
     c->device = device;
-    if (const char* v = std::getenv("HAKAI_ELEM_MINW")) c->elem_variant = std::atoi(v);
     if (const char* v = std::getenv("HAKAI_PIPE_BLOCKS")) c->pipe_blocks = std::atoi(v);
     // HAKAI_GRAPH=n: steps per captured graph (0 = stream mode). rocprofv3 --kernel-trace crashes
     // the host process on any hipGraph launch with this ROCm (tools/graph_probe.hip alone
@@ -532,12 +484,11 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     HIPCHK(hipMemcpyAsync(c->d_inc_ptr, ptr.data(), (nN + 1) * sizeof(int), hipMemcpyHostToDevice, s));
     if (maxinc <= 8) HIPCHK(dalloc(&c->d_inc8, 8 * (size_t)nN));  // padded table for the unrolled gather
     HIPCHK(hipStreamSynchronize(s));  // host vectors go out of scope
-    c->fe_layout = 0;
     c->max_inc = maxinc;
     c->h_ptr = ptr;
     c->h_inc0 = inc;
     {
-        int r = fe_upload_incidence(c, 0);
+        int r = fe_upload_incidence(c);
         if (r) return r;
     }
     c->h_coord.assign(coordmat, coordmat + 3 * nN);
@@ -546,7 +497,6 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     c->h_young.resize((size_t)nMat);
     for (int i = 0; i < nMat; ++i) c->h_young[i] = mats[i].young;
     c->model_ok = true;
-    c->tb_built_mb = -1;  // two-step schedule: rebuilt for this mesh on first use
     c->state_ok = false;
     return hakai_reset_state(c, 0, nullptr, nullptr, 1.0);
 }
@@ -764,7 +714,7 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
         } else {
             double* tmp = nullptr;
             HIPCHK(dalloc(&tmp, fn));
-            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, c->fe_layout == 1 ? c->nEp : 1, tmp, c->nN, s));
+            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, tmp, c->nN, s));
             HIPCHK(hipMemcpyAsync(st->Q, tmp, fn * sizeof(double), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             dfree(tmp);
@@ -918,6 +868,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
     rp[nN] = (int)ridx.size();
     if (rows > (1LL << 31) - 1) return false;
     // slots: a sum open over super-batches [s0, s1] holds its slot through s1; reuse strictly after
+    int max_slots = 1;
     for (long long lb = 0; lb < G; ++lb) {
         auto& v = segs[lb];
         std::sort(v.begin(), v.end(), [](const Seg& x, const Seg& y) { return x.s0 < y.s0; });
@@ -939,6 +890,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
                 slot = next++;
             }
             if (slot >= kOwnSlotsHost) return false;
+            max_slots = std::max(max_slots, slot + 1);
             for (auto& r : sg.refs) per[r.first][r.second].slot = slot;
             busy.emplace_back(sg.s1, slot);
             std::push_heap(busy.begin(), busy.end(), cmp);
@@ -981,6 +933,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
     HIPCHK(hipMemsetAsync(c->d_own_q, 0, 3 * (size_t)nN * sizeof(double), s));  // nodes without elements
     HIPCHK(hipStreamSynchronize(s));
     c->own_nop = (int)ne;
+    c->own_slots = max_slots;
     c->own_rows = rows;
     c->own_entries = ne;
     c->own_built_g = G;
@@ -999,8 +952,7 @@ static long long own_grid(const hakai_ctx* c) {
 // grid is the persistent kernel's, or 8x that (blocks then run in waves) when the default ranges
 // span so much of a wide cross-section that too many sums stay open in a block.
 static bool own_use(hakai_ctx* c) {
-    if (!c->own_assembly || c->elem_exact || c->fe_layout != 0 || c->diag_atomic_q || c->diag_no_assembly ||
-        c->tblock_mb || c->nmat > hk::kMaxLdsMats || (c->gp_nt != 0 && c->gp_nt != 3) || c->nE <= 0)
+    if (!c->own_assembly || c->nmat > hk::kMaxLdsMats || c->nE <= 0)
         return false;
     const long long G0 = own_grid(c);
     if (G0 <= 0) return false;
@@ -1039,20 +991,13 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.mass = c->d_mass;
     na.inc_ptr = c->d_inc_ptr;
     na.inc = c->d_inc;
-    na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
-    na.cstride = c->fe_layout == 1 ? c->nEp : 1;
-    na.early = c->nodal_early;
-    na.fe_nt = c->nodal_fe_nt;
-    na.reverse = c->nodal_reverse;
+    na.inc8 = c->d_inc8;
     na.fe = c->d_fe;
-    na.qbuf = (c->q_from_buf || c->diag_no_assembly || c->diag_atomic_q) ? c->d_qbuf : nullptr;
+    na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
     na.fext = nullptr;
     na.nN = c->nN;
     na.dt = d_time;
     na.bc_of_node = nullptr;
-    na.two_step = 0;
-    na.r1_lo = na.r1_hi = na.r2_lo = na.r2_hi = 0;
-    na.ct2 = 0.0;
     // owner-computed assembly: Q from the previous element step's sums (else the fe gather)
     const bool own = own_use(c);
     const bool own_q = c->own_valid && !na.qbuf;
@@ -1110,8 +1055,6 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     }
     c->cur = 1 - c->cur;  // disp <- disp_new, disp_pre <- disp (:626-627)
     c->q_from_buf = false;
-    if (c->diag_atomic_q)  // the element kernel adds this step's forces into it
-        HIPCHK(hipMemsetAsync(c->d_qbuf, 0, 3 * (size_t)c->nN * sizeof(double), s));
     // element update (:662-667) + triaxiality (:677) + ductile deletion (:684-764)
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
@@ -1121,6 +1064,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
         ea.own_off = c->d_own_off;
         ea.own_list = reinterpret_cast<const int4*>(c->d_own_list);
         ea.own_nop = c->own_nop;
+        ea.own_slots = c->own_slots;
         ea.own_q = c->d_own_q;
         ea.own_rows = c->d_own_rows;
         ea.own_dump = c->d_own_dump;
@@ -1140,143 +1084,6 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     if (rc) return rc;
     c->steps_done++;
     c->last_dt = d_time;
-    return 0;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Two-step chunked schedule (tuning "tblock_mb"). Steps s and s+1 are the same computations as two
-// step_once calls, reordered: element chunk it of step s, then the nodes of step s+1 whose incident
-// elements have all finished step s, then the elements of step s+1 whose nodes all have. Every
-// node still sums its incidences in element order and every element runs the same code, so the
-// result is bit-identical to stream mode; the gain is that step s+1 meets its Gauss-point state
-// (stored by step s one chunk earlier), the element forces and the node rows in the 256 MB Infinity
-// Cache. Iteration it launches
-//   nodal:   step s on nodes [A[it], A[it+1])  +  step s+1 on nodes [B[it-1], B[it])
-//   element: step s on batches [E[it], E[it+1]) + step s+1 on batches [D[it-1], D[it])
-// (it = 0..C; missing neighbours are empty ranges). Hazards, for any numbering:
-//  * step s on element e needs u_s of its nodes: they are < A[it+1] (A = 1 + max node of the
-//    elements so far), and overwriting fe_{s-1}(e) is safe because every node of e has gathered;
-//  * step s+1 on node n needs fe_s of every incident element: max incident element < E[it]·32;
-//    it overwrites u_{s-1}(n), which only the (finished) step-s elements around n read;
-//  * step s+1 on element e needs u_{s+1} of its nodes (< B[it]) and its own state_s.
-// Contiguous ranges come from prefix maxima, so a badly numbered mesh only loses the overlap (the
-// whole pair ends up in the last iteration), never correctness.
-static void tblock_build(hakai_ctx* c) {
-    const long long nE = c->nE, nN = c->nN, nb = c->nEp / 32;
-    const long long per_el = 8LL * 8 * (c->any_plastic ? 14 : 12);  // Gauss-point state bytes per element
-    const long long cb = std::max(1LL, ((long long)c->tblock_mb << 20) / per_el / 32);
-    const long long C = (nb + cb - 1) / cb;
-    std::vector<long long> pm_node(nE), pm_inc(nN, -1);  // prefix max of max node per element; of max incident element
-    long long run = -1;
-    for (long long e = 0; e < nE; ++e) {
-        for (int k = 0; k < 8; ++k) {
-            const long long n = c->h_conn[8 * e + k];
-            run = std::max(run, n);
-            pm_inc[n] = std::max(pm_inc[n], e);
-        }
-        pm_node[e] = run;
-    }
-    for (long long n = 1; n < nN; ++n) pm_inc[n] = std::max(pm_inc[n], pm_inc[n - 1]);
-    c->tb_E.assign(C + 1, 0);
-    c->tb_A.assign(C + 1, 0);
-    c->tb_B.assign(C + 1, 0);
-    c->tb_D.assign(C + 1, 0);
-    for (long long it = 1; it <= C; ++it) {
-        if (it == C) {
-            c->tb_E[it] = nb;
-            c->tb_A[it] = c->tb_B[it] = nN;
-            c->tb_D[it] = nb;
-            break;
-        }
-        const long long eb = it * cb, ebound = std::min(nE, 32 * eb);  // elements [0, ebound) done at step s
-        c->tb_E[it] = eb;
-        c->tb_A[it] = ebound > 0 ? std::min(nN, pm_node[ebound - 1] + 1) : 0;
-        // nodes [0, B): every incident element < ebound (and already updated for step s)
-        const long long b = std::lower_bound(pm_inc.begin(), pm_inc.end(), ebound) - pm_inc.begin();
-        c->tb_B[it] = std::min(b, c->tb_A[it]);
-        // elements [0, D): every node < B; whole batches only
-        const long long d = std::lower_bound(pm_node.begin(), pm_node.end(), c->tb_B[it]) - pm_node.begin();
-        c->tb_D[it] = std::min(d / 32, eb);
-    }
-    for (long long it = 1; it <= C; ++it) {  // monotone by construction; keep it explicit
-        c->tb_A[it] = std::max(c->tb_A[it], c->tb_A[it - 1]);
-        c->tb_B[it] = std::max(c->tb_B[it], c->tb_B[it - 1]);
-        c->tb_D[it] = std::max(c->tb_D[it], c->tb_D[it - 1]);
-    }
-    c->tb_built_mb = c->tblock_mb;
-}
-
-static bool tblock_eligible(const hakai_ctx* c) {
-    return c->tblock_mb > 0 && !c->comm && !c->contact && !c->q_from_buf && !c->diag_atomic_q &&
-           !c->diag_no_assembly && c->nE > 0 && c->nN > 0 && (c->nbc == 0 || c->d_bc_of_node);
-}
-
-// Steps t and t+1 with the chunked schedule (stream mode). last: the call ends with step t+1.
-static int step_pair(hakai_ctx* c, double t, double d_time, bool last) {
-    if (c->tb_built_mb != c->tblock_mb) tblock_build(c);
-    hipStream_t s = c->stream;
-    const int cur0 = c->cur;
-    const long long C = (long long)c->tb_E.size() - 1;
-    hk::NodalArgs na;
-    std::memset(&na, 0, sizeof na);
-    na.u = c->d_u[cur0];               // step s: u_{s-1}; out: u_{s-2} -> u_s (range 2 swaps them)
-    na.u_pre_out = c->d_u[1 - cur0];
-    na.mass = c->d_mass;
-    na.inc_ptr = c->d_inc_ptr;
-    na.inc = c->d_inc;
-    na.inc8 = c->fe_layout == 0 ? c->d_inc8 : nullptr;
-    na.cstride = c->fe_layout == 1 ? c->nEp : 1;
-    na.early = c->nodal_early;
-    na.fe_nt = c->nodal_fe_nt;
-    na.reverse = c->nodal_reverse;
-    na.fe = c->d_fe;
-    na.nN = c->nN;
-    na.dt = d_time;
-    na.poison = c->d_poison;
-    na.two_step = 1;
-    if (c->nbc > 0) {
-        na.bc_of_node = c->d_bc_of_node;
-        na.bc.dof = c->d_bc_dof;
-        na.bc.grp = c->d_bc_grp;
-        na.bc.val = c->d_bc_val;
-        na.bc.n = c->nbc;
-        na.bc.amp_n = c->d_amp_n;
-        na.bc.amp_off = c->d_amp_off;
-        na.bc.amp_t = c->d_amp_t;
-        na.bc.amp_v = c->d_amp_v;
-        na.bc.dt = d_time;
-        na.bc.poison = c->d_poison;
-    }
-    na.bc.ct = t * d_time;
-    na.ct2 = (t + 1.0) * d_time;
-    hk::ElemArgs ea = elem_args(c);
-    ea.u = c->d_u[1 - cur0];           // step s: u_s, u_{s-1} (range 2: u_{s+1}, u_s)
-    ea.u_pre = c->d_u[cur0];
-    ea.step_i = (int)t;
-    ea.two_step = 1;
-    EventPair ep;
-    for (long long it = 0; it <= C; ++it) {
-        const bool has1 = it < C, has2 = it > 0;
-        na.r1_lo = has1 ? c->tb_A[it] : 0;
-        na.r1_hi = has1 ? c->tb_A[it + 1] : 0;
-        na.r2_lo = has2 ? c->tb_B[it - 1] : 0;
-        na.r2_hi = has2 ? c->tb_B[it] : 0;
-        hkc::prof_begin(c, HAKAI_K_NODAL, &ep);
-        HIPCHK(hk::launch_nodal(na, s));
-        hkc::prof_end(c, &ep);
-        ea.r1_lo = has1 ? c->tb_E[it] : 0;
-        ea.r1_hi = has1 ? c->tb_E[it + 1] : 0;
-        ea.r2_lo = has2 ? c->tb_D[it - 1] : 0;
-        ea.r2_hi = has2 ? c->tb_D[it] : 0;
-        hkc::prof_begin(c, HAKAI_K_ELEMENT, &ep);
-        HIPCHK(hk::launch_element(ea, c->has_ductile, last, s));
-        hkc::prof_end(c, &ep);
-    }
-    c->q_from_buf = false;
-    c->own_valid = false;
-    c->steps_done += 2;
-    c->last_dt = d_time;
-    c->tb_pairs++;
     return 0;
 }
 
@@ -1384,13 +1191,6 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     while (it < n_steps) {
         const double t = t_first + (double)it;
         int rc;
-        if (it + 2 <= n_steps && tblock_eligible(c)) {
-            rc = step_pair(c, t, d_time, it + 2 == n_steps);
-            c->tdev_next = -1;
-            it += 2;
-            if (rc) return rc;
-            continue;
-        }
         // the call's last step stays in stream mode: it also stores triaxiality for downloads
         // (eligibility of step t implies it for the steps after it: step t clears every one-off
         // condition)
@@ -1459,11 +1259,11 @@ int hakai_graph_steps(hakai_ctx* c, int64_t* n) {
 int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(HAKAI_ERR_ARG, "null");
     if (!std::strcmp(key, "graph_steps")) *value = c->graph_steps;
-    else if (!std::strcmp(key, "tblock_pairs")) *value = c->tb_pairs;
     else if (!std::strcmp(key, "own_steps")) *value = c->own_steps;
     else if (!std::strcmp(key, "own_rows")) *value = c->own_built_g > 0 ? c->own_rows : -1;
     else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
     else if (!std::strcmp(key, "own_superbatch")) *value = c->own_built_g > 0 ? c->own_s : 0;
+    else if (!std::strcmp(key, "own_slots")) *value = c->own_built_g > 0 ? c->own_slots : 0;
     else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1499,49 +1299,19 @@ int hakai_deleted(hakai_ctx* c, int64_t* n_deleted, int64_t* log, int64_t cap) {
 int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
     if (!c || !key) return fail(HAKAI_ERR_ARG, "set_tuning: null");
-    if (!std::strcmp(key, "elem_minw")) {
-        if (value != 2 && value != 3 && value != 4) return fail(HAKAI_ERR_ARG, "elem_minw must be 2, 3 or 4");
-        c->elem_variant = (int)value;
-        return 0;
-    }
     if (!std::strcmp(key, "elem_pipe_blocks")) {
         if (value < 0 || value > 65536) return fail(HAKAI_ERR_ARG, "elem_pipe_blocks out of range");
         c->pipe_blocks = (int)value;
         return 0;
     }
-    if (!std::strcmp(key, "fe_layout")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "fe_layout must be 0 or 1");
-        HIPCHK(hipSetDevice(c->device));
-        return fe_set_layout(c, (int)value);
-    }
-    if (!std::strcmp(key, "nodal_early")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_early must be 0 or 1");
-        c->nodal_early = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "nodal_reverse")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_reverse must be 0 or 1");
-        c->nodal_reverse = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "nodal_fe_nt")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "nodal_fe_nt must be 0 or 1");
-        c->nodal_fe_nt = (int)value;
-        return 0;
-    }
     if (!std::strcmp(key, "elem_gp_nt")) {
-        if (value < 0 || value > 3) return fail(HAKAI_ERR_ARG, "elem_gp_nt must be 0..3 (bit 0 loads, bit 1 stores)");
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_gp_nt must be 0 or 1");
         c->gp_nt = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "fuse_bc")) {
         if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "fuse_bc must be 0, 1 or 2 (any mesh size)");
         c->fuse_bc = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "elem_exact_pipe")) {  // 1: the persistent pipelined kernel in elem_exact mode too
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact_pipe must be 0 or 1");
-        c->exact_pipe = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "elem_pipe_min")) {
@@ -1554,27 +1324,9 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         c->elem_exact = (int)value;
         return 0;
     }
-    if (!std::strcmp(key, "diag_atomic_q")) {  // timing diagnostic only: nondeterministic sums
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "diag_atomic_q must be 0 or 1");
-        if (c->comm && value) return fail(HAKAI_ERR_STATE, "diag_atomic_q: one GPU only");
-        c->diag_atomic_q = (int)value;
-        hkc::graph_invalidate(c);
-        return 0;
-    }
-    if (!std::strcmp(key, "diag_no_assembly")) {  // timing diagnostic only: results are invalid
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "diag_no_assembly must be 0 or 1");
-        if (value && c->model_ok) HIPCHK(hipMemset(c->d_qbuf, 0, 3 * (size_t)c->nN * sizeof(double)));
-        c->diag_no_assembly = (int)value;
-        return 0;
-    }
     if (!std::strcmp(key, "group_serial")) {  // timing: hakai_step_group drains each rank's phase
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "group_serial must be 0 or 1");
         c->group_serial = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "elem_map")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_map must be 0 or 1");
-        c->pipe_map = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "nodal_padded")) {
@@ -1587,11 +1339,6 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "own_assembly must be 0 or 1");
         c->own_assembly = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "tblock_mb")) {  // two-step chunked schedule, MB of Gauss-point state per chunk
-        if (value < 0 || value > (1 << 20)) return fail(HAKAI_ERR_ARG, "tblock_mb must be 0 (off) .. 2^20");
-        c->tblock_mb = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "graph")) {

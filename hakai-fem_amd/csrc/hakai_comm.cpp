@@ -93,7 +93,7 @@ __global__ void k_save_upre(const int* up, int n_up, const int* dn, int n_dn, co
 }
 
 __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
-                       const double* fe, long long cs, int nslot, double* up_sendP, double* dn_sendC) {
+                       const double* fe, int nslot, double* up_sendP, double* dn_sendC) {
 #pragma clang fp contract(off)
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j < n_up) {
@@ -102,8 +102,8 @@ __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const i
         for (int i = ptr[n]; i < ptr[n + 1]; ++i) {
             const double* f = fe + inc[i];
             q0 += f[0];
-            q1 += f[cs];
-            q2 += f[2 * cs];
+            q1 += f[1];
+            q2 += f[2];
         }
         up_sendP[3 * j + 0] = q0;
         up_sendP[3 * j + 1] = q1;
@@ -117,8 +117,8 @@ __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const i
             if (s < m) {
                 const double* f = fe + inc[b + s];
                 o[3 * s + 0] = f[0];
-                o[3 * s + 1] = f[cs];
-                o[3 * s + 2] = f[2 * cs];
+                o[3 * s + 1] = f[1];
+                o[3 * s + 2] = f[2];
             } else {
                 o[3 * s + 0] = 0.0;
                 o[3 * s + 1] = 0.0;
@@ -131,7 +131,7 @@ __global__ void k_pack(const int* up, int n_up, const int* dn, int n_dn, const i
 // Re-does the central-difference update (v2/HAKAI_j.jl:564, same expression as k_nodal) for the
 // interface nodes with the cross-rank Q.
 __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const int* ptr, const int* inc,
-                      const double* fe, long long cs, int nslot, const double* up_sendP, const double* up_recvC,
+                      const double* fe, int nslot, const double* up_sendP, const double* up_recvC,
                       const double* dn_recvP, const double* saved, const double* u, double* out, const double* mass,
                       const double* fext, double dt, const int* poison) {
 #pragma clang fp contract(off)
@@ -154,7 +154,7 @@ __global__ void k_fix(const int* up, int n_up, const int* dn, int n_dn, const in
         for (int s = 0; s < nslot; ++s) {
             if (s < m) {
                 const double* f = fe + inc[b + s];
-                for (int c = 0; c < 3; ++c) Q[c] += f[c * cs];
+                for (int c = 0; c < 3; ++c) Q[c] += f[c];
             } else {
                 for (int c = 0; c < 3; ++c) Q[c] += 0.0;
             }
@@ -469,7 +469,7 @@ int comm_post_nodal(hakai_ctx* c, double d_time) {
     } else if (!c->q_from_buf) {  // an uploaded Q already holds the global sum
         const int n = m->n_up + m->n_dn;
         hipLaunchKernelGGL(k_fix, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
-                           c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
+                           c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP[par], m->d_up_recvC, m->d_dn_recvP,
                            m->d_saved, c->d_u[c->cur], c->d_u[1 - c->cur], c->d_mass, c->contact ? c->d_fext : nullptr,
                            d_time, c->d_poison);
         HIPCHK(hipGetLastError());
@@ -489,7 +489,7 @@ int comm_post_element(hakai_ctx* c, long long step) {
                            m->d_up_sendP[par], m->d_dn_sendC[par]);
     else
         hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, m->d_up, m->n_up, m->d_dn, m->n_dn,
-                           c->d_inc_ptr, c->d_inc, c->d_fe, (long long)(c->fe_layout == 1 ? c->nEp : 1), m->nslot, m->d_up_sendP[par], m->d_dn_sendC[par]);
+                           c->d_inc_ptr, c->d_inc, c->d_fe, m->nslot, m->d_up_sendP[par], m->d_dn_sendC[par]);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(m->ev_packed[par], c->stream));
     if (m->mode == 0) {

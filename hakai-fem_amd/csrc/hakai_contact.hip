@@ -59,7 +59,9 @@ struct PairParam {
 // contact elements, one fixed-size block; the blocks are all-gathered (RCCL over xGMI, or device
 // copies in an in-process group) and scattered into the mirror. The block of step s is packed at
 // the end of step s-1 (or at the state reset, s = 0), so an in-process group stepped rank by rank
-// finds every peer's block ready. Contact work is replicated, not divided.
+// finds every peer's block ready. The triangle search is divided across the ranks (contact_divide,
+// the reference's triangle-parallel loop :2370, :2386, :2653-2667): rank r tests the candidate
+// triangles j = r (mod N) and the events are all-gathered before the force sums.
 // Two node sets travel: X0, the nodes of the entries live from the start (every step, owner
 // packs), and X1, the nodes only a deletion exposes. An X1 node is shipped by every rank that
 // deleted one of its adders (the adder contains the node, so that rank holds it), from the step
@@ -192,7 +194,6 @@ struct Contact {
     // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
     bool small = false;
     int fuse_small = 1;
-    int tri_w64 = 0;  // tuning "contact_tri_wave": one candidate triangle per wave (k_ct_tri64)
 
     // events and per-node gather over the touched nodes
     long long cap = 0;
@@ -1000,8 +1001,7 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
 #pragma unroll
         for (int a = 0; a < 8; ++a) own8[a] = cn[a];
     }
-    // the point-independent part of the test, held in registers for the whole bucket (scalar
-    // registers when the record is wave-uniform, k_ct_tri64)
+    // the point-independent part of the test, held in registers for the whole bucket
     const double c0 = rec->c[0], c1 = rec->c[1], c2 = rec->c[2], Rmax = rec->Rmax;
     const double q00 = rec->q0[0], q01 = rec->q0[1], q02 = rec->q0[2], vdet = rec->vdet;
     double im[9];
@@ -1149,52 +1149,6 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
         if (valid && !dup)
             tri_cell(s, rec, mj, hoff + (int)hb, 0, 1, par, boff, blist, d_lim, myu, evn, shard_cap, sh_nodes, sh_f,
                          eb);
-        ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
-    }
-}
-
-// One candidate triangle per WAVE: the record address is wave-uniform (scalar loads, no VGPRs for
-// the triangle's constants), lane c and lane 32 + c both take cell c and split its bucket (even /
-// odd entries), so a wave's longest serial chain is half a bucket. The events are the same set
-// as k_ct_tri's (their order in the shards differs; the per-node sums do not depend on it).
-__global__ __launch_bounds__(128) void k_ct_tri64(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
-                                                  const TriRec* __restrict__ cand, long long cshard_cap,
-                                                  const PairParam* par, const int* boff, const BEnt* blist,
-                                                  double d_lim, double myu, unsigned int* evs, long long shard_cap,
-                                                  int* ev_nodes, double* ev_f) {
-    __shared__ unsigned s_cpre[kCandShards + 4];
-    const long long nt = shard_scan(ccnt, cshard_cap, s_cpre);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl[kNcand] = s_cpre[kCandShards + 2];
-        atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
-        atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
-        ctl[kCandOver] = s_cpre[kCandShards + 1];
-    }
-    const int lane = (int)(threadIdx.x & 63);
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int wpb = (int)(blockDim.x >> 6);
-    const int shard = (int)(((long long)blockIdx.x * wpb + wv) % kEvShards);
-    unsigned int* evn = evs + shard * kShardStride;
-    int* sh_nodes = ev_nodes + 4 * (long long)shard * shard_cap;
-    double* sh_f = ev_f + 3 * (long long)shard * shard_cap;
-    const int cell = lane & 31, part = lane >> 5;
-    const bool valid = cell < 27;
-    for (long long t = (long long)blockIdx.x * wpb + wv; t < nt; t += (long long)gridDim.x * wpb) {
-        EvBuf eb;
-        eb.n = 0;
-        eb.j0 = eb.j1 = eb.j2 = 0;
-        const TriRec* rec = cand + shard_slot(s_cpre, cshard_cap, t);
-        const long long mj[3] = {rec->mj[0], rec->mj[1], rec->mj[2]};
-        unsigned hb = 0x80000000u | (unsigned)lane;
-        if (valid)
-            hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
-                 (unsigned)rec->hmask;
-        bool dup = false;
-#pragma unroll
-        for (int c2 = 0; c2 < 26; ++c2) dup |= c2 < cell && (unsigned)__builtin_amdgcn_readlane((int)hb, c2) == hb;
-        if (valid && !dup)
-            tri_cell(s, rec, mj, rec->hoff + (int)hb, part, 2, par, boff, blist, d_lim, myu, evn, shard_cap,
-                         sh_nodes, sh_f, eb);
         ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
 }
@@ -2198,9 +2152,7 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                                C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
                                C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
-        auto tri = C->tri_w64 ? k_ct_tri64 : k_ct_tri;
-        const int gt = C->tri_w64 ? std::min(2 * C->g_tri, 8192) : C->g_tri;
-        hipLaunchKernelGGL(tri, dim3(gt), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
+        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
                            C->cshard_cap,
                            C->d_par, C->d_boff, C->d_blist, C->d_lim, C->myu, C->d_evs,
                            C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
@@ -2364,12 +2316,6 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     if (!std::strcmp(key, "contact_fuse_small")) {  // small decks: fused single-workgroup phases
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_small must be 0 or 1");
         C->fuse_small = (int)value;
-        graph_invalidate(c);
-        return 0;
-    }
-    if (!std::strcmp(key, "contact_tri_wave")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_tri_wave must be 0 or 1");
-        C->tri_w64 = (int)value;
         graph_invalidate(c);
         return 0;
     }

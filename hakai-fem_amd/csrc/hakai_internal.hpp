@@ -51,34 +51,19 @@ struct hakai_ctx {
     int* d_inc = nullptr;        // CSR incidences as force base offsets of the active layout
     int* d_inc_row = nullptr;    // the same incidences as (8e+k), for element-indexed data
     int* d_inc8 = nullptr;       // padded incidence table, null if a node has > 8 incidences
-    // Element-force layout: component c of (element e, local node k) lives at fe[base + c*cs].
-    //   layout 0 (AoS rows, = the reference's Qe column order): base = 24e + 3k, cs = 1;
-    //   layout 1 (component SoA): base = 3k*nEp + e, cs = nEp -- a wave of neighbouring nodes
-    //   gathers neighbouring elements' same slot, i.e. contiguous doubles.
-    // d_inc / d_inc8 hold bases of the active layout; base 24nEp is all-zero in both (padding).
-    int fe_layout = 0;
+    // Element forces [nEp][8][3] (= the reference's Qe column order), row (e, k) at base 24e + 3k;
+    // d_inc / d_inc8 hold the bases, and base 24nEp is an all-zero row (padding).
     long long fe_len = 0;        // doubles allocated for fe
     int max_inc = 0;
     std::vector<int> h_ptr, h_inc0;  // CSR node -> (8e+k), ascending element order
-    int elem_variant = 2;        // k_element occupancy variant (HAKAI_ELEM_MINW)
     int pipe_blocks = 512;       // persistent pipelined element kernel grid (0 = simple kernel)
-    int pipe_map = 1;            // batch schedule of the persistent kernel (0 per block, 1 per XCD)
     int pipe_min = 2;            // persistent kernel only with >= pipe_min batches per block (small
                                  // meshes: one batch per block, the pipeline only adds latency)
-    int nodal_early = 1;         // nodal kernel loads its node operands before the gather
-    int gp_nt = 3;               // element kernel: Gauss-point state nontemporal (bit 0 loads, bit 1 stores)
-    int nodal_fe_nt = 0;         // nodal kernel gathers element forces nontemporally
-    int nodal_reverse = 1;       // nodal kernel walks each XCD's node chunk from its end
+    int gp_nt = 1;               // element kernel: Gauss-point state nontemporal (loads and stores)
     int elem_exact = 0;          // tuning "elem_exact": reference-order element arithmetic
-    int exact_pipe = 0;          // tuning "elem_exact_pipe": the persistent kernel in elem_exact mode (default: one-batch)
     int group_serial = 0;        // tuning "group_serial" (rank 0 of a hakai_step_group): drain every rank's
                                  // phase before the next rank's (per-rank timings without the ranks
                                  // sharing the one GPU)
-    int diag_atomic_q = 0;       // tuning "diag_atomic_q": TIMING DIAGNOSTIC -- the element kernel adds the
-                                 // node forces into d_qbuf with FP64 atomics (order nondeterministic)
-    int diag_no_assembly = 0;    // tuning "diag_no_assembly": TIMING DIAGNOSTIC, results invalid --
-                                 // no element-force traffic (rows to one dummy row, Q read from a
-                                 // zero buffer): the step's cost without any force assembly
     double* d_pusai = nullptr;   // cal_Pusai_hexa table for the exact element kernel (192 doubles)
     int nmat = 0;
     long long elem_offset = 0;   // global id of local element 0
@@ -135,16 +120,6 @@ struct hakai_ctx {
     long long tdev_next = -1;          // the step the device counter is valid for (-1: unknown)
     int graph = 16;                    // tuning "graph": steps per graph (even), 0 = no capture
     long long graph_steps = 0;         // steps run from graphs (tests, stats)
-    // Two-step chunked schedule (tuning "tblock_mb", hakai_step on one GPU without contact): steps s
-    // and s+1 are interleaved chunk by chunk so that step s+1 of a chunk re-reads its Gauss-point
-    // state, element forces and node rows while they are still in the Infinity Cache. Boundaries,
-    // per iteration it = 0..C (see tblock_build): element batches tb_E[it] (step s chunks), node
-    // counts tb_A[it] (nodes step s's chunk it needs), tb_B[it] (nodes whose step-s forces are all
-    // in after chunks < it) and element batches tb_D[it] (elements whose nodes are all < tb_B[it]).
-    int tblock_mb = 0;                 // MB of Gauss-point state per chunk, 0 = off
-    long long tb_built_mb = -1;        // chunk size the schedule below was built for (-1: none)
-    std::vector<long long> tb_E, tb_A, tb_B, tb_D;
-    long long tb_pairs = 0;            // step pairs run with the chunked schedule (tests, stats)
     // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): the persistent
     // element kernel sums node forces in LDS in element order and stores Q (or a prefix partial plus
     // the later contributions as rows) instead of the per-element fe array.
@@ -155,6 +130,7 @@ struct hakai_ctx {
     int* d_own_off = nullptr;          // [nb+1] per-batch entry offsets
     int* d_own_list = nullptr;         // 4 ints per entry (+ one no-op entry at own_nop)
     int own_nop = 0;
+    int own_slots = 0;                 // LDS running-sum slots the lists use (the kernel's dynamic LDS)
     double* d_own_q = nullptr;         // [nN][3]
     int* d_own_rp = nullptr;           // [nN+1]
     double* d_own_rows = nullptr;      // [rows][3], numbered by super-batch

@@ -63,7 +63,7 @@ __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int
     in.n = a.conn[8 * e + k];
     in.mt = a.mat[e];
     const int kn = EXACT ? k : ref_of_sign(k);  // the node whose force lane k ends up with
-    in.fb = a.cstride == 1 ? (int)(24 * e + 3 * kn) : (int)(3 * kn * a.nEp + e);
+    in.fb = (int)(24 * e + 3 * kn);
 }
 
 // Gauss-point state accesses: plain, or nontemporal (streamed once per step; keeps the caches for
@@ -82,15 +82,10 @@ __device__ __forceinline__ void gp_st(double* p, double v) {
         *p = v;
 }
 
+// stage B: the lane's node (position = coord + u, d_disp = u - u_pre) and its Gauss-point state
 template <bool ANY_PLASTIC, int NT = 0>
-__device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int k, ElemIn& in) {
-    const long long gp = 8 * e + k, ld = a.ld, n = in.n;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double uc = a.u[3 * n + c];
-        in.x[c] = a.coord[3 * n + c] + uc;
-        in.du[c] = uc - a.u_pre[3 * n + c];
-    }
+__device__ __forceinline__ void load_gp(const ElemArgs& a, long long e, int k, ElemIn& in) {
+    const long long gp = 8 * e + k, ld = a.ld;
 #pragma unroll
     for (int c = 0; c < 6; ++c) in.sig[c] = gp_ld<NT>(a.stress + c * ld + gp);
 #pragma unroll
@@ -101,6 +96,22 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
         in.eqp = gp_ld<NT>(a.eqps + gp);
         in.ys = gp_ld<NT>(a.yield + gp);
     }
+}
+
+__device__ __forceinline__ void load_node(const ElemArgs& a, ElemIn& in) {
+    const long long n = in.n;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double uc = a.u[3 * n + c];
+        in.x[c] = a.coord[3 * n + c] + uc;
+        in.du[c] = uc - a.u_pre[3 * n + c];
+    }
+}
+
+template <bool ANY_PLASTIC, int NT = 0>
+__device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int k, ElemIn& in) {
+    load_node(a, in);
+    load_gp<ANY_PLASTIC, NT>(a, e, k, in);
 }
 
 // Unconditional write-back of one lane (selects, no branches): its node's force fk, its Gauss
@@ -116,22 +127,12 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
         fo[0] = active ? fk[0] : 0.0;
         fo[1] = active ? fk[1] : 0.0;
         fo[2] = active ? fk[2] : 0.0;
-        if (STORE_TRIAX) {  // a call's last step also keeps fe (Q / Qe downloads, mode switches)
-            double* fg = a.fe + in.fb;
-            fg[0] = active ? fk[0] : 0.0;
-            fg[a.cstride] = active ? fk[1] : 0.0;
-            fg[2 * a.cstride] = active ? fk[2] : 0.0;
-        }
-    } else if (a.qatomic) {  // timing diagnostic: atomics into Q instead of the fe round trip
-        const int src = (int)(threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k));
-        const int node = __shfl(in.n, src);
-        if (active)
-            for (int c = 0; c < 3; ++c) atomicAdd(a.qatomic + 3 * (long long)node + c, fk[c]);
-    } else {
-        double* fo = a.fe + (in.fb & a.fe_mask);
-        fo[0] = active ? fk[0] : 0.0;
-        fo[a.cstride] = active ? fk[1] : 0.0;
-        fo[2 * a.cstride] = active ? fk[2] : 0.0;
+    }
+    if (!OWN || STORE_TRIAX) {  // fe; with owner assembly only on a call's last step (Q / Qe downloads, mode switches)
+        double* fg = a.fe + in.fb;
+        fg[0] = active ? fk[0] : 0.0;
+        fg[1] = active ? fk[1] : 0.0;
+        fg[2] = active ? fk[2] : 0.0;
     }
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
@@ -367,53 +368,102 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// Reference-order element update (tuning key "elem_exact"): cal_stress_hexa's own arithmetic,
-// operation for operation (the oracle's restatement: oracle/hakai_oracle.c cal_BVbar_hexa,
-// cal_Bfinal, stress_one_element), so the element forces and the Gauss-point state are the
-// reference's bits -- and, with the bit-exact nodal update and contact, whole trajectories are.
-// Same mapping as elem_step (lane k = Gauss point k); no contraction, fma exactly where the
-// reference's StaticArrays products use muladd:
+// Reference-order element update (tuning key "elem_exact"): cal_stress_hexa's own arithmetic
+// (the oracle's restatement: oracle/hakai_oracle.c cal_BVbar_hexa, cal_Bfinal, stress_one_element),
+// so the Gauss-point state, the element forces and -- with the bit-exact nodal update and contact --
+// whole trajectories are the reference's bits. Same mapping as elem_step (lane k = Gauss point k),
+// no contraction, fma exactly where the reference's StaticArrays products use muladd:
 //   * Jacobian of GP k summed in node order 1..8 (:1424-1434) from the Pusai table (cal_Pusai_hexa,
-//     built on the host with the reference's expression), cofactor det/inverse (:1436-1455);
-//   * BVbar[:, 3i+c] = (sum over k in GP order of (P2_k/3)*|det_k|) / V with V = sum |det_k|
-//     (:1729-1780): each lane writes its 8 node terms to LDS, lane i sums node i's column over
-//     the 8 lanes in GP order -- (P2/3)*|det| equals (P_signed/3)*det_signed exactly;
-//   * Bfinal (:1472-1490) is never stored: its entries are Pix, Piy, Piz, BVbar - P/3 and the
-//     explicit zeros, fed to the 6x24 * 24 chain (:1204) column by column in the reference's order;
-//   * D * de as the full 6x6 muladd chain (:1205); radial return with the reference's divisions
-//     (:1251-1282); Qe[:, e] += detJ * Bfinal' sigma (:1330-1340) summed over GPs in order via LDS;
-//   * deletion averages (:701-712) summed in GP order; triaxiality in invariant form (the
+//     built on the host with the reference's expression), cofactor det/inverse (:1436-1455), and
+//     P2 = dN_i/dx (:1457-1470), computed ONCE per GP: cal_BVbar_hexa (:1716-1754) forms the same
+//     P2 with 1/|det| and weights it with |det|, which is (P2/3)*det with the signed det, bit for bit;
+//   * BVbar[:, 3i+c] = (sum over GPs in order of (P2/3)*|det|) / V, V = sum |det| (:1729-1780): each
+//     lane writes its 8 node terms to an LDS exchange area, lane i sums node i's column over the 8
+//     lanes in GP order;
+//   * Bfinal (:1472-1490) is never stored: its entries are Pix, Piy, Piz, t = BVbar - P2/3 (kept in
+//     registers, one division by 3 per entry) and structural zeros, fed to the 6x24 * 24 chain (:1204)
+//     column by column in the reference's order; the same for D*de (:1205) and Bfinal'*sigma
+//     (:1330-1340). A structural zero term is fma(0, x, acc) == acc unless acc is a zero, so dropping
+//     it can change only the SIGN of a zero intermediate; every stored quantity is a sum started
+//     from +0 or a previous value that is never -0, so the stored bits are the same
+//     (tests/test_exact_chains.py checks the chains on ±0-rich inputs);
+//   * radial return with the reference's divisions (:1251-1282): x/3 and a/q are correctly rounded
+//     by div3 / div_cr below (same bits as IEEE division, fewer instructions);
+//   * Qe[:, e] += detJ * Bfinal' * sigma summed over the GPs in order through the exchange area;
+//     deletion averages (:701-712) summed in GP order; triaxiality in invariant form (the
 //     reference's eigvals agree to rounding; it only enters the deletion test and the output).
 // ---------------------------------------------------------------------------------------------
-constexpr int kXbStride = 104;  // doubles of LDS per element: w[64] + av[8] + bv[24] + pad
+constexpr int kXbStride = 66;  // doubles of LDS per element: exchange area [8 nodes][8 lanes] + pad
 
 // x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
 // q = RN(x*y) with y = RN(1/3), then one exact-remainder correction q + (x - 3q)*y. The exact
 // quotient x/3 (a multiple of 1/3 of the last place) is never within 1/6 ulp of a rounding
 // boundary, and the corrected value is within |x - 3q| * |y - 1/3| < 2^-52 ulp of it, so both round
-// the same way (tests/test_div3.py checks the identity against IEEE division on the CPU). x == 0
-// keeps its sign.
+// the same way (tests/test_div3.py checks the identity against IEEE division on the CPU). A zero
+// comes out as +0 (see the zero-sign note above).
 __device__ __forceinline__ double div3(double x) {
     constexpr double y = 1.0 / 3.0;
     const double q = x * y;
     const double r = __builtin_fma(-q, 3.0, x);
-    const double q1 = __builtin_fma(r, y, q);
-    return x == 0.0 ? x : q1;
+    return __builtin_fma(r, y, q);
 }
 
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0>
+// a / b correctly rounded given rb = RN(1/b) (one IEEE division per divisor): two Newton-Markstein
+// corrections of q0 = RN(a*rb). q0 is within 1.5 ulp of a/b, q1 within one ulp, and then
+// RN(q1 + (a - b*q1)*rb) is RN(a/b) (Markstein's theorem: the residual is exact for a faithful
+// q1, rb is the correctly rounded reciprocal). Normal-range operands (the element's stresses,
+// volumes); tests/test_div3.py checks it against IEEE division on the CPU.
+__device__ __forceinline__ double div_cr(double a, double b, double rb) {
+    const double q0 = a * rb;
+    const double q1 = __builtin_fma(__builtin_fma(-q0, b, a), rb, q0);
+    return __builtin_fma(__builtin_fma(-q1, b, a), rb, q1);
+}
+
+// Ordered sum over the 8 Gauss points (lanes) of an element, for every node at once: lane k
+// contributes v[i] for node i; lane i returns ((v_0[i] + v_1[i]) + ...) + v_7[i] (GP order, from
+// +0 like the reference's zero-initialised accumulators). w: the element's exchange area.
+__device__ __forceinline__ double gp_sum8(double* w, int k, const double (&v)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[8 * i + k] = v[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double r[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) r[kk] = w[8 * k + kk];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double acc = 0.0 + r[0];
+#pragma unroll
+    for (int kk = 1; kk < 8; ++kk) acc += r[kk];
+    return acc;
+}
+
+// Ordered sum over the 8 lanes of one scalar; every lane gets it.
+__device__ __forceinline__ double gp_all8(double* w, int k, double x) {
+    w[k] = x;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double r[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) r[kk] = w[kk];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double acc = 0.0 + r[0];
+#pragma unroll
+    for (int kk = 1; kk < 8; ++kk) acc += r[kk];
+    return acc;
+}
+
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0, bool OWN = false>
 __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat* __restrict__ mats, long long e,
                                                 int k, double* nd8, double* xb, const double* pus,
-                                                const ElemIn& in) {
+                                                const ElemIn& in, double* sfe = nullptr) {
 #pragma clang fp contract(off)
     const DevMat* M = mats + in.mt;
     const bool active = in.fl == 1;
     const int npp = M->npp;
     const int nd = DO_DELETE ? M->nd : 0;
     double eqp = in.eqp, ys = in.ys;
-    double* w = xb;        // [node i][lane kk] exchange of one component
-    double* av = xb + 64;  // one scalar per lane
-    double* bv = xb + 72;  // BVbar row (24)
 
     nd8[6 * k + 0] = in.x[0];
     nd8[6 * k + 1] = in.x[1];
@@ -425,13 +475,19 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ---- Jacobian at GP k in node order, det and inverse (cal_Bfinal :1424-1455; cal_BVbar_hexa
-    // computes the same J and det at :1716-1740)
+    // computes the same J and det at :1716-1740). The first term starts the sum (0 + x == x).
     const double* P0 = pus + 24 * k;  // Pusai_mat[k][r][i] = pus[24k + 8r + i]
     const double* P1 = P0 + 8;
     const double* P2 = P0 + 16;
-    double J11 = 0.0, J12 = 0.0, J13 = 0.0, J21 = 0.0, J22 = 0.0, J23 = 0.0, J31 = 0.0, J32 = 0.0, J33 = 0.0;
+    double J11, J12, J13, J21, J22, J23, J31, J32, J33;
+    {
+        const double X0 = nd8[0], X1 = nd8[1], X2 = nd8[2];
+        J11 = P0[0] * X0; J12 = P0[0] * X1; J13 = P0[0] * X2;
+        J21 = P1[0] * X0; J22 = P1[0] * X1; J23 = P1[0] * X2;
+        J31 = P2[0] * X0; J32 = P2[0] * X1; J33 = P2[0] * X2;
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 1; i < 8; ++i) {
         const double X0 = nd8[6 * i + 0], X1 = nd8[6 * i + 1], X2 = nd8[6 * i + 2];
         J11 += P0[i] * X0;
         J12 += P0[i] * X1;
@@ -465,34 +521,29 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         }
     }
 
-    // ---- V and BVbar (:1729-1780), summed over the 8 GPs in order by the lane of each node.
-    // (P2_abs/3)*|det| of the reference equals (P2/3)*det with the signed det, bit for bit.
-    av[k] = fabs(v);
-    double bvk[3];
+    // ---- V and BVbar (:1729-1780)
+    const double V = gp_all8(xb, k, fabs(v));
+    {
+        double bs[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+        for (int c = 0; c < 3; ++c) {
+            double w[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) w[8 * i + k] = div3(pd[i][c]) * v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double s = 0.0;
+            for (int i = 0; i < 8; ++i) w[i] = div3(pd[i][c]) * v;
+            bs[c] = gp_sum8(xb, k, w);
+        }
+        // lane k holds node k's BVbar column sums; the X slots of the node area are free now
+        const double rV = 1.0 / V;
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) s += w[8 * k + kk];
-        bvk[c] = s;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int c = 0; c < 3; ++c) nd8[6 * k + c] = div_cr(bs[c], V, rV);
     }
-    double V = 0.0;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) V += av[kk];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) bv[3 * k + c] = bvk[c] / V;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // Bfinal rows 1-3 carry -P2/3 + BVbar (:1482-1490)
-    auto tq = [&](int i, int c) { return -div3(pd[i][c]) + bv[3 * i + c]; };
+    // Bfinal rows 1-3 carry t(i,c) = -P2/3 + BVbar (:1482-1490), formed where it is used (keeping
+    // all 24 live next to P2 would spill at 2 waves per SIMD)
+    auto tq = [&](int i, int c) { return nd8[6 * i + c] - div3(pd[i][c]); };
 
-    // ---- de = Bfinal * d_u (:1204): per row, the chain over columns j = 3i+c in order.
+    // ---- de = Bfinal * d_u (:1204): per row, the fma chain over columns j = 3i+c in order.
     // Bfinal column (i,c) by rows: c=0: (Pix+t0, t0, t0, Piy, 0, Piz); c=1: (t1, Piy+t1, t1, Pix,
     // Piz, 0); c=2: (t2, t2, Piz+t2, 0, Piy, Pix).
     double de[6];
@@ -501,47 +552,42 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         const double* D = nd8 + 6 * i + 3;
         const double u0 = D[0], u1 = D[1], u2 = D[2];
         const double t0 = tq(i, 0), t1 = tq(i, 1), t2 = tq(i, 2);
+        const double px = pd[i][0], py = pd[i][1], pz = pd[i][2];
         if (i == 0) {
-            de[0] = (pd[0][0] + t0) * u0;
+            de[0] = (px + t0) * u0;
             de[1] = t0 * u0;
             de[2] = t0 * u0;
-            de[3] = pd[0][1] * u0;
-            de[4] = 0.0 * u0;
-            de[5] = pd[0][2] * u0;
+            de[3] = py * u0;
+            de[4] = pz * u1;  // column 0 of row 5 is a structural zero
+            de[5] = pz * u0;
         } else {
-            de[0] = __builtin_fma(pd[i][0] + t0, u0, de[0]);
+            de[0] = __builtin_fma(px + t0, u0, de[0]);
             de[1] = __builtin_fma(t0, u0, de[1]);
             de[2] = __builtin_fma(t0, u0, de[2]);
-            de[3] = __builtin_fma(pd[i][1], u0, de[3]);
-            de[4] = __builtin_fma(0.0, u0, de[4]);
-            de[5] = __builtin_fma(pd[i][2], u0, de[5]);
+            de[3] = __builtin_fma(py, u0, de[3]);
+            de[5] = __builtin_fma(pz, u0, de[5]);
+            de[4] = __builtin_fma(pz, u1, de[4]);
         }
         de[0] = __builtin_fma(t1, u1, de[0]);
-        de[1] = __builtin_fma(pd[i][1] + t1, u1, de[1]);
+        de[1] = __builtin_fma(py + t1, u1, de[1]);
         de[2] = __builtin_fma(t1, u1, de[2]);
-        de[3] = __builtin_fma(pd[i][0], u1, de[3]);
-        de[4] = __builtin_fma(pd[i][2], u1, de[4]);
-        de[5] = __builtin_fma(0.0, u1, de[5]);
+        de[3] = __builtin_fma(px, u1, de[3]);
         de[0] = __builtin_fma(t2, u2, de[0]);
         de[1] = __builtin_fma(t2, u2, de[1]);
-        de[2] = __builtin_fma(pd[i][2] + t2, u2, de[2]);
-        de[3] = __builtin_fma(0.0, u2, de[3]);
-        de[4] = __builtin_fma(pd[i][1], u2, de[4]);
-        de[5] = __builtin_fma(pd[i][0], u2, de[5]);
+        de[2] = __builtin_fma(pz + t2, u2, de[2]);
+        de[4] = __builtin_fma(py, u2, de[4]);
+        de[5] = __builtin_fma(px, u2, de[5]);
     }
 
-    // ---- d_o = Dmat * de (:1205), the full 6x6 chain (Dmat[r][j] = c*M[r][j], zeros included)
-    const double Dn = M->Dn, Do = M->Do, Ds = M->Ds, Z = 0.0;
-    const double Dm[6][6] = {{Dn, Do, Do, Z, Z, Z}, {Do, Dn, Do, Z, Z, Z}, {Do, Do, Dn, Z, Z, Z},
-                             {Z, Z, Z, Ds, Z, Z},   {Z, Z, Z, Z, Ds, Z},   {Z, Z, Z, Z, Z, Ds}};
+    // ---- d_o = Dmat * de (:1205): the 6x6 chain without its structural zeros
+    const double Dn = M->Dn, Do = M->Do, Ds = M->Ds;
     double fin[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        double acc = Dm[r][0] * de[0];
-#pragma unroll
-        for (int j = 1; j < 6; ++j) acc = __builtin_fma(Dm[r][j], de[j], acc);
-        fin[r] = in.sig[r] + acc;
-    }
+    fin[0] = in.sig[0] + __builtin_fma(Do, de[2], __builtin_fma(Do, de[1], Dn * de[0]));
+    fin[1] = in.sig[1] + __builtin_fma(Do, de[2], __builtin_fma(Dn, de[1], Do * de[0]));
+    fin[2] = in.sig[2] + __builtin_fma(Dn, de[2], __builtin_fma(Do, de[1], Do * de[0]));
+    fin[3] = in.sig[3] + Ds * de[3];
+    fin[4] = in.sig[4] + Ds * de[4];
+    fin[5] = in.sig[5] + Ds * de[5];
     // ---- J2 radial return (:1227-1289)
     if (ANY_PLASTIC && npp > 0) {
         const double mean = div3(fin[0] + fin[1] + fin[2]);
@@ -559,10 +605,11 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
             const double H = M->Hd[p];
             const double dep = (q - ys) / (3.0 * M->G + H);
             const double s = ys + H * dep;
+            const double rq = 1.0 / q;
 #pragma unroll
-            for (int r = 0; r < 3; ++r) fin[r] = dev[r] * s / q + mean;
+            for (int r = 0; r < 3; ++r) fin[r] = div_cr(dev[r] * s, q, rq) + mean;
 #pragma unroll
-            for (int r = 3; r < 6; ++r) fin[r] = dev[r] * s / q + 0.0;
+            for (int r = 3; r < 6; ++r) fin[r] = div_cr(dev[r] * s, q, rq) + 0.0;
             eqp = eqp + dep;
             ys = ys + H * dep;
         }
@@ -582,68 +629,52 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     }
     bool kill = false;
     if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
-        av[k] = eqp;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double v_e = 0.0;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) v_e += av[kk];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        av[k] = tri;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double t_e = 0.0;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) t_e += av[kk];
-        v_e = v_e * 0.125;  // /8, exact
-        t_e = t_e * 0.125;
+        const double v_e = gp_all8(xb, k, eqp) * 0.125;  // /8, exact
+        const double t_e = gp_all8(xb, k, tri) * 0.125;
         if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
     }
 
     // ---- Qe[:, e] += detJ * Bfinal' * sigma (:1330-1340), GP contributions summed in GP order
     double fk[3];
+    {
+        double w[8];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const double t = tq(i, c);
-            double acc;
-            if (c == 0) {
-                acc = (pd[i][0] + t) * fin[0];
-                acc = __builtin_fma(t, fin[1], acc);
-                acc = __builtin_fma(t, fin[2], acc);
-                acc = __builtin_fma(pd[i][1], fin[3], acc);
-                acc = __builtin_fma(0.0, fin[4], acc);
-                acc = __builtin_fma(pd[i][2], fin[5], acc);
-            } else if (c == 1) {
-                acc = t * fin[0];
-                acc = __builtin_fma(pd[i][1] + t, fin[1], acc);
-                acc = __builtin_fma(t, fin[2], acc);
-                acc = __builtin_fma(pd[i][0], fin[3], acc);
-                acc = __builtin_fma(pd[i][2], fin[4], acc);
-                acc = __builtin_fma(0.0, fin[5], acc);
-            } else {
-                acc = t * fin[0];
-                acc = __builtin_fma(t, fin[1], acc);
-                acc = __builtin_fma(pd[i][2] + t, fin[2], acc);
-                acc = __builtin_fma(0.0, fin[3], acc);
-                acc = __builtin_fma(pd[i][1], fin[4], acc);
-                acc = __builtin_fma(pd[i][0], fin[5], acc);
-            }
-            w[8 * i + k] = v * acc;  // W*W*W*detJ*acc with W = 1
+        for (int i = 0; i < 8; ++i) {  // column (i, 0): (Pix+t0, t0, t0, Piy, 0, Piz)
+            const double t0 = tq(i, 0);
+            double acc = (pd[i][0] + t0) * fin[0];
+            acc = __builtin_fma(t0, fin[1], acc);
+            acc = __builtin_fma(t0, fin[2], acc);
+            acc = __builtin_fma(pd[i][1], fin[3], acc);
+            acc = __builtin_fma(pd[i][2], fin[5], acc);
+            w[i] = v * acc;  // W*W*W*detJ*acc with W = 1
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double s = 0.0;
+        fk[0] = gp_sum8(xb, k, w);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) s += w[8 * k + kk];
-        fk[c] = s;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = 0; i < 8; ++i) {  // column (i, 1): (t1, Piy+t1, t1, Pix, Piz, 0)
+            const double t1 = tq(i, 1);
+            double acc = t1 * fin[0];
+            acc = __builtin_fma(pd[i][1] + t1, fin[1], acc);
+            acc = __builtin_fma(t1, fin[2], acc);
+            acc = __builtin_fma(pd[i][0], fin[3], acc);
+            acc = __builtin_fma(pd[i][2], fin[4], acc);
+            w[i] = v * acc;
+        }
+        fk[1] = gp_sum8(xb, k, w);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // column (i, 2): (t2, t2, Piz+t2, 0, Piy, Pix)
+            const double t2 = tq(i, 2);
+            double acc = t2 * fin[0];
+            acc = __builtin_fma(t2, fin[1], acc);
+            acc = __builtin_fma(pd[i][2] + t2, fin[2], acc);
+            acc = __builtin_fma(pd[i][1], fin[4], acc);
+            acc = __builtin_fma(pd[i][0], fin[5], acc);
+            w[i] = v * acc;
+        }
+        fk[2] = gp_sum8(xb, k, w);
     }
     if (WITH_VOL) a.vol[e] = V;
-    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys, tri);
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys,
+                                                                      tri, sfe);
 }
 
 // Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.
@@ -667,31 +698,13 @@ __device__ __forceinline__ void graph_step(ElemArgs& a) {
     }
 }
 
-// Two-step chunked schedule (ElemArgs::two_step): virtual batch v < n1 is batch r1_lo + v of step s,
-// the others batch r2_lo + v - n1 of step s+1, whose displacement buffers are swapped. A batch lies
-// in one range, so the selection is uniform over the block.
-__device__ __forceinline__ long long two_step_batch(const ElemArgs& a, long long v) {
-    const long long n1 = a.r1_hi - a.r1_lo;
-    return v < n1 ? a.r1_lo + v : a.r2_lo + (v - n1);
-}
-__device__ __forceinline__ ElemArgs two_step_args(const ElemArgs& a, long long v) {
-    ElemArgs b = a;
-    if (v >= a.r1_hi - a.r1_lo) {
-        b.u = a.u_pre;
-        b.u_pre = a.u;
-        b.step_i = a.step_i + 1;
-    }
-    return b;
-}
-
-// One batch of 32 elements per block (simple form; small meshes, the literal drop-in, A/B).
-template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, int MINW, bool EXACT, bool TWO = false>
-__global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
+// One batch of 32 elements per block (simple form; small meshes, the literal drop-in).
+template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, bool EXACT>
+__global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
     const long long vb = xcd_remap(blockIdx.x, gridDim.x);
-    ElemArgs a = TWO ? two_step_args(a0, vb) : a0;
     if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
     const int k = threadIdx.x & 7;
@@ -700,7 +713,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
         stage_pusai(a, s_pus);
         __syncthreads();
     }
-    const long long e = (TWO ? two_step_batch(a0, vb) : vb) * kEPB + grp;
+    const long long e = vb * kEPB + grp;
     ElemIn in;
     load_stage_a<EXACT>(a, e, k, in);
     load_stage_b<true>(a, e, k, in);
@@ -724,7 +737,8 @@ __global__ __launch_bounds__(kBlock, MINW) void k_element(ElemArgs a0) {
 // unconditionally (unused ones to a per-block dump line, which a wave's lanes share) so the loads of
 // the pipeline stay in flight across the pass. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
 // ---------------------------------------------------------------------------------------------
-constexpr int kOwnSlots = 1024;            // LDS running sums per block (24 KB)
+// LDS running sums per block: at most 1024 (24 KB), sized per launch to what the lists use
+// (ElemArgs::own_slots, dynamic LDS next to the staged materials)
 // batches per super-batch: 2, or 1 for meshes whose 64-element super-batches need more than 512
 // entries; the host picks (own_build), the kernel is instantiated for both
 constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
@@ -796,15 +810,17 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO = false,
-          int OS = 0>
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS = 0>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
     constexpr int kOwnFe = OS * kEPB * 24;       // staged forces per super-batch (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_fe[OWN ? 2 * kOwnFe : 1];
-    __shared__ __attribute__((aligned(16))) double s_part[OWN ? kOwnSlots * 3 : 1];
-    __shared__ __attribute__((aligned(16))) DevMat s_mats[LDS_MATS ? kMaxLdsMats : 1];
+    // dynamic LDS (sized by the launch, launch_pipe): [own_slots][3] running sums, then the
+    // nmat staged materials
+    extern __shared__ __attribute__((aligned(16))) double s_dyn[];
+    double* s_part = s_dyn;
+    DevMat* s_mats = reinterpret_cast<DevMat*>(s_dyn + (OWN ? 3 * a.own_slots : 0));
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
     __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
     if (poisoned(a.poison)) return;  // block-uniform
@@ -822,40 +838,37 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     const DevMat* mats = LDS_MATS ? s_mats : a.mats;
     double* nd8 = s_nd + grp * kLdsStride;
     double* xb = s_xb + (EXACT ? grp * kXbStride : 0);
-    const long long nb = TWO ? (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo) : a.nEp / kEPB;
+    const long long nb = a.nEp / kEPB;
     // Batch schedule, as (first, stride, count):
-    //  map 0: each block walks a contiguous run of batches;
-    //  map 1: each XCD owns a contiguous run and its blocks stride through it together, so the
-    //         batches that share a node layer (one element layer apart) are processed close in
-    //         time on the same L2 (blocks are dealt round-robin over the 8 XCDs).
+    //  * owner assembly: each block walks a contiguous run of batches, in order (own_build's partition);
+    //  * otherwise each XCD owns a contiguous run and its blocks stride through it together, so the
+    //    batches that share a node layer (one element layer apart) are processed close in time on
+    //    the same L2 (blocks are dealt round-robin over the 8 XCDs; C3 element reads 2.39 -> 2.20 GB).
     long long first, stride, count;
-    if (OWN) {  // contiguous batch range per block, in order (own_build's partition)
+    if (OWN || gridDim.x % 8 != 0) {
         first = (long long)blockIdx.x * nb / gridDim.x;
         stride = 1;
         count = ((long long)blockIdx.x + 1) * nb / gridDim.x - first;
-    } else if (a.pipe_map == 1 && gridDim.x % 8 == 0) {
+    } else {
         const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, per = gridDim.x >> 3;
         const long long r0 = x * nb / 8, r1 = (x + 1) * nb / 8;
         first = r0 + j;
         stride = per;
         count = first < r1 ? (r1 - first + per - 1) / per : 0;
-    } else {
-        const long long lb = xcd_remap(blockIdx.x, gridDim.x);
-        first = lb * nb / gridDim.x;
-        stride = 1;
-        count = (lb + 1) * nb / gridDim.x - first;
     }
     if (count <= 0) return;  // block-uniform
     // iterations past the end are clamped to the last batch (loaded, never computed)
-    // (TWO: virtual batches, mapped to the two ranges; each call site takes its batch's step args)
     auto vb_of = [&](long long i) { return first + (i < count ? i : count - 1) * stride; };
-    auto elem_of = [&](long long i) { return (TWO ? two_step_batch(a, vb_of(i)) : vb_of(i)) * kEPB + grp; };
+    auto elem_of = [&](long long i) { return vb_of(i) * kEPB + grp; };
 
     ElemIn cur, nxt;
     int4 ent_cur = {0, 0, 0, 0}, ent_nxt = {0, 0, 0, 0};
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
-    load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(0)) : a, elem_of(0), k, cur);
+    if (EXACT)
+        load_node(a, cur);
+    else
+        load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // its first batch)
     constexpr int S = OS > 0 ? OS : 1;
@@ -864,15 +877,23 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
-        load_stage_b<ANY_PLASTIC, NT>(TWO ? two_step_args(a, vb_of(i + 1)) : a, elem_of(i + 1), k, nxt);
+        // (reference-order mode: its longer arithmetic holds more registers, so only the node
+        // gathers run a batch ahead; the Gauss-point state is loaded at the start of the step and
+        // first used after the Jacobian, B-bar and strain passes)
+        if (EXACT)
+            ;
+        else
+            load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
-        const ElemArgs ai = TWO ? two_step_args(a, vb_of(i)) : a;
-        if (EXACT)
-            elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT>(ai, mats, elem_of(i), k, nd8, xb, s_pus,
-                                                                            cur);
+        if (EXACT) {
+            load_node(a, cur);
+            load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
+            elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
+                                                                                 cur, sfe);
+        }
         else
-            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(ai, mats, elem_of(i), k, nd8, cur, sfe);
+            elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, cur, sfe);
         if (OWN) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
@@ -886,145 +907,103 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
 }
 
 // Runtime flags -> template instantiations.
-template <int MINW, bool EXACT, bool TWO>
+template <bool EXACT>
 static void launch_element_w(const ElemArgs& a, bool do_delete, bool store_triax, bool with_vol, unsigned grid,
                              hipStream_t s) {
     if (with_vol) {
-        hipLaunchKernelGGL((k_element<false, false, true, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_element<false, false, true, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     } else if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<true, true, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, true, false, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<true, false, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<true, false, false, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element<false, true, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, true, false, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
         else
-            hipLaunchKernelGGL((k_element<false, false, false, MINW, EXACT, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element<false, false, false, EXACT>), dim3(grid), dim3(kBlock), 0, s, a);
     }
 }
 
-template <bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, bool TWO>
+template <bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS>
 static void launch_pipe(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    const size_t dyn = (OS > 0 ? 24 * (size_t)a.own_slots : 0) + (LDS_MATS ? sizeof(DevMat) * (size_t)a.nmat : 0);
     if (do_delete) {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, OS>), dim3(grid),
+                               dim3(kBlock), dyn, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, OS>), dim3(grid),
+                               dim3(kBlock), dyn, s, a);
     } else {
         if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, LDS_MATS, NT, EXACT, OS>), dim3(grid),
+                               dim3(kBlock), dyn, s, a);
         else
-            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, TWO>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, LDS_MATS, NT, EXACT, OS>), dim3(grid),
+                               dim3(kBlock), dyn, s, a);
     }
 }
 
-template <bool ANY_PLASTIC, bool LDS_MATS, bool TWO>
-static void launch_element_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
-    if (a.exact) {  // reference-order kernel: Gauss-point state nontemporal when any is requested
-        if (a.gp_nt)
-            launch_pipe<ANY_PLASTIC, LDS_MATS, 3, true, TWO>(a, do_delete, store_triax, grid, s);
-        else
-            launch_pipe<ANY_PLASTIC, LDS_MATS, 0, true, TWO>(a, do_delete, store_triax, grid, s);
-        return;
-    }
-    if (ANY_PLASTIC && LDS_MATS && a.gp_nt) {
-        switch (a.gp_nt) {
-            case 1: launch_pipe<true, true, 1, false, TWO>(a, do_delete, store_triax, grid, s); break;
-            case 2: launch_pipe<true, true, 2, false, TWO>(a, do_delete, store_triax, grid, s); break;
-            default: launch_pipe<true, true, 3, false, TWO>(a, do_delete, store_triax, grid, s); break;
-        }
-        return;
-    }
-    launch_pipe<ANY_PLASTIC, LDS_MATS, 0, false, TWO>(a, do_delete, store_triax, grid, s);
-}
-
-template <bool ANY_PLASTIC, int NT, int OS>
-static void launch_own(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
-    if (do_delete) {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<true, true, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element_pipe<true, false, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
-    } else {
-        if (store_triax)
-            hipLaunchKernelGGL((k_element_pipe<false, true, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_element_pipe<false, false, ANY_PLASTIC, true, NT, false, false, OS>), dim3(grid),
-                               dim3(kBlock), 0, s, a);
-    }
-}
-
-template <bool ANY_PLASTIC, int NT>
-static void launch_own_s(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
-    if (a.own == 1)
-        launch_own<ANY_PLASTIC, NT, 1>(a, do_delete, store_triax, grid, s);
+template <bool ANY_PLASTIC, bool LDS_MATS, bool EXACT, int OS>
+static void launch_pipe_nt(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (a.gp_nt)
+        launch_pipe<ANY_PLASTIC, LDS_MATS, 3, EXACT, OS>(a, do_delete, store_triax, grid, s);
     else
-        launch_own<ANY_PLASTIC, NT, 2>(a, do_delete, store_triax, grid, s);
+        launch_pipe<ANY_PLASTIC, LDS_MATS, 0, EXACT, OS>(a, do_delete, store_triax, grid, s);
 }
 
-template <bool TWO>
-static hipError_t launch_element_t(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
-    const long long nb = TWO ? (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo) : a.nEp / kEPB;
-    if (nb <= 0) return hipSuccess;
-    if (a.pipe_blocks > 0 && !a.vol) {
-        const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
-        const bool lds = a.nmat <= kMaxLdsMats;
-        if (a.any_plastic) {
-            if (lds) launch_element_p<true, true, TWO>(a, do_delete, store_triax, grid, s);
-            else launch_element_p<true, false, TWO>(a, do_delete, store_triax, grid, s);
-        } else {
-            if (lds) launch_element_p<false, true, TWO>(a, do_delete, store_triax, grid, s);
-            else launch_element_p<false, false, TWO>(a, do_delete, store_triax, grid, s);
-        }
-        return hipGetLastError();
+template <bool ANY_PLASTIC, bool LDS_MATS, bool EXACT>
+static void launch_pipe_os(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    if (a.own == 1)
+        launch_pipe_nt<ANY_PLASTIC, true, EXACT, 1>(a, do_delete, store_triax, grid, s);
+    else if (a.own == 2)
+        launch_pipe_nt<ANY_PLASTIC, true, EXACT, 2>(a, do_delete, store_triax, grid, s);
+    else
+        launch_pipe_nt<ANY_PLASTIC, LDS_MATS, EXACT, 0>(a, do_delete, store_triax, grid, s);
+}
+
+template <bool EXACT>
+static void launch_pipe_p(const ElemArgs& a, bool do_delete, bool store_triax, unsigned grid, hipStream_t s) {
+    const bool lds = a.nmat <= kMaxLdsMats;
+    if (a.any_plastic) {
+        if (lds) launch_pipe_os<true, true, EXACT>(a, do_delete, store_triax, grid, s);
+        else launch_pipe_os<true, false, EXACT>(a, do_delete, store_triax, grid, s);
+    } else {
+        if (lds) launch_pipe_os<false, true, EXACT>(a, do_delete, store_triax, grid, s);
+        else launch_pipe_os<false, false, EXACT>(a, do_delete, store_triax, grid, s);
     }
-    const unsigned grid = (unsigned)nb;
-    if (a.exact) {
-        launch_element_w<2, true, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s);
-        return hipGetLastError();
-    }
-    switch (a.variant) {
-        case 3: launch_element_w<3, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        case 4: launch_element_w<4, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-        default: launch_element_w<2, false, TWO>(a, do_delete, store_triax, a.vol != nullptr, grid, s); break;
-    }
-    return hipGetLastError();
 }
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s) {
     if (a.nE <= 0) return hipSuccess;
     if (a.exact && !a.pusai) return hipErrorInvalidValue;
-    if (a.own) {  // owner-computed assembly: fused persistent kernel only (own_build sized its lists for it)
-        const long long nb = a.nEp / kEPB;
-        if (a.own > 2 || a.exact || a.two_step || a.vol || a.qatomic || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats ||
-            (a.gp_nt != 0 && a.gp_nt != 3) || !a.own_off || !a.own_list || !a.own_q || !a.own_dump)
+    const long long nb = a.nEp / kEPB;
+    if (nb <= 0) return hipSuccess;
+    if (a.own) {  // owner-computed assembly: persistent kernel only (own_build sized its lists for it)
+        if (a.own > 2 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
+            !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > 1024)
             return hipErrorInvalidValue;
         if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;
-        const unsigned grid = (unsigned)a.own_grid;
-        if (a.any_plastic) {
-            if (a.gp_nt) launch_own_s<true, 3>(a, do_delete, store_triax, grid, s);
-            else launch_own_s<true, 0>(a, do_delete, store_triax, grid, s);
-        } else {
-            if (a.gp_nt) launch_own_s<false, 3>(a, do_delete, store_triax, grid, s);
-            else launch_own_s<false, 0>(a, do_delete, store_triax, grid, s);
-        }
+        if (a.exact)
+            launch_pipe_p<true>(a, do_delete, store_triax, (unsigned)a.own_grid, s);
+        else
+            launch_pipe_p<false>(a, do_delete, store_triax, (unsigned)a.own_grid, s);
         return hipGetLastError();
     }
-    if (a.two_step) {
-        if (a.vol || a.t_rd || a.r1_lo < 0 || a.r2_lo < 0 || a.r1_hi < a.r1_lo || a.r2_hi < a.r2_lo ||
-            a.r1_hi * kEPB > a.nEp || a.r2_hi * kEPB > a.nEp)
-            return hipErrorInvalidValue;
-        return launch_element_t<true>(a, do_delete, store_triax, s);
+    if (a.pipe_blocks > 0 && !a.vol) {
+        const unsigned grid = (unsigned)std::min<long long>(nb, a.pipe_blocks);
+        if (a.exact)
+            launch_pipe_p<true>(a, do_delete, store_triax, grid, s);
+        else
+            launch_pipe_p<false>(a, do_delete, store_triax, grid, s);
+        return hipGetLastError();
     }
-    return launch_element_t<false>(a, do_delete, store_triax, s);
+    if (a.exact)
+        launch_element_w<true>(a, do_delete, store_triax, a.vol != nullptr, (unsigned)nb, s);
+    else
+        launch_element_w<false>(a, do_delete, store_triax, a.vol != nullptr, (unsigned)nb, s);
+    return hipGetLastError();
 }
 
 // Negative-Jacobian diagnostic (the reference prints a warning, v2/HAKAI_j.jl:1736-1739): counts
@@ -1136,36 +1115,21 @@ __device__ __forceinline__ void nodal_update(const NodalArgs& a, long long n, co
     }
 }
 
-// MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer; 3: owner-computed Q + rows. Compile-time modes keep the
-// kernel branch-free: a runtime branch makes the compiler drain all loads (vmcnt(0)) at the join,
-// which serialises the early node loads with the gather again.
-// TWO (NodalArgs::two_step): thread index v < n1 updates node r1_lo + v for step s, the others node
-// r2_lo + v - n1 for step s+1 (displacement buffers swapped, BC time ct2).
-template <int MODE, bool FEXT, bool AOS, bool EARLY, bool FE_NT = false, bool BCF = false, bool TWO = false>
-__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
+// MODE 0: padded [nN][8] table; 1: CSR; 2: Q from an uploaded buffer; 3: owner-computed Q + rows.
+// Compile-time modes keep the kernel branch-free: a runtime branch makes the compiler drain all loads
+// (vmcnt(0)) at the join, which serialises the node loads with the gather again. Blocks are dealt
+// to XCDs round-robin and each XCD walks its contiguous node chunk from the END (xcd_remap_rev):
+// the element kernel wrote each XCD's element range in ascending order, so the forces written last
+// (still in the Infinity Cache) are gathered first (C3: 0.180 -> 0.164 ms, DESIGN.md §2 k_nodal).
+template <int MODE, bool FEXT, bool BCF>
+__global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a) {
 #pragma clang fp contract(off)
-    if (poisoned(a0.poison)) return;
-    const unsigned lb = a0.reverse ? xcd_remap_rev(blockIdx.x, gridDim.x) : xcd_remap(blockIdx.x, gridDim.x);
-    const long long v = (long long)lb * kBlock + threadIdx.x;
-    NodalArgs a = a0;
-    long long n = v;
-    if (TWO) {
-        const long long n1 = a0.r1_hi - a0.r1_lo, n2 = a0.r2_hi - a0.r2_lo;
-        if (v >= n1 + n2) return;
-        if (v < n1) {
-            n = a0.r1_lo + v;
-        } else {
-            n = a0.r2_lo + (v - n1);
-            a.u = a0.u_pre_out;
-            a.u_pre_out = const_cast<double*>(a0.u);
-            a.bc.ct = a0.ct2;
-        }
-    } else if (n >= a.nN) {
-        return;
-    }
+    if (poisoned(a.poison)) return;
+    const unsigned lb = xcd_remap_rev(blockIdx.x, gridDim.x);
+    const long long n = (long long)lb * kBlock + threadIdx.x;
+    if (n >= a.nN) return;
     NodeIn in;
-    if (EARLY) nodal_load<FEXT>(a, n, in);
-    const long long cs = AOS ? 1 : a.cstride;  // compile-time 1: a row's 3 loads merge into 2
+    nodal_load<FEXT>(a, n, in);  // in flight with the incidence indices
     double Q0 = 0.0, Q1 = 0.0, Q2 = 0.0;
     if (MODE == 2) {
         Q0 = a.qbuf[3 * n + 0];
@@ -1190,9 +1154,9 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const double* p = a.fe + idx[j];
-            f[j][0] = gp_ld<FE_NT ? 1 : 0>(p);
-            f[j][1] = gp_ld<FE_NT ? 1 : 0>(p + cs);
-            f[j][2] = gp_ld<FE_NT ? 1 : 0>(p + 2 * cs);
+            f[j][0] = p[0];
+            f[j][1] = p[1];
+            f[j][2] = p[2];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1205,70 +1169,38 @@ __global__ __launch_bounds__(kBlock) void k_nodal(NodalArgs a0) {
         for (int j = j0; j < j1; ++j) {
             const double* f = a.fe + a.inc[j];
             Q0 += f[0];
-            Q1 += f[cs];
-            Q2 += f[2 * cs];
+            Q1 += f[1];
+            Q2 += f[2];
         }
     }
-    if (!EARLY) nodal_load<FEXT>(a, n, in);
     nodal_update<BCF>(a, n, in, Q0, Q1, Q2);
 }
 
-template <bool FEXT, bool AOS, bool EARLY, bool BCF, bool TWO>
-static void launch_nodal_e(const NodalArgs& a, unsigned grid, hipStream_t s) {
+template <bool FEXT, bool BCF>
+static void launch_nodal_m(const NodalArgs& a, unsigned grid, hipStream_t s) {
     if (a.qbuf)
-        hipLaunchKernelGGL((k_nodal<2, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<2, FEXT, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.own_q)
-        hipLaunchKernelGGL((k_nodal<3, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (a.inc8 && a.fe_nt)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, true, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<3, FEXT, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (a.inc8)
-        hipLaunchKernelGGL((k_nodal<0, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_nodal<0, FEXT, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((k_nodal<1, FEXT, AOS, EARLY, false, BCF, TWO>), dim3(grid), dim3(kBlock), 0, s, a);
-}
-
-template <bool FEXT, bool AOS, bool BCF, bool TWO>
-static void launch_nodal_f(const NodalArgs& a, unsigned grid, hipStream_t s) {
-    if (a.early)
-        launch_nodal_e<FEXT, AOS, true, BCF, TWO>(a, grid, s);
-    else
-        launch_nodal_e<FEXT, AOS, false, BCF, TWO>(a, grid, s);
-}
-
-template <bool FEXT, bool BCF, bool TWO>
-static void launch_nodal_a(const NodalArgs& a, unsigned grid, hipStream_t s) {
-    if (a.cstride == 1)
-        launch_nodal_f<FEXT, true, BCF, TWO>(a, grid, s);
-    else
-        launch_nodal_f<FEXT, false, BCF, TWO>(a, grid, s);
+        hipLaunchKernelGGL((k_nodal<1, FEXT, BCF>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
 hipError_t launch_nodal(const NodalArgs& a, hipStream_t s) {
     if (a.nN <= 0) return hipSuccess;
-    if (a.two_step) {  // chunked two-step schedule: no external force, no uploaded Q, no graph counter
-        if (a.fext || a.qbuf || a.bc.t_rd || a.r1_lo < 0 || a.r2_lo < 0 || a.r1_hi < a.r1_lo ||
-            a.r2_hi < a.r2_lo || a.r1_hi > a.nN || a.r2_hi > a.nN)
-            return hipErrorInvalidValue;
-        const long long nv = (a.r1_hi - a.r1_lo) + (a.r2_hi - a.r2_lo);
-        if (nv <= 0) return hipSuccess;
-        const unsigned grid = (unsigned)((nv + kBlock - 1) / kBlock);
-        if (a.bc_of_node)
-            launch_nodal_a<false, true, true>(a, grid, s);
-        else
-            launch_nodal_a<false, false, true>(a, grid, s);
-        return hipGetLastError();
-    }
     const unsigned grid = (unsigned)((a.nN + kBlock - 1) / kBlock);
     if (a.bc_of_node) {
         if (a.fext)
-            launch_nodal_a<true, true, false>(a, grid, s);
+            launch_nodal_m<true, true>(a, grid, s);
         else
-            launch_nodal_a<false, true, false>(a, grid, s);
+            launch_nodal_m<false, true>(a, grid, s);
     } else {
         if (a.fext)
-            launch_nodal_a<true, false, false>(a, grid, s);
+            launch_nodal_m<true, false>(a, grid, s);
         else
-            launch_nodal_a<false, false, false>(a, grid, s);
+            launch_nodal_m<false, false>(a, grid, s);
     }
     return hipGetLastError();
 }
@@ -1305,7 +1237,7 @@ hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s) {
 // node averages for output.
 // ---------------------------------------------------------------------------------------------
 __global__ void k_gather_q(const int* __restrict__ ptr, const int* __restrict__ inc, const double* __restrict__ fe,
-                           long long cs, double* Q, long long nN) {
+                           double* Q, long long nN) {
 #pragma clang fp contract(off)
     const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= nN) return;
@@ -1313,19 +1245,18 @@ __global__ void k_gather_q(const int* __restrict__ ptr, const int* __restrict__ 
     for (int j = ptr[n]; j < ptr[n + 1]; ++j) {
         const double* f = fe + inc[j];
         q0 += f[0];
-        q1 += f[cs];
-        q2 += f[2 * cs];
+        q1 += f[1];
+        q2 += f[2];
     }
     Q[3 * n + 0] = q0;
     Q[3 * n + 1] = q1;
     Q[3 * n + 2] = q2;
 }
 
-hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, long long cstride, double* Q,
-                           long long nN, hipStream_t s) {
+hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
+                           hipStream_t s) {
     if (nN <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, inc_ptr, inc, fe, cstride,
-                       Q, nN);
+    hipLaunchKernelGGL(k_gather_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, inc_ptr, inc, fe, Q, nN);
     return hipGetLastError();
 }
 

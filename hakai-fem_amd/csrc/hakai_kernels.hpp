@@ -20,8 +20,7 @@ struct ElemArgs {
     double* eqps;          // [ld]
     double* yield;         // [ld]
     double* triax;         // [ld]
-    double* fe;            // element nodal forces: component c of (e, k) at fe[base + c*cstride],
-    long long cstride;     // base = 24e+3k (cstride 1, Qe order) or 3k*nEp+e (cstride nEp)
+    double* fe;            // element nodal forces [nEp][8][3] (the reference's Qe column order)
     double* vol;           // optional current volume per element (elementVolume, :1169)
     long long nE;          // elements
     long long nEp;         // elements padded to whole 32-element batches (padding: flag 0)
@@ -31,27 +30,14 @@ struct ElemArgs {
     const double* t_rd;    // graph mode: step number = *t_rd + 1 (read on device), else step_i
     double* t_wr;          // graph mode: block 0 stores *t_rd + 1 here (the next step's t_rd)
     int any_plastic;       // some material has a *Plastic table (eqps/yield are live)
-    int variant;           // occupancy variant of the simple kernel: min waves per SIMD (2, 3, 4)
     int pipe_blocks;        // > 0: persistent pipelined kernel with this many blocks
-    int pipe_map;           // batch schedule: 0 contiguous per block, 1 contiguous per XCD, strided
     int nmat;               // materials (staged in LDS when <= kMaxLdsMats)
-    int gp_nt;              // 1: Gauss-point state streamed with nontemporal loads/stores
+    int gp_nt;              // 1: Gauss-point state streamed with nontemporal loads and stores
     int exact;              // 1: reference-order arithmetic (elem_step_exact), bit-identical to
                             //    cal_stress_hexa; 0: fused single-pass form (elem_step)
     const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
-    double* qatomic;        // null; the timing diagnostic "diag_atomic_q": node forces are added
-                            // straight into this 3nN array with FP64 atomics (no fe round trip,
-                            // nondeterministic summation order: results not bit-reproducible)
-    long long fe_mask;      // -1; 0 only in the timing diagnostic "diag_no_assembly" (all force
-                            // rows land on one dummy row: no fe traffic, results invalid)
     const int* poison;      // [0] != 0: a contact buffer overflowed in this call; every state-writing
                             // kernel is a no-op from then on (the state stays the last good step's)
-    // Two-step chunked schedule (tuning "tblock_mb", hakai_step): when two_step is set the launch
-    // covers batches [r1_lo, r1_hi) of step step_i (u, u_pre as above) and batches [r2_lo, r2_hi)
-    // of step step_i + 1, whose displacement buffers are the other way round (u_pre holds u_{s+1},
-    // u holds u_s). Batch ranges are element batches of kEPB.
-    int two_step;
-    long long r1_lo, r1_hi, r2_lo, r2_hi;
     // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): logical block lb of
     // the persistent kernel walks batches [lb*nb/G, (lb+1)*nb/G) in order and sums every node force
     // it holds in LDS, in element order, from a per-batch list of 16-B entries
@@ -64,6 +50,7 @@ struct ElemArgs {
     const int* own_off;
     const int4* own_list;
     int own_nop;            // index of a no-op entry (list padding)
+    int own_slots;          // LDS running-sum slots the lists use (1..1024)
     double* own_q;          // [nN][3]
     double* own_rows;       // [rows][3]
     double* own_dump;       // [grid][8] target of the no-op entries' stores
@@ -95,20 +82,11 @@ struct NodalArgs {
     const double* fe;
     const double* qbuf;    // if non-null: Q taken from this 3nN buffer (uploaded state), not from fe
     const double* fext;    // external force 3nN or null (= 0)
-    long long cstride;     // component stride of fe (inc / inc8 hold base offsets)
-    int early;             // 1: node operands loaded before the gather (in flight with the indices)
-    int fe_nt;             // 1: element forces gathered with nontemporal loads (read once)
-    int reverse;           // 1: each XCD walks its node chunk from the end (xcd_remap_rev)
     long long nN;
     double dt;
     const int* bc_of_node; // one GPU: [nN] first entry of `bc` of each node (-1 none); the nodal
     BCArgs bc;             // kernel then applies the BCs itself (no k_bc launch)
     const int* poison;     // see ElemArgs::poison
-    // Two-step chunked schedule (see ElemArgs): nodes [r1_lo, r1_hi) get step s's update (u, u_pre_out,
-    // bc.ct) and nodes [r2_lo, r2_hi) step s+1's, with u and u_pre_out swapped and BC time ct2.
-    int two_step;
-    long long r1_lo, r1_hi, r2_lo, r2_hi;
-    double ct2;
     // Owner-computed assembly (ElemArgs::own): Q = own_q[n] + own_rows[own_ridx[own_rp[n]]] + ...
     // in element order
     const double* own_q;
@@ -126,8 +104,7 @@ hipError_t launch_bc(const BCArgs& a, hipStream_t s);
 hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s);
 
 // Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
-hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, long long cstride, double* Q,
-                           long long nN,
+hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
                            hipStream_t s);
 // AoS [gp][6] <-> SoA [6][ld] conversions used at upload/download.
 hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, long long ld, hipStream_t s);

@@ -191,7 +191,7 @@ class Solver:
         check(self.L.hakai_set_tuning(self.ctx, key.encode(), int(value)))
 
     def stat(self, key: str) -> int:
-        """Step-loop counter (hakai_stat): graph_steps, tblock_pairs, own_steps, own_rows, own_entries."""
+        """Step-loop counter (hakai_stat): graph_steps, own_steps, own_rows, own_entries, own_superbatch, own_slots."""
         n = I64(0)
         check(self.L.hakai_stat(self.ctx, key.encode(), ctypes.byref(n)))
         return n.value

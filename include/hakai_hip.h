@@ -119,10 +119,10 @@ int hakai_step(hakai_ctx* ctx, double t_first, int64_t n_steps, double d_time);
  * uploaded Q, contact in its steady state -- and the call's last step always runs in stream mode.
  * Results are bit-identical to stream mode. hakai_graph_steps returns the steps run from graphs. */
 int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
-/* Step-loop counters (tests, tools; no reference counterpart): "graph_steps", "tblock_pairs" (step
- * pairs run with the two-step chunked schedule), "own_steps" (element steps with owner-computed
- * assembly), "own_rows" / "own_entries" (its exported rows / per-batch entries for this mesh),
- * "own_superbatch" (batches of 32 elements per LDS summing pass: 2, or 1 for wide meshes). */
+/* Step-loop counters (tests, tools; no reference counterpart): "graph_steps", "own_steps" (element
+ * steps with owner-computed assembly), "own_rows" / "own_entries" (its exported rows / per-batch
+ * entries for this mesh), "own_superbatch" (batches of 32 elements per LDS summing pass: 2, or 1
+ * for wide meshes), "own_slots" (LDS running sums a block keeps open at most). */
 int hakai_stat(hakai_ctx* ctx, const char* key, int64_t* value);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
@@ -172,32 +172,21 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       trajectories bit-identical to the reference's expression order; the mode
  *                       hakai_run_inp uses), 0 (default for hakai_step): fused single-pass element
  *                       kernel (rounding-level differences); env HAKAI_ELEM_EXACT sets the default;
- *   "elem_exact_pipe"   1: elem_exact mode also uses the persistent kernel (default 0: one batch
- *                       per block, faster for the reference-order arithmetic);
  *   "elem_pipe_blocks"  >0: persistent software-pipelined element kernel on that many blocks
  *                       (default 512); 0: one batch of 32 elements per block;
  *   "elem_pipe_min"     persistent kernel only with >= this many batches per block (default 2);
- *   "elem_map"          batch schedule: 1 (default) contiguous per XCD, 0 contiguous per block;
- *   "elem_minw"         2|3|4: occupancy variant of the one-batch kernel;
- *   "elem_gp_nt"        0..3: Gauss-point state with nontemporal loads (bit 0) / stores (bit 1);
- *   "fe_layout"         element-force layout: 0 (default) Qe rows, 1 component SoA;
+ *   "elem_gp_nt"        1 (default): Gauss-point state streamed with nontemporal loads and stores;
+ *   "own_assembly"      1 (default; env HAKAI_OWN_ASSEMBLY): the persistent element kernel sums node
+ *                       forces in LDS in element order and hands the nodal update Q (+ the rows of
+ *                       nodes shared between blocks) instead of the per-element force array; meshes
+ *                       it does not fit use that array (hakai_stat "own_steps");
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
- *   "nodal_early"       1 (default): node operands loaded before the force gather;
- *   "nodal_reverse"     1 (default): each XCD walks its node chunk from its end;
- *   "nodal_fe_nt"       1: element forces gathered with nontemporal loads;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
- *   "own_assembly"      1 (default; env HAKAI_OWN_ASSEMBLY): one GPU, fused persistent kernel: the
- *                       element kernel sums node forces in LDS in element order and hands the nodal
- *                       update Q (+ the rows of nodes shared between blocks) instead of the per-element
- *                       force array; meshes it does not fit use that array (hakai_stat "own_steps");
- *   "tblock_mb"         > 0: two-step chunked schedule with chunks of this many MB of Gauss-point
- *                       state (one GPU, no contact; default 0 = off: measured slower on C3);
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
  *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
  *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy;
  *   "contact_divide"    multi-GPU contact: 1 (default) divided search, 0 replicated search;
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
- *   "contact_tri_wave"  1: one wave per candidate triangle in the triangle test (default 0: 32 lanes);
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0). */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);

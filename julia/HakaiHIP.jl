@@ -165,7 +165,7 @@ function graph_steps(c::Ctx)
     check(ccall((:hakai_graph_steps, lib), Cint, (Ptr{Cvoid}, Ref{Int64}), c.p, n))
     return n[]
 end
-# step-loop counters: "graph_steps", "tblock_pairs", "own_steps", "own_rows", "own_entries"
+# step-loop counters: "graph_steps", "own_steps", "own_rows", "own_entries", "own_superbatch", "own_slots"
 function stat(c::Ctx, key::AbstractString)
     n = Ref{Int64}(0)
     check(ccall((:hakai_stat, lib), Cint, (Ptr{Cvoid}, Cstring, Ref{Int64}), c.p, key, n))

@@ -1,8 +1,12 @@
-"""The exact element kernel's x/3.0 (div3 in csrc/hakai_kernels.hip: q = x*y, y = RN(1/3), then
-q + (x - 3q)*y with fused multiply-adds) must equal IEEE division bit for bit. Checked here on the
-CPU with the same three operations (gcc, -mfma) against `x / 3.0` on 2e7 doubles: random bit
-patterns over the exponent range the kernel meets, multiples of 3 (exact quotients), values next to
-powers of two, and signed zeros."""
+"""The exact element kernel's divisions must equal IEEE division bit for bit:
+  * x/3.0 (div3 in csrc/hakai_kernels.hip: q = x*y, y = RN(1/3), then q + (x - 3q)*y with fused
+    multiply-adds), checked against `x / 3.0` on 2e7 doubles: random bit patterns over the exponent
+    range the kernel meets, multiples of 3 (exact quotients), values next to powers of two; a zero
+    comes out as +0 (the kernel's zero-sign argument, tests/test_exact_chains.py);
+  * a/b given rb = RN(1/b) (div_cr: two Newton-Markstein corrections of a*rb), checked against
+    `a / b` on 2e7 random pairs over the kernel's exponent range and on pairs whose quotient lies
+    next to a rounding midpoint (the hard cases of correct rounding).
+Same operations on the CPU (gcc, -mfma, no contraction)."""
 import ctypes
 import os
 import subprocess
@@ -17,16 +21,33 @@ static double div3(double x) {
     const double y = 1.0 / 3.0;
     const double q = x * y;
     const double r = fma(-q, 3.0, x);
-    const double q1 = fma(r, y, q);
-    return x == 0.0 ? x : q1;
+    return fma(r, y, q);
 }
-/* number of x with div3(x) != x / 3.0 (bitwise) */
+/* number of x with div3(x) != x / 3.0 (bitwise; a zero may come out as +0) */
 int64_t check(const double* x, int64_t n) {
     int64_t bad = 0;
     for (int64_t i = 0; i < n; ++i) {
         const double a = div3(x[i]), b = x[i] / 3.0;
-        if (memcmp(&a, &b, sizeof a) != 0) ++bad;
+        if (x[i] == 0.0 ? a != 0.0 : memcmp(&a, &b, sizeof a) != 0) ++bad;
     }
+    return bad;
+}
+static double div_cr(double a, double b, double rb) {
+    const double q0 = a * rb;
+    const double q1 = fma(fma(-q0, b, a), rb, q0);
+    return fma(fma(-q1, b, a), rb, q1);
+}
+/* pairs with div_cr(a, b) != a / b (bitwise); *one: pairs where ONE correction would not do */
+int64_t check_div(const double* a, const double* b, int64_t n, int64_t* one) {
+    int64_t bad = 0, b1 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double rb = 1.0 / b[i];
+        const double x = div_cr(a[i], b[i], rb), y = a[i] / b[i];
+        const double q0 = a[i] * rb, q1 = fma(fma(-q0, b[i], a[i]), rb, q0);
+        if (memcmp(&x, &y, sizeof x) != 0) ++bad;
+        if (memcmp(&q1, &y, sizeof q1) != 0) ++b1;
+    }
+    *one = b1;
     return bad;
 }
 """
@@ -41,7 +62,16 @@ def _lib(tmp_path):
     L = ctypes.CDLL(str(so))
     L.check.restype = ctypes.c_int64
     L.check.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    L.check_div.restype = ctypes.c_int64
+    L.check_div.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
     return L
+
+
+def _rand_doubles(rng, n, lo, hi, signed=True):
+    mant = rng.integers(0, 1 << 52, size=n, dtype=np.uint64)
+    expo = rng.integers(1023 + lo, 1023 + hi, size=n, dtype=np.uint64)
+    sign = rng.integers(0, 2, size=n, dtype=np.uint64) if signed else np.zeros(n, np.uint64)
+    return ((sign << np.uint64(63)) | (expo << np.uint64(52)) | mant).view(np.float64)
 
 
 def test_div3_equals_ieee_division(tmp_path):
@@ -61,3 +91,30 @@ def test_div3_equals_ieee_division(tmp_path):
     for arr in (x, extra):
         a = np.ascontiguousarray(arr, np.float64)
         assert L.check(a.ctypes.data, a.size) == 0
+
+
+def test_div_cr_equals_ieee_division(tmp_path):
+    L = _lib(tmp_path)
+    rng = np.random.default_rng(1)
+    n = 10_000_000
+    one = ctypes.c_int64(0)
+    # random pairs: numerators over the stresses' range, positive divisors (q, V of the kernel)
+    a = _rand_doubles(rng, n, -60, 60)
+    b = _rand_doubles(rng, n, -30, 30, signed=False)
+    assert L.check_div(a.ctypes.data, b.ctypes.data, n, ctypes.byref(one)) == 0
+    # quotients next to a rounding midpoint: a = RN(b * (q + ulp(q)/2)) for random q, b
+    m = n // 2
+    q = _rand_doubles(rng, m, -20, 20)
+    b2 = _rand_doubles(rng, m, -20, 20, signed=False)
+    mid = q.astype(np.longdouble) + (np.spacing(q).astype(np.longdouble) / 2)
+    a2 = np.ascontiguousarray((b2.astype(np.longdouble) * mid).astype(np.float64))
+    for da in (0, 1, -1):  # and their neighbours
+        aa = np.ascontiguousarray(a2 if da == 0 else np.nextafter(a2, da * np.inf))
+        assert L.check_div(aa.ctypes.data, b2.ctypes.data, m, ctypes.byref(one)) == 0
+    # exact quotients and zeros
+    b3 = _rand_doubles(rng, m, -20, 20, signed=False)
+    q3 = (rng.integers(1, 1 << 40, size=m).astype(np.float64)) * np.exp2(rng.integers(-30, 30, m))
+    a3 = np.ascontiguousarray(q3 * b3)
+    ok = (a3 / b3) == q3
+    a3, b3 = np.ascontiguousarray(a3[ok]), np.ascontiguousarray(b3[ok])
+    assert L.check_div(a3.ctypes.data, b3.ctypes.data, a3.size, ctypes.byref(one)) == 0

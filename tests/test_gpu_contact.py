@@ -228,24 +228,3 @@ def test_fused_small_deck_phases_bitexact(flag, graph):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
 
 
-@pytest.mark.parametrize("flag", [1, 2])
-def test_triangle_search_variants_bitexact(flag):
-    """The triangle test's two launch shapes (tuning contact_tri_wave: 32 lanes per candidate
-    triangle, or a whole wave per triangle splitting each bucket over two lanes) find the same
-    events: the trajectory, deletions and event counters equal bit for bit, with self-contact and
-    deletions."""
-    m = mesh.two_body_model(plate=(8, 8, 1), impactor=(3, 3, 4), v=-4e5, d_time=2e-8, n_steps=400,
-                            contact_flag=flag)
-    out = []
-    for wave in (0, 1):
-        with Solver(m) as sv:
-            sv.set_tuning("contact_tri_wave", wave)
-            sv.step(1, 250)
-            sv.step(251, m.n_steps - 250)
-            out.append((sv.download(), [tuple(int(v) for v in x) for x in sv.deleted()], sv.contact_stats()))
-    (a, da, sa), (b, db, sb) = out
-    assert sa["max_events"] > 0
-    assert db == da
-    assert sb["max_events"] == sa["max_events"] and sb["events"] == sa["events"]
-    for k in ("disp", "disp_pre", "velo", "integ_stress", "integ_eq_plastic_strain", "element_flag"):
-        assert np.array_equal(getattr(a, k), getattr(b, k)), k

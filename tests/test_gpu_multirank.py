@@ -15,13 +15,12 @@ from util import fast_deletion_bar
 pytestmark = pytest.mark.gpu
 
 
-def _run_group(glob, world, n_steps, key, fe_layout=0):
+def _run_group(glob, world, n_steps, key):
     nx = ny = 2
     parts = [dist.slab_partition(glob, r, world, nx, ny) for r in range(world)]
     svs = []
     for r, (loc, diag, iface) in enumerate(parts):
         sv = Solver(loc, diag_M=diag)
-        sv.set_tuning("fe_layout", fe_layout)
         sv.set_element_offset(loc.global_element_offset)
         sv.comm_init_local(r, world, key)
         sv.set_interface(*iface)
@@ -35,8 +34,8 @@ def _run_group(glob, world, n_steps, key, fe_layout=0):
     return out
 
 
-@pytest.mark.parametrize("world,fe_layout", [(2, 0), (3, 0), (2, 1)])
-def test_local_group_bitexact(world, fe_layout):
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_group_bitexact(world):
     glob = fast_deletion_bar(2, 2, 12)
     n = 1200
     with Solver(glob) as sv:
@@ -44,7 +43,7 @@ def test_local_group_bitexact(world, fe_layout):
         g = sv.download()
         gdel = [tuple(x) for x in sv.deleted()]
     assert len(gdel) > 0, "config must delete elements"
-    parts = _run_group(glob, world, n, key=100 + 10 * fe_layout + world, fe_layout=fe_layout)
+    parts = _run_group(glob, world, n, key=100 + world)
     dels = sorted(d for _, _, dl in parts for d in dl)
     assert dels == gdel
     for loc, st, _ in parts:

@@ -11,7 +11,7 @@ import pytest
 
 from hakai import mesh
 from hakai.solver import Solver
-from test_gpu_tblock import _same, _shuffled
+from util import same_state as _same, shuffled as _shuffled
 from util import fast_deletion_bar, small_bar
 
 pytestmark = pytest.mark.gpu
@@ -173,7 +173,7 @@ def test_own_isolated_node_and_ragged_batch():
     g1, _, s1 = _run(m, [(1, 151), (152, 149)], PIPE, 1)
     assert s1["own_steps"] == 300
     # the isolated node has no mass (the reference's update divides by it): compare NaN as equal
-    from test_gpu_tblock import STATE
+    from util import STATE
     for k in STATE:
         assert np.array_equal(getattr(g1, k), getattr(g0, k), equal_nan=True), k
     assert np.all(g1.Q[3 * extra - 3:] == 0.0)

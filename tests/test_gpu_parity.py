@@ -215,13 +215,13 @@ def test_hakai_driver_async_output_equals_sync(tmp_path, monkeypatch):
     assert "\nCELLS 4 36\n" in (tmp_path / "a" / "file100.vtk").read_text()
 
 
-@pytest.mark.parametrize("tuning", [{"fe_layout": 1}, {"elem_map": 1}, {"fe_layout": 1, "elem_map": 1},
-                                    {"elem_pipe_blocks": 0, "fe_layout": 1}, {"elem_map": 0},
-                                    {"nodal_padded": 0}, {"nodal_padded": 0, "fe_layout": 1},
-                                    {"elem_pipe_min": 2}, {"fuse_bc": 0}])
+@pytest.mark.parametrize("tuning", [{"elem_pipe_blocks": 0}, {"elem_pipe_blocks": 24}, {"nodal_padded": 0},
+                                    {"elem_pipe_min": 2}, {"fuse_bc": 0}, {"elem_gp_nt": 0},
+                                    {"own_assembly": 0}, {"own_assembly": 0, "nodal_padded": 0}])
 def test_tuning_variants_bitexact(tuning):
-    """Force layouts (AoS rows / component SoA) and batch schedules change only where bytes
-    live and which block computes what: the trajectory is bit-identical to the default."""
+    """Kernel forms (one-batch / persistent), grids, the CSR force gather, cache policies and the
+    assembly path change only where bytes live and which block computes what: the trajectory is
+    bit-identical to the default."""
     m = fast_deletion_bar(3, 3, 10)
     n = 1200
     with Solver(m) as sv:
@@ -234,9 +234,6 @@ def test_tuning_variants_bitexact(tuning):
         for k, v in tuning.items():
             sv.set_tuning(k, v)
         sv.step(1, 500)
-        if "fe_layout" in tuning:   # switching mid-run converts the live forces
-            sv.set_tuning("fe_layout", 0)
-            sv.set_tuning("fe_layout", tuning["fe_layout"])
         sv.step(501, n - 500)
         g = sv.download()
         dels = [tuple(x) for x in sv.deleted()]

@@ -34,3 +34,47 @@ def random_state(rng, nE, scale=300.0, yield_frac=0.5):
     eq[rng.random(8 * nE) < 0.3] = 0.0
     ys = 755.0 + 50 * eq
     return st, sn, eq, ys
+
+
+# State arrays a bit-exact comparison covers (hakai.solver.State fields).
+STATE = ("disp", "disp_pre", "integ_stress", "integ_strain", "integ_yield_stress", "integ_eq_plastic_strain",
+         "element_flag", "Q", "Qe")
+
+
+def bits(x):
+    """The IEEE bit patterns of a float array (so -0.0 != +0.0), or the array itself for integers."""
+    x = np.ascontiguousarray(x)
+    return x.view(np.uint64) if x.dtype == np.float64 else x
+
+
+def bitwise_equal(a, b):
+    return np.shape(a) == np.shape(b) and np.array_equal(bits(a), bits(b))
+
+
+def same_state(a, b, keys=STATE, triax=True):
+    """Two downloaded states are identical bit for bit (signed zeros included)."""
+    for k in keys:
+        x, y = getattr(a, k), getattr(b, k)
+        assert bitwise_equal(x, y), f"{k}: max rel diff {rel_err(x, y):.3e}"
+    if triax:
+        assert bitwise_equal(a.integ_triax_stress, b.integ_triax_stress)
+
+
+def shuffled(m: Model, seed: int) -> Model:
+    """The same model with randomly permuted element and node numbering."""
+    rng = np.random.default_rng(seed)
+    nN, nE = m.nNode, m.nElement
+    pe = rng.permutation(nE)                 # new element i = old element pe[i]
+    pn = rng.permutation(nN)                 # new node j = old node pn[j]
+    newid = np.empty(nN, np.int64)
+    newid[pn] = np.arange(nN)                # old node -> new (0-based)
+
+    def dof(d):  # 1-based dof of an old node -> 1-based dof of its new number
+        d = np.asarray(d, np.int64)
+        n, c = (d - 1) // 3, (d - 1) % 3
+        return 3 * newid[n] + c + 1
+
+    bc = [BCGroup([(dof(d), v) for d, v in g.entries], g.amp_time, g.amp_value) for g in m.bc]
+    return Model(m.coordmat[pn], newid[m.elementmat[pe] - 1] + 1, m.element_material[pe], m.materials, bc=bc,
+                 ic_dofs=dof(m.ic_dofs), ic_values=np.asarray(m.ic_values), d_time=m.d_time,
+                 end_time=m.end_time, mass_scaling=m.mass_scaling, name=m.name + "_shuffled")

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--serial", type=int, default=1,
                     help="multi-rank: drain each rank's phase before the next rank's (tuning group_serial), so "
                          "the per-rank kernel timings are not inflated by the ranks sharing this one GPU")
-    ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_tri_wave=1")
+    ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_divide=0")
     a = ap.parse_args()
     a.tuning = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in a.tuning.split(",") if kv]
     if a.ranks > 1:

@@ -36,7 +36,8 @@ sv.step(1, 400)
 sv.sync()
 t = 401
 res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
-DEFAULTS = {"elem_exact_pipe": 0, "elem_minw": 2, "elem_exact": 0, "diag_no_assembly": 0, "diag_atomic_q": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_map": 1, "fe_layout": 0, "nodal_early": 1, "elem_gp_nt": 3, "nodal_fe_nt": 0, "nodal_reverse": 1, "tblock_mb": 0, "own_assembly": 1}
+DEFAULTS = {"elem_exact": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_pipe_min": 2, "elem_gp_nt": 1,
+            "own_assembly": 1}
 for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
@@ -48,7 +49,6 @@ for r in range(a.rounds):
         t += a.steps
         el, nd = sv.profile_read(K_ELEMENT), sv.profile_read(K_NODAL)
         sv.profile(False)
-        # per STEP (a variant may launch a kernel several times per step: tblock_mb)
         res[name]["el"].append(el[0] / a.steps)
         res[name]["nd"].append(nd[0] / a.steps)
         sv.sync()  # wall time without profiling events
