@@ -586,6 +586,7 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
                                c->d_mats, c->nE, c->nEp, c->ld, s));
     c->h_velo0.assign(fn, 0.0);
     c->q_from_buf = false;
+    c->fe_ok = c->triax_ok = true;
     c->steps_done = 0;
     c->poison_halt = false;
     HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), s));
@@ -675,6 +676,7 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
     c->poison_halt = false;
+    c->fe_ok = c->triax_ok = true;
     hkc::comm_reset(c);
     c->state_ok = true;
     if (c->contact) {
@@ -687,6 +689,12 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
 int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
     if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
     if (!c->state_ok) return fail(HAKAI_ERR_STATE, "download_state without state");
+    if (st->Qe && !c->fe_ok)
+        return fail(HAKAI_ERR_STATE, "download_state: Qe is not available after a call whose last steps a contact "
+                    "overflow skipped (owner-computed assembly keeps node sums only); Q is -- or step once more");
+    if (st->integ_triax_stress && !c->triax_ok)
+        return fail(HAKAI_ERR_STATE, "download_state: integ_triax_stress is not available after a call whose last "
+                    "steps a contact overflow skipped (it is stored on a call's last step); step once more");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const size_t fn = 3 * (size_t)c->nN, nGP = 8 * (size_t)c->nE;
@@ -714,7 +722,10 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
         } else {
             double* tmp = nullptr;
             HIPCHK(dalloc(&tmp, fn));
-            HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, tmp, c->nN, s));
+            if (c->own_valid)  // the last element step's owner-computed sums (fe may be stale)
+                HIPCHK(hk::launch_own_q(c->d_own_q, c->d_own_rp, c->d_own_ridx, c->d_own_rows, tmp, c->nN, s));
+            else
+                HIPCHK(hk::launch_gather_q(c->d_inc_ptr, c->d_inc, c->d_fe, tmp, c->nN, s));
             HIPCHK(hipMemcpyAsync(st->Q, tmp, fn * sizeof(double), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             dfree(tmp);
@@ -951,12 +962,28 @@ static long long own_grid(const hakai_ctx* c) {
 // This step's element update uses owner-computed assembly (builds the lists on first use). The
 // grid is the persistent kernel's, or 8x that (blocks then run in waves) when the default ranges
 // span so much of a wide cross-section that too many sums stay open in a block.
+// Owner assembly stops being used while the previous element step's forces exist only as its
+// node sums (a tuning change, a list rebuild): hand the next nodal update Q through the uploaded-Q
+// buffer, the same bits (k_own_q = k_nodal's own additions). Multi-GPU ranks cannot: their next
+// interface fix needs the per-contribution rows.
+static int own_materialize(hakai_ctx* c) {
+    if (!c->own_valid) return 0;
+    if (c->comm)
+        return fail(HAKAI_ERR_STATE, "owner-computed assembly cannot be switched off or rebuilt on a multi-GPU rank "
+                    "mid-run: upload or reset the state first");
+    HIPCHK(hk::launch_own_q(c->d_own_q, c->d_own_rp, c->d_own_ridx, c->d_own_rows, c->d_qbuf, c->nN, c->stream));
+    c->q_from_buf = true;
+    c->own_valid = false;
+    return 0;
+}
+
 static bool own_use(hakai_ctx* c) {
     if (!c->own_assembly || c->nmat > hk::kMaxLdsMats || c->nE <= 0)
         return false;
     const long long G0 = own_grid(c);
     if (G0 <= 0) return false;
     if (c->own_for_g0 == G0) return c->own_built_g > 0;  // built (or found not to fit) for this grid
+    if (c->own_valid && own_materialize(c)) return false;  // (multi-GPU: step_once reports it)
     const long long nb = c->nEp / 32;
     bool ok = false;
     for (long long G : {G0, 8 * G0}) {
@@ -993,13 +1020,16 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     na.inc = c->d_inc;
     na.inc8 = c->d_inc8;
     na.fe = c->d_fe;
+    // owner-computed assembly: Q from the previous element step's sums (else the fe gather)
+    const bool own = own_use(c);
+    if (c->own_valid && !own) {  // switched off (or the lists could not be rebuilt)
+        if (int r = own_materialize(c)) return r;
+    }
     na.qbuf = c->q_from_buf ? c->d_qbuf : nullptr;
     na.fext = nullptr;
     na.nN = c->nN;
     na.dt = d_time;
     na.bc_of_node = nullptr;
-    // owner-computed assembly: Q from the previous element step's sums (else the fe gather)
-    const bool own = own_use(c);
     const bool own_q = c->own_valid && !na.qbuf;
     na.own_q = own_q ? c->d_own_q : nullptr;
     na.own_rp = own_q ? c->d_own_rp : nullptr;
@@ -1078,6 +1108,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     hkc::prof_end(c, &ep);
     c->own_valid = own;
     c->own_steps += own ? 1 : 0;
+    c->fe_ok = !own || last;  // owner assembly stores fe on a call's last step only
+    c->triax_ok = last;
     rc = hkc::comm_post_element(c, (long long)t);
     if (rc) return rc;
     rc = hkc::contact_post_step(c);
@@ -1140,6 +1172,8 @@ static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
         hkc::contact_graph_advance(c, t + len - 1);
         c->q_from_buf = false;
         c->own_steps += c->own_valid ? len : 0;  // captured in the steady state: every step or none
+        c->fe_ok = !c->own_valid;                 // (a captured step is never a call's last)
+        c->triax_ok = false;
         c->steps_done += len;
         c->last_dt = d_time;
     }
@@ -1152,7 +1186,8 @@ static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
 // End of a stepping call: the contact overflow check. An overflow poisoned step p: the device's
 // state-writing kernels of steps p.. were no-ops, so the device holds the state after step p-1;
 // bring the host's view back to that step.
-static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, long long done0) {
+static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, long long done0, bool fe_ok0,
+                       bool triax_ok0) {
     const int rc = hkc::contact_check(c);
     if (rc && c->contact) {
         int pz[2] = {0, 0};
@@ -1162,6 +1197,9 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, 
             if (good >= 0 && good <= n_steps) {
                 c->cur = (good & 1) ? 1 - cur0 : cur0;
                 c->steps_done = done0 + good;
+                // the call's last step (the one that stores fe and triax) did not run
+                c->fe_ok = good == 0 ? fe_ok0 : !c->own_valid;
+                c->triax_ok = good == 0 ? triax_ok0 : false;
             }
             hkc::graph_invalidate(c);
             hkc::contact_after_overflow(c, c->steps_done);
@@ -1187,6 +1225,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     (void)own_use(c);  // owner-assembly lists are built here, never inside a graph capture
     const int cur0 = c->cur;
     const long long done0 = c->steps_done;
+    const bool fe_ok0 = c->fe_ok, triax_ok0 = c->triax_ok;
     int64_t it = 0;
     while (it < n_steps) {
         const double t = t_first + (double)it;
@@ -1205,7 +1244,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         }
         if (rc) return rc;
     }
-    return finish_call(c, t_first, n_steps, cur0, done0);
+    return finish_call(c, t_first, n_steps, cur0, done0, fe_ok0, triax_ok0);
 }
 
 int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
@@ -1214,6 +1253,7 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
                                                   (long long)n_steps, d_time);
     std::vector<int> cur0(n);
     std::vector<long long> done0(n);
+    std::vector<char> fe0(n), tx0(n);
     for (int r = 0; r < n; ++r) {
         hakai_ctx* c = ctxs[r];
         if (!c) return fail(HAKAI_ERR_ARG, "step_group: null context %d", r);
@@ -1226,6 +1266,8 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
             return fail(HAKAI_ERR_ARG, "step_group: context %d is not rank %d of an in-process group of %d", r, r, n);
         cur0[r] = c->cur;
         done0[r] = c->steps_done;
+        fe0[r] = c->fe_ok;
+        tx0[r] = c->triax_ok;
         hkc::graph_invalidate(c);
     }
     HIPCHK(hipSetDevice(ctxs[0]->device));
@@ -1244,7 +1286,7 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
     }
     int first = 0;
     for (int r = 0; r < n; ++r) {
-        const int rc = finish_call(ctxs[r], t_first, n_steps, cur0[r], done0[r]);
+        const int rc = finish_call(ctxs[r], t_first, n_steps, cur0[r], done0[r], fe0[r], tx0[r]);
         if (rc && !first) first = rc;
     }
     return first;

@@ -81,6 +81,11 @@ struct hakai_ctx {
     // state extras
     double* d_qbuf = nullptr;
     bool q_from_buf = false;
+    // fe / triax hold the current state's element forces / triaxiality. With owner-computed assembly
+    // the element kernel stores fe (and, in both modes, triax) only on a call's last step, so after
+    // a call whose later steps a contact overflow turned into no-ops they are stale: the Qe and
+    // triaxiality downloads then fail (HAKAI_ERR_STATE) until a step has run (Q stays available).
+    bool fe_ok = true, triax_ok = true;
     std::vector<double> h_velo0;  // velo as uploaded / set by IC, valid until the first step
     long long steps_done = 0;
     double last_dt = 0.0;

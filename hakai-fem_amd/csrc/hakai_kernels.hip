@@ -1260,6 +1260,60 @@ hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe,
     return hipGetLastError();
 }
 
+// Q of every node from the owner-computed sums (for downloads, and for handing the nodal update
+// a Q when owner assembly stops being used): own_q[n] + its exported rows, in element order --
+// the same additions as k_nodal MODE 3, so the same bits.
+__global__ void k_own_q(const double* __restrict__ own_q, const int* __restrict__ rp, const int* __restrict__ ridx,
+                        const double* __restrict__ rows, double* Q, long long nN) {
+#pragma clang fp contract(off)
+    const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= nN) return;
+    double q0 = own_q[3 * n + 0], q1 = own_q[3 * n + 1], q2 = own_q[3 * n + 2];
+    for (int j = rp[n]; j < rp[n + 1]; ++j) {
+        const long long r = ridx[j];
+        q0 += rows[3 * r + 0];
+        q1 += rows[3 * r + 1];
+        q2 += rows[3 * r + 2];
+    }
+    Q[3 * n + 0] = q0;
+    Q[3 * n + 1] = q1;
+    Q[3 * n + 2] = q2;
+}
+
+hipError_t launch_own_q(const double* own_q, const int* rp, const int* ridx, const double* rows, double* Q,
+                        long long nN, hipStream_t s) {
+    if (nN <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_own_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, own_q, rp, ridx, rows, Q, nN);
+    return hipGetLastError();
+}
+
+// Triaxiality of every Gauss point from the SoA stress, the element kernel's invariant form
+// (elem_step_exact's expression, so the same bits as the reference-order kernel) -- for downloads
+// after a call whose last step did not run (contact overflow).
+__global__ void k_triax_soa(const double* __restrict__ st, double* __restrict__ tx, const int* __restrict__ flag,
+                            long long nGP, long long ld) {
+#pragma clang fp contract(off)
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nGP) return;
+    double f[6];
+    for (int c = 0; c < 6; ++c) f[c] = st[c * ld + g];
+    const double x = f[0] + f[1] + f[2];
+    constexpr double y = 1.0 / 3.0;
+    const double q = x * y;
+    const double mean = __builtin_fma(__builtin_fma(-q, 3.0, x), y, q);
+    const double a01 = f[0] - f[1], a12 = f[1] - f[2], a20 = f[2] - f[0];
+    const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) + 3.0 * (f[3] * f[3] + f[4] * f[4] + f[5] * f[5]));
+    tx[g] = (flag[g >> 3] != 1 || oeq < 1e-10) ? 0.0 : mean / oeq;
+}
+
+hipError_t launch_triax_soa(const double* stress, double* triax, const int* flag, long long nGP, long long ld,
+                            hipStream_t s) {
+    if (nGP <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_triax_soa, dim3((unsigned)((nGP + 255) / 256)), dim3(256), 0, s, stress, triax, flag, nGP,
+                       ld);
+    return hipGetLastError();
+}
+
 __global__ void k_aos_to_soa6(const double* __restrict__ aos, double* __restrict__ soa, long long n, long long ld) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 6 * n) return;

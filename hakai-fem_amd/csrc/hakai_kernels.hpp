@@ -106,6 +106,12 @@ hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s);
 // Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
 hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,
                            hipStream_t s);
+// Q from the owner-computed sums: own_q[n] + the node's rows in element order (= k_nodal MODE 3).
+hipError_t launch_own_q(const double* own_q, const int* rp, const int* ridx, const double* rows, double* Q,
+                        long long nN, hipStream_t s);
+// Triaxiality of the SoA stress in the element kernel's invariant form (0 for inactive elements).
+hipError_t launch_triax_soa(const double* stress, double* triax, const int* flag, long long nGP, long long ld,
+                            hipStream_t s);
 // AoS [gp][6] <-> SoA [6][ld] conversions used at upload/download.
 hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, long long ld, hipStream_t s);
 hipError_t launch_soa_to_aos6(const double* soa, double* aos, long long nGP, long long ld, hipStream_t s);

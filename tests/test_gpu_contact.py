@@ -13,7 +13,7 @@ import pytest
 from hakai import mesh
 from hakai.solver import Solver, State
 import oracle as O
-from util import rel_err
+from util import bitwise_equal, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -125,42 +125,63 @@ def test_incremental_surface_lists_match_full_rebuild_and_oracle():
     assert p0["live_nodes_j"] == sum(p["n_nodes_j"] for p in cp)
 
 
-@pytest.mark.parametrize("graph", [0, 16])
-def test_event_cap_overflow_is_reported(graph):
+@pytest.mark.parametrize("graph,own", [(0, 0), (16, 0), (0, 1), (16, 1)])
+def test_event_cap_overflow_is_reported(graph, own):
     """A contact step with more events than the buffer holds fails loudly (no silent truncation) AT
     that step: a device-side poison flag makes the nodal, BC and element kernels of that and every
-    later step of the call no-ops, so the state afterwards is the last good step's, bit for bit.
-    Raising the cap through hakai_set_tuning and stepping on from the failed step gives the same
-    run as a sufficient buffer from the start."""
+    later step of the call no-ops, so the state afterwards is the last good step's, bit for bit
+    (Q included: with owner-computed assembly it comes from the node sums, as the element kernel
+    stored the per-element forces and the triaxiality only on the call's skipped last step, and
+    those two downloads fail loudly until a step has run). Raising the cap through
+    hakai_set_tuning and stepping on from the failed step gives the same run as a sufficient buffer
+    from the start -- also when owner assembly is switched off for the rest of the run (the next
+    nodal update then takes the owner sums as its Q)."""
     import re
     from hakai._abi import HakaiError
     # > 64 events per step once the 9x9-node impactor face is in contact: the smallest buffer (one
     # event in each of the 64 shards) must overflow
     m = mesh.two_body_model(plate=(12, 12, 1), impactor=(8, 8, 1), v=-1e5, perturb=0.03, seed=4, n_steps=60)
-    with Solver(m) as sv:
-        sv.set_tuning("graph", graph)
-        sv.set_tuning("contact_event_cap", 1 << 12)
+    tune = {"graph": graph, "own_assembly": own, "elem_pipe_min": 0, "elem_pipe_blocks": 3}
+
+    def solver(cap):
+        sv = Solver(m)
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("contact_event_cap", cap)
+        return sv
+
+    keys = ("disp", "disp_pre", "velo", "integ_stress", "integ_eq_plastic_strain", "element_flag", "Q")
+    with solver(1 << 12) as sv:
         sv.step(1, m.n_steps)
         full = sv.download()
-    with Solver(m) as sv:
-        sv.set_tuning("graph", graph)
-        sv.set_tuning("contact_event_cap", 1)
-        with pytest.raises(HakaiError) as ei:
-            sv.step(1, m.n_steps)
-        p = int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
-        assert 1 < p < m.n_steps
-        after = sv.download()
-        sv.set_tuning("contact_event_cap", 1 << 12)
-        sv.step(p, m.n_steps - p + 1)
-        cont = sv.download()
-    with Solver(m) as sv:
-        sv.set_tuning("graph", graph)
-        sv.set_tuning("contact_event_cap", 1 << 12)
+        assert (sv.stat("own_steps") > 0) == bool(own)
+    conts = []
+    for switch_off in (False, True):
+        with solver(1) as sv:
+            with pytest.raises(HakaiError) as ei:
+                sv.step(1, m.n_steps)
+            p = int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
+            assert 1 < p < m.n_steps
+            after = sv.download(**{k: True for k in keys})
+            if own:
+                with pytest.raises(HakaiError):
+                    sv.download(Qe=True)
+            with pytest.raises(HakaiError):
+                sv.download(integ_triax_stress=True)
+            sv.set_tuning("contact_event_cap", 1 << 12)
+            if switch_off:
+                sv.set_tuning("own_assembly", 0)
+            sv.step(p, m.n_steps - p + 1)
+            conts.append(sv.download())
+    with solver(1 << 12) as sv:
         sv.step(1, p - 1)
         good = sv.download()
-    for k in ("disp", "disp_pre", "velo", "integ_stress", "integ_eq_plastic_strain", "element_flag"):
-        assert np.array_equal(getattr(after, k), getattr(good, k)), k
-        assert np.array_equal(getattr(cont, k), getattr(full, k)), k
+    for k in keys:
+        assert bitwise_equal(getattr(after, k), getattr(good, k)), k
+        for cont in conts:
+            assert bitwise_equal(getattr(cont, k), getattr(full, k)), k
+    for cont in conts:
+        assert bitwise_equal(cont.integ_triax_stress, full.integ_triax_stress)
     o = O.Oracle(m)
     o.run(1, m.n_steps)
     assert rel_err(full.disp, o.s["disp"]) < 1e-9
