@@ -7,9 +7,14 @@
     python bench.py --local-ranks R          # rehearsal of the N-rank path on one GPU
 
 A "step" is one full pass of the reference time-loop body (v2/HAKAI_j.jl:497-764): nodal central
-difference with element-order force assembly, prescribed BCs, fused hex8 B-bar + J2 return +
-internal force + triaxiality + ductile-deletion check for every active element (and, for N > 1, the
+difference with element-order force assembly, prescribed BCs, hex8 B-bar + J2 return + internal
+force + triaxiality + ductile-deletion check for every active element (and, for N > 1, the
 interface exchange). Inputs are resident in HBM before timing starts.
+
+Element arithmetic (`config.element_mode`): "exact" (default) is the reference-order kernel, whose
+trajectories equal the CPU restatement of the reference bit for bit (tests/test_gpu_exact.py); the
+line also carries `config.fused_mode`, the same workload timed in the same process with the fused
+single-pass kernel (rounding-level differences, the round-2 headline).
 
 Workloads (BASELINE.json):
   N = 1 (default)  C3, the 2 M-hex elastoplastic tensile bar 20x20x5000 (Tensile5e steel_Ductile,
@@ -17,11 +22,12 @@ Workloads (BASELINE.json):
   N > 1 (weak)     each rank owns one C3 bar: the 20x20x(5000N) bar in N z-slabs of 20x20x5000
                    (2 M hex each, the same velocity gradient, preload and plastic share as N = 1),
                    so value_N / (N x value_1) compares the same per-GPU work; N = 8 is 16 M hex.
-                   --weak-shape c5: 2 M-hex z-slabs of the C5 bar 100x100x(200N) instead (uniform
-                   v_z = -1e5 mm/s into the clamped face). The line carries `single_gpu_same_slab`:
-                   the same run's rate of one rank's slab on its GPU alone (no exchange).
-  --strong         the whole C5 bar 100x100x1600 (16 M hex) split over N (N = 1 holds all 16 M),
-                   so value_N / value_1 is the strong-scaling speed-up ("scaling": "strong").
+                   The line also carries `config.c5_strong`: BASELINE config 5, the C5 bar
+                   100x100x1600 (16 M hex) split over the same N ranks, timed in the same run, with
+                   its ratio to the committed one-GPU C5 line (profiles/r03_bench_strong_n1_c5.json).
+                   --weak-shape c5: 2 M-hex z-slabs of the C5 bar 100x100x(200N) instead.
+  --strong         the whole C5 bar 100x100x1600 (16 M hex) split over N as the headline (N = 1
+                   holds all 16 M), so value_N / value_1 is the strong-scaling speed-up.
 Before warm-up an untimed preload advances the bar into its plastic regime (the share of yielding
 Gauss points is reported).
 
@@ -49,6 +55,7 @@ B_E_ELASTIC = 1576
 B_N = 224                      # compulsory bytes per node per step (whole step)
 B_N_ELEMENT_SIDE = 72          # coord, u, u_pre read by the element kernel, once per node
 C5_LAYERS = 1600               # C5: 100x100x1600
+C5_N1_LINE = os.path.join(ROOT, "profiles", "r03_bench_strong_n1_c5.json")
 
 
 def parse():
@@ -58,13 +65,22 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--preload", type=int, default=-1, help="untimed steps before warm-up (-1: config default)")
     ap.add_argument("--layers", type=int, default=0, help="override z layers (tests / quick runs)")
+    ap.add_argument("--element-mode", choices=("exact", "fused"), default="exact",
+                    help="element arithmetic of the headline: reference order (bit-exact) or fused")
+    ap.add_argument("--compare-fused", type=int, default=1,
+                    help="also time the fused element kernel on the same workload (config.fused_mode)")
     ap.add_argument("--strong", action="store_true", help="strong scaling: C5 16 M hex split over the ranks")
     ap.add_argument("--weak-shape", choices=("c3", "c5"), default="c3",
                     help="N > 1 weak scaling: a C3 bar per rank (default) or 2 M-hex slabs of the C5 bar")
+    ap.add_argument("--c5-strong", type=int, default=1,
+                    help="N > 1 weak: also time BASELINE config 5 (C5 16 M split over the ranks)")
+    ap.add_argument("--c5-steps", type=int, default=50)
     ap.add_argument("--local-ranks", type=int, default=0,
                     help="rehearsal: the N-rank path as an in-process group of R contexts on one GPU")
     ap.add_argument("--same-slab-ref", type=int, default=1,
                     help="N > 1 weak: also time one rank's slab alone (single_gpu_same_slab)")
+    ap.add_argument("--breakdown", type=int, default=1,
+                    help="per-kernel breakdown pass after the timed region (profiling scripts: 0)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -73,22 +89,28 @@ def parse():
     return ap.parse_args()
 
 
+def c5_strong_model(rank, world, layers_override=0):
+    from hakai import mesh
+    from hakai.dist import slab_partition
+    layers = layers_override or C5_LAYERS
+    glob = mesh.config_c5(layers=layers)
+    cfg = {"workload": "C5 100x100x%d elastoplastic impact bar (%d hex), split into %d z-slab(s) (strong scaling)"
+           % (layers, glob.nElement, world), "elements": glob.nElement, "nodes": glob.nNode,
+           "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"
+           if world > 1 else "single GPU"}
+    if world == 1:
+        diag, _ = glob.lumped_mass()
+        return glob, diag, None, cfg, 20
+    local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
+    return local, diag, iface, cfg, 20
+
+
 def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=False, weak_shape="c3"):
     """Returns (local Model, local diag_M, interface arrays or None, config dict, preload)."""
     from hakai import mesh
     from hakai.dist import slab_partition
     if strong:
-        layers = layers_override or C5_LAYERS
-        glob = mesh.config_c5(layers=layers)
-        cfg = {"workload": "C5 100x100x%d elastoplastic impact bar (%d hex), split into %d z-slab(s) (strong scaling)"
-               % (layers, glob.nElement, world), "elements": glob.nElement, "nodes": glob.nNode,
-               "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"
-               if world > 1 else "single GPU"}
-        if world == 1:
-            diag, _ = glob.lumped_mass()
-            return glob, diag, None, cfg, 20
-        local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
-        return local, diag, iface, cfg, 20
+        return c5_strong_model(rank, world, layers_override)
     if world == 1 and not dist_path:
         nz = layers_override or 5000
         m = mesh.config_c3(v_end=5e5) if nz == 5000 else mesh.bar_model(
@@ -139,12 +161,13 @@ def cpu_baseline(seconds, threads):
                       f"{n} steps in {dt:.1f} s, {threads} OpenMP threads"}
 
 
-def same_slab_rate(model, diag, t, preload, warmup, steps):
+def same_slab_rate(model, diag, exact, preload, warmup, steps):
     """One rank's slab alone on its GPU (no communicator, no interface): wall time of `steps`."""
     import torch
     from hakai.solver import Solver
     sv = Solver(model, device=torch.cuda.current_device(), diag_M=diag)
     sv.set_tuning("graph", 0)
+    sv.set_tuning("elem_exact", int(exact))
     sv.step(1, preload + warmup)
     sv.sync()
     t0 = time.perf_counter()
@@ -154,6 +177,102 @@ def same_slab_rate(model, diag, t, preload, warmup, steps):
     n_act = int(sv.download(element_flag=True).element_flag.sum())
     sv.close()
     return el, n_act
+
+
+class Group:
+    """This process's subdomain solvers (one per rank, or R in-process ranks on one device)."""
+
+    def __init__(self, built, ids, R, rank, world, device, exact, tag):
+        import torch
+        import torch.distributed as dist
+        from hakai.solver import Solver, comm_unique_id
+        self.R = R
+        self.svs = []
+        for r, (model, diag, iface, _, _) in zip(ids, built):
+            sv = Solver(model, device=device, diag_M=diag)
+            # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region
+            # is stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
+            sv.set_tuning("graph", 0)
+            sv.set_tuning("elem_exact", int(exact))
+            if iface is not None:
+                sv.set_element_offset(model.global_element_offset)
+                if R:
+                    sv.comm_init_local(r, R, 7117 + tag)
+                else:
+                    uid = comm_unique_id() if rank == 0 else bytes(128)
+                    tu = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
+                    dist.broadcast(tu, 0)
+                    sv.comm_init(rank, world, bytes(tu.cpu().tolist()))
+                sv.set_interface(*iface)
+            self.svs.append(sv)
+
+    def run(self, t_first, n):
+        from hakai.solver import step_group
+        if self.R:
+            step_group(self.svs, t_first, n)
+        else:
+            self.svs[0].step(t_first, n)
+
+    def sync(self):
+        for sv in self.svs:
+            sv.sync()
+
+    def set(self, key, value):
+        for sv in self.svs:
+            sv.set_tuning(key, value)
+
+    def close(self):
+        for sv in self.svs:
+            sv.close()
+        self.svs = []
+
+
+def timed(g, t, steps, multi):
+    """Barrier + sync, `steps` steps, sync + barrier: (wall seconds, element-kernel (ms, launches) per solver)."""
+    import torch
+    import torch.distributed as dist
+    from hakai._abi import K_ELEMENT, K_EXCHANGE
+    for sv in g.svs:
+        sv.profile(True, kernels=[K_ELEMENT, K_EXCHANGE])
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.run(t, steps)
+    g.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if multi:
+        dist.barrier()
+    el = [sv.profile_read(K_ELEMENT) for sv in g.svs]
+    ex = [sv.profile_read(K_EXCHANGE) for sv in g.svs]
+    for sv in g.svs:
+        sv.profile(False)
+    return elapsed, el, ex
+
+
+def max_over_ranks(x, multi):
+    if not multi:
+        return x
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return float(v.item())
+
+
+def sum_over_ranks(x, multi):
+    if not multi:
+        return x
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    return float(v.item())
+
+
+def active_elements(g):
+    return sum(int(sv.download(element_flag=True).element_flag.sum()) for sv in g.svs)
 
 
 def main():
@@ -168,7 +287,6 @@ def main():
     import torch.distributed as dist
     from hakai._abi import K_ELEMENT, K_EXCHANGE, K_NODAL, K_BC
     from hakai.dist import rank_device
-    from hakai.solver import Solver, comm_unique_id, step_group
     R = a.local_ranks if a.local_ranks > 1 else 0
     if R and world > 1:
         raise SystemExit("--local-ranks is a one-process rehearsal")
@@ -184,102 +302,81 @@ def main():
         device = rank_device(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
         torch.cuda.set_device(device)
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-    # this process's subdomains: one per rank, or R in-process ranks on one device
+    exact = a.element_mode == "exact"
     ids = list(range(R)) if R else [rank]
     built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong, a.weak_shape) for r in ids]
     cfg = built[0][3]
     preload = built[0][4] if a.preload < 0 else a.preload
-    svs = []
-    for r, (model, diag, iface, _, _) in zip(ids, built):
-        sv = Solver(model, device=device, diag_M=diag)
-        # stream mode throughout: graphs gain nothing at 2 M elements per step, the timed region is
-        # stream mode anyway (it records events), and rocprofv3 cannot trace graph launches
-        sv.set_tuning("graph", 0)
-        if iface is not None:
-            sv.set_element_offset(model.global_element_offset)
-            if R:
-                sv.comm_init_local(r, R, 7117)
-            else:
-                uid = comm_unique_id() if rank == 0 else bytes(128)
-                tu = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
-                dist.broadcast(tu, 0)
-                sv.comm_init(rank, world, bytes(tu.cpu().tolist()))
-            sv.set_interface(*iface)
-        svs.append(sv)
-
-    def run(t_first, n):
-        if R:
-            step_group(svs, t_first, n)
-        else:
-            svs[0].step(t_first, n)
+    g = Group(built, ids, R, rank, world, device, exact, 0)
 
     t = 1
     if preload:
-        run(t, preload)
+        g.run(t, preload)
         t += preload
     if a.warmup:
-        run(t, a.warmup)
+        g.run(t, a.warmup)
         t += a.warmup
-    for sv in svs:
-        sv.sync()
+    g.sync()
 
-    def barrier():
-        if multi:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    # timed region: HIP events around the element kernel only (the roofline figure), so the step
-    # loop is not slowed by events around every launch
-    for sv in svs:
-        sv.profile(True, kernels=[K_ELEMENT])
-    barrier()
-    t0 = time.perf_counter()
-    run(t, a.steps)
-    for sv in svs:
-        sv.sync()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if multi:
-        dist.barrier()
-    elapsed = t1 - t0
+    # timed region: HIP events around the element kernel (the roofline figure) and the exchange
+    elapsed, el_timed, ex_timed = timed(g, t, a.steps, multi)
     t += a.steps
-    el_timed = [sv.profile_read(K_ELEMENT) for sv in svs]
-    # per-kernel breakdown from a short extra pass after the timed region (reported, not timed)
-    for sv in svs:
-        sv.profile(True)
-    nb = min(20, max(a.steps, 1))
-    run(t, nb)
-    t += nb
-    k_tot = {}
-    for sv in svs:
-        sv.sync()
-        for k, name in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"), (K_EXCHANGE, "exchange")):
-            ms, n = sv.profile_read(k)
-            if n:
-                p = k_tot.setdefault(name, [0.0, 0])
-                p[0] += ms
-                p[1] += n
-        sv.profile(False)
-    n_active, plastic = 0, []
-    for sv in svs:
-        st = sv.download(integ_eq_plastic_strain=True, element_flag=True)
+    n_active = active_elements(g)
+    own_steps = sum(sv.stat("own_steps") for sv in g.svs)
+    own_rows = sum(max(sv.stat("own_rows"), 0) for sv in g.svs)
+    own_entries = sum(max(sv.stat("own_entries"), 0) for sv in g.svs)
+    plastic = []
+    for sv in g.svs:
+        st = sv.download(integ_eq_plastic_strain=True)
         plastic.append(float(np.mean(st.integ_eq_plastic_strain > 0)))
-        n_active += int(st.element_flag.sum())
     plastic_frac = float(np.mean(plastic))
-    own_steps = sum(sv.stat("own_steps") for sv in svs)
+
+    # the same workload with the other element arithmetic (same process, same state, re-warmed)
+    other = None
+    if a.compare_fused:
+        g.set("elem_exact", 0 if exact else 1)
+        g.run(t, 10)
+        t += 10
+        g.sync()
+        e2, el2, _ = timed(g, t, a.steps, multi)
+        t += a.steps
+        n2 = active_elements(g)
+        g.set("elem_exact", int(exact))
+        g.run(t, 2)  # back to the headline mode for anything after this
+        t += 2
+        g.sync()
+        e2 = max_over_ranks(e2, multi)
+        n2 = sum_over_ranks(n2, multi)
+        other = {"element_mode": "fused" if exact else "exact",
+                 "value": round(n2 * a.steps / e2 / 1e6, 3), "unit": "M element-updates/s",
+                 "ms_per_step": round(e2 / a.steps * 1e3, 4),
+                 "element_avg_ms": round(sum(x[0] for x in el2) / max(el2[0][1], 1) / len(g.svs), 4),
+                 "what": ("fused single-pass element kernel (rounding-level differences from the reference order; "
+                          "tests/test_gpu_decks.py bounds, tools/oracle_conditioning.py)" if exact else
+                          "reference-order element kernel (bit-exact)")}
+
+    # per-kernel breakdown from a short extra pass after the timed regions (reported, not timed)
+    k_tot = {}
+    if a.breakdown:
+        for sv in g.svs:
+            sv.profile(True)
+        nb = min(20, max(a.steps, 1))
+        g.run(t, nb)
+        t += nb
+        g.sync()
+        for sv in g.svs:
+            for k, name in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"), (K_EXCHANGE, "exchange")):
+                ms, n = sv.profile_read(k)
+                if n:
+                    p = k_tot.setdefault(name, [0.0, 0])
+                    p[0] += ms
+                    p[1] += n
+            sv.profile(False)
     n_elem_local = sum(b[0].nElement for b in built)
     n_node_local = sum(b[0].nNode for b in built)
-    if multi:
-        v = torch.tensor([elapsed, float(n_active), plastic_frac], dtype=torch.float64, device="cuda")
-        mx = v.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = v.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0].item())
-        n_active_total = sm[1].item()
-        plastic_frac = sm[2].item() / world
-    else:
-        n_active_total = n_active
+    elapsed = max_over_ranks(elapsed, multi)
+    n_active_total = sum_over_ranks(n_active, multi)
+    plastic_frac = sum_over_ranks(plastic_frac, multi) / (world if multi else 1)
     n_deleted = cfg["elements"] - n_active_total
     # element updates: active elements x steps (metric definition)
     updates = n_active_total * a.steps
@@ -288,8 +385,12 @@ def main():
     # roofline of the dominant kernel, from HIP events on the library's stream (this process)
     el_ms = sum(x[0] for x in el_timed)
     el_n = max(el_timed[0][1], 1)
-    el_avg_s = el_ms / el_n / 1e3 / len(svs)   # per subdomain launch
-    alg_bytes = (B_E_PLASTIC * n_active + B_N_ELEMENT_SIDE * n_node_local) / len(svs)
+    el_avg_s = el_ms / el_n / 1e3 / len(g.svs)   # per subdomain launch
+    alg_bytes = (B_E_PLASTIC * n_active + B_N_ELEMENT_SIDE * n_node_local) / len(g.svs)
+    # with owner-computed assembly the element kernel also reads its entry lists and writes Q
+    # (own_q) and the exported rows: not in §8(d)'s byte model, reported beside it
+    alg_bytes_own = alg_bytes + ((24 * n_node_local + 24 * own_rows + 16 * own_entries + 4 * n_elem_local // 32)
+                                 / len(g.svs) if own_steps else 0)
     achieved = alg_bytes / el_avg_s / 1e9
     whole_bytes = B_E_PLASTIC * n_active + B_N * n_node_local
     traffic = None
@@ -298,25 +399,54 @@ def main():
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            # measured on the one-GPU C3 workload (tools/gpu_prof.sh): attached to that workload only
-            if pm.get("elements") == n_elem_local and world == 1 and cfg["workload"].startswith("C3"):
+            # measured on the one-GPU C3 workload (tools/gpu_prof.sh): attached to that workload and mode only
+            if (pm.get("elements") == n_elem_local and world == 1 and cfg["workload"].startswith("C3")
+                    and pm.get("element_mode", "fused") == a.element_mode):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in k_tot.items()}
     extra = {}
     if nparts > 1:
-        extra["exchange_ms_per_step"] = k_ms.get("exchange")
+        ex_ms = sum(x[0] for x in ex_timed) / max(ex_timed[0][1], 1) / len(g.svs)
+        extra["exchange_ms_per_step"] = round(max_over_ranks(ex_ms, multi), 4)
+    g.close()
+    if nparts > 1 and not a.strong and a.c5_strong:
+        # BASELINE config 5: the C5 16 M bar split over the same ranks, timed in the same run
+        b5 = [c5_strong_model(r, nparts, 0) for r in ids]
+        g5 = Group(b5, ids, R, rank, world, device, exact, 1)
+        pre5 = b5[0][4]
+        t5 = 1
+        g5.run(t5, pre5 + 10)
+        t5 += pre5 + 10
+        g5.sync()
+        e5, el5, ex5 = timed(g5, t5, a.c5_steps, multi)
+        n5 = sum_over_ranks(active_elements(g5), multi)
+        e5 = max_over_ranks(e5, multi)
+        ex5_ms = max_over_ranks(sum(x[0] for x in ex5) / max(ex5[0][1], 1) / len(g5.svs), multi)
+        el5_ms = sum(x[0] for x in el5) / max(el5[0][1], 1) / len(g5.svs)
+        g5.close()
+        v5 = n5 * a.c5_steps / e5 / 1e6
+        c5 = {"workload": b5[0][3]["workload"], "elements": b5[0][3]["elements"], "steps": a.c5_steps,
+              "value": round(v5, 3), "unit": "M element-updates/s", "ms_per_step": round(e5 / a.c5_steps * 1e3, 4),
+              "exchange_ms_per_step": round(ex5_ms, 4), "element_avg_ms_per_rank": round(el5_ms, 4),
+              "n1_reference": None, "speedup_vs_n1": None}
+        if os.path.exists(C5_N1_LINE):
+            try:
+                with open(C5_N1_LINE) as f:
+                    n1 = json.loads([ln for ln in f if ln.strip().startswith("{")][-1])
+                if n1.get("config", {}).get("element_mode") == a.element_mode:
+                    c5["n1_reference"] = {"value": n1["value"], "ms_per_step": n1["ms_per_step"],
+                                          "source": os.path.relpath(C5_N1_LINE, ROOT)}
+                    c5["speedup_vs_n1"] = round(v5 / n1["value"], 3)
+            except Exception:
+                pass
+        extra["c5_strong"] = c5
     if world > 1 and not a.strong and a.same_slab_ref:
         # the same slab alone on each GPU, concurrently; the slowest rank, like the timed run
-        for sv in svs:
-            sv.close()
-        svs = []
         model, diag = built[0][0], built[0][1]
-        e_ref, n_ref = same_slab_rate(model, diag, 1, preload, a.warmup, a.steps)
-        v = torch.tensor([e_ref], dtype=torch.float64, device="cuda")
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        e_ref = float(v.item())
+        e_ref, n_ref = same_slab_rate(model, diag, exact, preload, a.warmup, a.steps)
+        e_ref = max_over_ranks(e_ref, multi)
         extra["single_gpu_same_slab"] = {
             "value": round(n_ref * a.steps / e_ref / 1e6, 3), "unit": "M element-updates/s",
             "ms_per_step": round(e_ref / a.steps * 1e3, 4),
@@ -335,11 +465,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (structured hex bar, 1% node perturbation, seed 0; no reference checkpoint needed)",
-        "config": dict(cfg, preload_steps=preload, plastic_gp_frac=round(plastic_frac, 4),
+        "config": dict(cfg, element_mode=a.element_mode,
+                       element_mode_what=("reference-order element arithmetic: trajectories bit-identical to the "
+                                          "CPU restatement of v2/HAKAI_j.jl (tests/test_gpu_exact.py)" if exact else
+                                          "fused single-pass element arithmetic (rounding-level differences)"),
+                       preload_steps=preload, plastic_gp_frac=round(plastic_frac, 4),
                        deleted_elements=int(n_deleted),
                        whole_step_roofline_frac=round(whole_bytes * a.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)
                        if nparts == 1 else None,
-                       kernel_ms_per_step=k_ms, **extra,
+                       kernel_ms_per_step=k_ms, fused_mode=other, **extra,
                        assembly=("owner-computed node sums in LDS (own_assembly), element order" if own_steps
                                  else "fe round trip (element forces gathered by the nodal kernel)"),
                        parallelism=(f"dp{world}" if world > 1 else
@@ -347,15 +481,14 @@ def main():
                                      if R else "single"))),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": ("static: rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this kernel and "
+                     "traffic_source": ("static: rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this kernel, mode and "
                                         "workload, calibrated (profiles/element_pmc.json); not measured in this run")
                      if traffic else None,
-                     "kernel": "k_element", "alg_bytes_per_launch": int(alg_bytes),
+                     "kernel": "k_element_pipe", "alg_bytes_per_launch": int(alg_bytes),
+                     "alg_bytes_per_launch_with_assembly_outputs": int(alg_bytes_own),
                      "avg_launch_ms": round(el_avg_s * 1e3, 4), "measured_peak_GBs": HBM_MEASURED_GBS},
         "cpu_baseline": None,
     }
-    for sv in svs:
-        sv.close()
     if rank == 0 and world == 1 and not R and not a.strong and a.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_threads)

@@ -249,6 +249,10 @@ static hk::ElemArgs elem_args(hakai_ctx* c) {
     ea.mats = c->d_mats;
     ea.stress = c->d_stress;
     ea.strain = c->d_strain;
+    for (int q = 0; q < 6; ++q) {
+        ea.sc[q] = c->d_stress + q * c->ld;
+        ea.ec[q] = c->d_strain + q * c->ld;
+    }
     ea.eqps = c->d_eqps;
     ea.yield = c->d_yield;
     ea.triax = c->d_triax;
@@ -396,6 +400,12 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
         return fail(HAKAI_ERR_ARG, "upload_model: bad arguments");
     if (26 * (nElement + 32) + 8 >= (int64_t)INT32_MAX || nNode >= (int64_t)INT32_MAX)
         return fail(HAKAI_ERR_ARG, "upload_model: mesh too large for int32 indexing on one rank");
+    // the element kernel addresses its arrays with a 32-bit byte offset per lane (the element
+    // forces, 192 B per element, are the largest): at most ~22 M hex per context; larger meshes
+    // are split over ranks (hakai_comm_init / hakai_comm_init_local, also on one GPU)
+    if (192 * (nElement + 32) >= (int64_t)1 << 32)
+        return fail(HAKAI_ERR_ARG, "upload_model: %lld elements exceed one context's 32-bit element-kernel offsets "
+                    "(max %lld); split the mesh over ranks", (long long)nElement, (long long)(((int64_t)1 << 32) / 192 - 32));
     HIPCHK(hipSetDevice(c->device));
     (void)hipStreamSynchronize(c->stream);
     hkc::free_model(c);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hakai_kernels.hpp"
 
@@ -57,11 +58,23 @@ struct ElemIn {
 // stores of the previous batch (a conditional store makes its vmcnt accounting fall back to 0).
 // EXACT: lane k stores the force of local node k (elem_step_exact); otherwise that of node
 // ref_of_sign(k) (elem_step's relative slots).
+// Addressing: a wave-uniform base (SGPRs) plus a 32-bit per-lane byte offset, so every access is a
+// global_load/store with an SGPR base and one VGPR offset instead of a 64-bit VGPR address per
+// array and component (12 Gauss-point components, 3 node arrays: ~60 VGPRs of addresses in the
+// element kernel otherwise). The host keeps every element-kernel array below 4 GB
+// (hakai_upload_model: nEp <= kMaxElemPerCtx).
+template <class T>
+__device__ __forceinline__ T* at32(T* base, unsigned bytes) {
+    using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return reinterpret_cast<T*>(reinterpret_cast<C*>(base) + bytes);
+}
+
 template <bool EXACT = false>
 __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int k, ElemIn& in) {
-    in.fl = a.flag[e];
-    in.n = a.conn[8 * e + k];
-    in.mt = a.mat[e];
+    const unsigned ue = (unsigned)e;
+    in.fl = *at32(a.flag, 4u * ue);
+    in.n = *at32(a.conn, 32u * ue + 4u * (unsigned)k);
+    in.mt = *at32(a.mat, 4u * ue);
     const int kn = EXACT ? k : ref_of_sign(k);  // the node whose force lane k ends up with
     in.fb = (int)(24 * e + 3 * kn);
 }
@@ -83,28 +96,30 @@ __device__ __forceinline__ void gp_st(double* p, double v) {
 }
 
 // stage B: the lane's node (position = coord + u, d_disp = u - u_pre) and its Gauss-point state
+__device__ __forceinline__ unsigned gp_off(long long e, int k) { return 64u * (unsigned)e + 8u * (unsigned)k; }
+
 template <bool ANY_PLASTIC, int NT = 0>
 __device__ __forceinline__ void load_gp(const ElemArgs& a, long long e, int k, ElemIn& in) {
-    const long long gp = 8 * e + k, ld = a.ld;
+    const unsigned go = gp_off(e, k);
 #pragma unroll
-    for (int c = 0; c < 6; ++c) in.sig[c] = gp_ld<NT>(a.stress + c * ld + gp);
+    for (int c = 0; c < 6; ++c) in.sig[c] = gp_ld<NT>(at32(a.sc[c], go));
 #pragma unroll
-    for (int c = 0; c < 6; ++c) in.eps[c] = gp_ld<NT>(a.strain + c * ld + gp);
+    for (int c = 0; c < 6; ++c) in.eps[c] = gp_ld<NT>(at32(a.ec[c], go));
     in.eqp = 0.0;
     in.ys = 0.0;
     if (ANY_PLASTIC) {
-        in.eqp = gp_ld<NT>(a.eqps + gp);
-        in.ys = gp_ld<NT>(a.yield + gp);
+        in.eqp = gp_ld<NT>(at32(a.eqps, go));
+        in.ys = gp_ld<NT>(at32(a.yield, go));
     }
 }
 
 __device__ __forceinline__ void load_node(const ElemArgs& a, ElemIn& in) {
-    const long long n = in.n;
+    const unsigned no = 24u * (unsigned)in.n;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const double uc = a.u[3 * n + c];
-        in.x[c] = a.coord[3 * n + c] + uc;
-        in.du[c] = uc - a.u_pre[3 * n + c];
+        const double uc = at32(a.u, no)[c];
+        in.x[c] = at32(a.coord, no)[c] + uc;
+        in.du[c] = uc - at32(a.u_pre, no)[c];
     }
 }
 
@@ -116,12 +131,15 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
 
 // Unconditional write-back of one lane (selects, no branches): its node's force fk, its Gauss
 // point's state, the element flag and the deletion log.
-template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false, bool OWN = false>
+// PRESEL: fin/eps/eqp/ys already hold the values to store (the caller selected the previous state
+// for inactive elements early, so in.sig/eps need not stay live until here).
+template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false, bool OWN = false,
+          bool PRESEL = false>
 __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, int k, const ElemIn& in, bool active,
                                                bool kill, const double (&fk)[3], const double (&fin)[6],
                                                const double (&eps)[6], double eqp, double ys, double tri,
                                                double* sfe = nullptr) {
-    const long long gp = 8 * e + k, ld = a.ld;
+    const unsigned go = gp_off(e, k);
     if (OWN) {  // owner-computed assembly: the batch's forces go to LDS [element][local node][3]
         double* fo = sfe + 3 * ((threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k)));
         fo[0] = active ? fk[0] : 0.0;
@@ -129,7 +147,7 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
         fo[2] = active ? fk[2] : 0.0;
     }
     if (!OWN || STORE_TRIAX) {  // fe; with owner assembly only on a call's last step (Q / Qe downloads, mode switches)
-        double* fg = a.fe + in.fb;
+        double* fg = at32(a.fe, 8u * (unsigned)in.fb);
         fg[0] = active ? fk[0] : 0.0;
         fg[1] = active ? fk[1] : 0.0;
         fg[2] = active ? fk[2] : 0.0;
@@ -137,20 +155,20 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-        gp_st<NT>(a.stress + c * ld + gp, kill ? 0.0 : (active ? fin[c] : in.sig[c]));
-        gp_st<NT>(a.strain + c * ld + gp, kill ? 0.0 : (active ? eps[c] : in.eps[c]));
+        gp_st<NT>(at32(a.sc[c], go), kill ? 0.0 : (PRESEL || active ? fin[c] : in.sig[c]));
+        gp_st<NT>(at32(a.ec[c], go), kill ? 0.0 : (PRESEL || active ? eps[c] : in.eps[c]));
     }
     if (ANY_PLASTIC) {
-        gp_st<NT>(a.eqps + gp, active ? eqp : in.eqp);
-        gp_st<NT>(a.yield + gp, active ? ys : in.ys);
+        gp_st<NT>(at32(a.eqps, go), PRESEL || active ? eqp : in.eqp);
+        gp_st<NT>(at32(a.yield, go), PRESEL || active ? ys : in.ys);
     }
-    if (STORE_TRIAX) a.triax[gp] = active ? tri : 0.0;
+    if (STORE_TRIAX) *at32(a.triax, go) = active ? tri : 0.0;
     if (DO_DELETE) {
-        a.flag[e] = kill ? 2 : (in.fl == 2 ? 0 : in.fl);        // 8 lanes, same value
+        *at32(a.flag, 4u * (unsigned)e) = kill ? 2 : (in.fl == 2 ? 0 : in.fl);  // 8 lanes, same value
         // lane 0: the element's deletion step; lanes 1-7 of a killed element: slot nEp+1, "last step
         // with a deletion" (contact rebuilds its live surface lists from it); others: dump slot nEp
-        int* ds = kill ? a.del_step + (k == 0 ? e : a.nEp + 1) : a.del_step + a.nEp;
-        *ds = a.step_i;
+        const unsigned di = kill ? (k == 0 ? (unsigned)e : (unsigned)a.nEp + 1u) : (unsigned)a.nEp;
+        *at32(a.del_step, 4u * di) = a.step_i;
     }
 }
 
@@ -541,7 +559,16 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // Bfinal rows 1-3 carry t(i,c) = -P2/3 + BVbar (:1482-1490), formed where it is used (keeping
     // all 24 live next to P2 would spill at 2 waves per SIMD)
+#ifdef HK_EXACT_KEEP_T
+    double tk[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tk[i][c] = nd8[6 * i + c] - div3(pd[i][c]);
+    auto tq = [&](int i, int c) { return tk[i][c]; };
+#else
     auto tq = [&](int i, int c) { return nd8[6 * i + c] - div3(pd[i][c]); };
+#endif
 
     // ---- de = Bfinal * d_u (:1204): per row, the fma chain over columns j = 3i+c in order.
     // Bfinal column (i,c) by rows: c=0: (Pix+t0, t0, t0, Piy, 0, Piz); c=1: (t1, Piy+t1, t1, Pix,
@@ -577,6 +604,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         de[2] = __builtin_fma(pz + t2, u2, de[2]);
         de[4] = __builtin_fma(py, u2, de[4]);
         de[5] = __builtin_fma(px, u2, de[5]);
+        asm volatile("" ::: "memory");  // one node's LDS operands in flight at a time (VGPRs)
     }
 
     // ---- d_o = Dmat * de (:1205): the 6x6 chain without its structural zeros
@@ -616,7 +644,15 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     }
     double eps[6];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) eps[c] = in.eps[c] + de[c];
+    for (int c = 0; c < 6; ++c) eps[c] = active ? in.eps[c] + de[c] : in.eps[c];
+    // inactive elements keep their state (:1116-1118); selected here so the previous state does not
+    // stay live through the force pass (their forces are masked at the write-back)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) fin[c] = active ? fin[c] : in.sig[c];
+    if (!active) {
+        eqp = in.eqp;
+        ys = in.ys;
+    }
 
     // ---- triaxiality of the final stress (invariant form of :995-1018)
     double tri;
@@ -673,8 +709,8 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         fk[2] = gp_sum8(xb, k, w);
     }
     if (WITH_VOL) a.vol[e] = V;
-    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN>(a, e, k, in, active, kill, fk, fin, eps, eqp, ys,
-                                                                      tri, sfe);
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN, true>(a, e, k, in, active, kill, fk, fin, eps,
+                                                                            eqp, ys, tri, sfe);
 }
 
 // Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.
@@ -865,9 +901,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     int4 ent_cur = {0, 0, 0, 0}, ent_nxt = {0, 0, 0, 0};
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
-    if (EXACT)
+    if (EXACT) {
+#ifndef HK_EXACT_NO_NODE_PREFETCH
         load_node(a, cur);
-    else
+#endif
+    } else
         load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // its first batch)
@@ -880,14 +918,22 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         // (reference-order mode: its longer arithmetic holds more registers, so only the node
         // gathers run a batch ahead; the Gauss-point state is loaded at the start of the step and
         // first used after the Jacobian, B-bar and strain passes)
+#ifdef HK_EXACT_NO_NODE_PREFETCH
         if (EXACT)
             ;
         else
+#else
+        if (EXACT)
+            load_node(a, nxt);
+        else
+#endif
             load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
+#ifdef HK_EXACT_NO_NODE_PREFETCH
             load_node(a, cur);
+#endif
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                                  cur, sfe);

@@ -17,6 +17,8 @@ struct ElemArgs {
     const DevMat* mats;
     double* stress;        // SoA [6][ld]
     double* strain;        // SoA [6][ld]
+    double* sc[6];         // stress + c*ld, strain + c*ld: one uniform base per component, so the
+    double* ec[6];         // element kernel addresses each with an SGPR base + a 32-bit lane offset
     double* eqps;          // [ld]
     double* yield;         // [ld]
     double* triax;         // [ld]

@@ -13,7 +13,8 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhakai_hip.so")
+# HAKAI_LIB: another build of the library (A/B timing of kernel variants, tools/variants.sh)
+LIB_PATH = os.environ.get("HAKAI_LIB") or os.path.join(PKG_ROOT, "lib", "libhakai_hip.so")
 
 HAKAI_OK = 0
 HAKAI_ERR_ARG = -1

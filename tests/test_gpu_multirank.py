@@ -399,7 +399,8 @@ def test_divided_contact_overflow_poisons_every_rank():
     import re
     p = int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
     assert 1 < p < glob.n_steps
-    after = [sv.download() for sv in svs]
+    # (triaxiality and Qe are stored on a call's last step, which the overflow skipped)
+    after = [sv.download(disp=True, velo=True, integ_stress=True) for sv in svs]
     for sv in svs:
         sv.close()
     _, good_svs = group(1 << 12, 9192)

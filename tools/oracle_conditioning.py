@@ -5,8 +5,9 @@ v0.0.2) against ITSELF under a perturbation of one unit in the last place.
 For each deck the committed golden fixture (tests/golden/deck_*.npz) holds the oracle's final
 displacement from the deck as read. This tool runs the oracle again from the same deck with the
 load perturbed by one ulp (np.nextafter towards +inf on every nonzero *Initial Conditions
-velocity, or on every prescribed BC value of a deck without one), or one node coordinate moved by
-one ulp, and reports the relative difference of the final
+velocity, or on every prescribed BC value of a deck without one), one node coordinate moved by one
+ulp, or every coordinate moved by one ulp up or down (rounding-level noise everywhere, what a
+re-associated element kernel injects), and reports the relative difference of the final
 displacement, max|u_a - u_b| / max|u_b|, plus the deletion logs. A drift of the fused GPU element
 kernel (rounding-level element differences) of the same size is then the decks' conditioning, not
 a kernel error (VERDICT r2 "what's missing" 5). Output: one JSON line per (deck, perturbation).
@@ -49,7 +50,8 @@ def main():
         ref_disp = z["disp"]
         ref_del = sorted(tuple(int(v) for v in x) for x in z["deletions"])
         den = float(np.max(np.abs(ref_disp)))
-        for how in ("none", "load", "one_coord"):  # "none": the control, must reproduce the fixture
+        hows = os.environ.get("COND_PERTURB", "none,load,one_coord,all_coords").split(",")
+        for how in hows:  # "none": the control, must reproduce the fixture
             m = model_from_arrays(z, name)
             npert = 0
             if how == "load":  # every nonzero *Initial Conditions velocity, or every BC value
@@ -69,6 +71,13 @@ def main():
                 j = m.nNode // 2
                 m.coordmat[j, 0] = np.nextafter(m.coordmat[j, 0], np.inf)
                 npert = 1
+            elif how == "all_coords":  # every coordinate one ulp up or down (seeded): rounding noise
+                rng = np.random.default_rng(0)
+                c = m.coordmat.copy()
+                up = rng.random(c.shape) < 0.5
+                c = np.where(up, np.nextafter(c, np.inf), np.nextafter(c, -np.inf))
+                m.coordmat = c
+                npert = c.size
             t0 = time.time()
             d, dels = run(m, steps, indexed, threads)
             rel = float(np.max(np.abs(d - ref_disp)) / den)
