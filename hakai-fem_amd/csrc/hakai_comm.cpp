@@ -564,6 +564,15 @@ int hakai_comm_init_local(hakai_ctx* c, int rank, int nranks, int64_t group_key)
             delete m;
             return fail(HAKAI_ERR_ARG, "comm_init_local: group %lld size/rank clash", (long long)group_key);
         }
+        // the group's kernels read the peers' buffers directly (k_gather_local, the phase-B event
+        // gather) and no peer access is enabled: every member must live on one device
+        for (int q = 0; q < nranks; ++q)
+            if (g->ctx[q] && g->ctx[q]->device != c->device) {
+                delete m;
+                return fail(HAKAI_ERR_ARG, "comm_init_local: rank %d is on device %d but rank %d of group %lld is on "
+                            "device %d; an in-process group shares one device (use hakai_comm_init, RCCL, across "
+                            "devices)", rank, c->device, q, (long long)group_key, g->ctx[q]->device);
+            }
         g->ctx[rank] = c;
         g->refs++;
         m->group = g;

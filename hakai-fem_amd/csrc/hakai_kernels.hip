@@ -411,7 +411,7 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
 //     deletion averages (:701-712) summed in GP order; triaxiality in invariant form (the
 //     reference's eigvals agree to rounding; it only enters the deletion test and the output).
 // ---------------------------------------------------------------------------------------------
-constexpr int kXbStride = 66;  // doubles of LDS per element: exchange area [8 nodes][8 lanes] + pad
+constexpr int kXbStride = 74;  // doubles of LDS per element: exchange area [8 nodes][8 lanes] + one scalar row + pad
 
 // x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
 // q = RN(x*y) with y = RN(1/3), then one exact-remainder correction q + (x - 3q)*y. The exact
@@ -456,20 +456,52 @@ __device__ __forceinline__ double gp_sum8(double* w, int k, const double (&v)[8]
     return acc;
 }
 
-// Ordered sum over the 8 lanes of one scalar; every lane gets it.
-__device__ __forceinline__ double gp_all8(double* w, int k, double x) {
-    w[k] = x;
+// The same, plus one scalar per lane summed in GP order into every lane (x_sum), in the same LDS
+// round trip (row 8 of the exchange area).
+__device__ __forceinline__ double gp_sum8x(double* w, int k, const double (&v)[8], double x, double& x_sum) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[8 * i + k] = v[i];
+    w[64 + k] = x;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double r[8];
+    double r[8], q[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) r[kk] = w[8 * k + kk];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) q[kk] = w[64 + kk];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double acc = 0.0 + r[0], xs = 0.0 + q[0];
+#pragma unroll
+    for (int kk = 1; kk < 8; ++kk) {
+        acc += r[kk];
+        xs += q[kk];
+    }
+    x_sum = xs;
+    return acc;
+}
+
+// Ordered sums over the 8 lanes of two scalars (one LDS round trip); every lane gets both.
+__device__ __forceinline__ void gp_all8x2(double* w, int k, double x, double y, double& xs, double& ys) {
+    w[k] = x;
+    w[8 + k] = y;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double r[8], q[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) r[kk] = w[kk];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) q[kk] = w[8 + kk];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double acc = 0.0 + r[0];
+    double a = 0.0 + r[0], b = 0.0 + q[0];
 #pragma unroll
-    for (int kk = 1; kk < 8; ++kk) acc += r[kk];
-    return acc;
+    for (int kk = 1; kk < 8; ++kk) {
+        a += r[kk];
+        b += q[kk];
+    }
+    xs = a;
+    ys = b;
 }
 
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0, bool OWN = false>
@@ -540,7 +572,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     }
 
     // ---- V and BVbar (:1729-1780)
-    const double V = gp_all8(xb, k, fabs(v));
+    double V;  // sum of |det| in GP order, in the first component's round trip
     {
         double bs[3];
 #pragma unroll
@@ -548,7 +580,10 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
             double w[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) w[i] = div3(pd[i][c]) * v;
-            bs[c] = gp_sum8(xb, k, w);
+            if (c == 0)
+                bs[c] = gp_sum8x(xb, k, w, fabs(v), V);
+            else
+                bs[c] = gp_sum8(xb, k, w);
         }
         // lane k holds node k's BVbar column sums; the X slots of the node area are free now
         const double rV = 1.0 / V;
@@ -557,18 +592,14 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // Bfinal rows 1-3 carry t(i,c) = -P2/3 + BVbar (:1482-1490), formed where it is used (keeping
-    // all 24 live next to P2 would spill at 2 waves per SIMD)
-#ifdef HK_EXACT_KEEP_T
+    // Bfinal rows 1-3 carry t(i,c) = -P2/3 + BVbar (:1482-1490), formed once per node and component
+    // (the 32-bit addressing leaves the registers for all 24 next to P2)
     double tk[8][3];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int c = 0; c < 3; ++c) tk[i][c] = nd8[6 * i + c] - div3(pd[i][c]);
     auto tq = [&](int i, int c) { return tk[i][c]; };
-#else
-    auto tq = [&](int i, int c) { return nd8[6 * i + c] - div3(pd[i][c]); };
-#endif
 
     // ---- de = Bfinal * d_u (:1204): per row, the fma chain over columns j = 3i+c in order.
     // Bfinal column (i,c) by rows: c=0: (Pix+t0, t0, t0, Piy, 0, Piz); c=1: (t1, Piy+t1, t1, Pix,
@@ -642,6 +673,16 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
             ys = ys + H * dep;
         }
     }
+    // ---- triaxiality of the final stress (invariant form of :995-1018; the reference's eigenvalue
+    // differences give the same value to rounding -- it enters only the deletion test and the output)
+    double tri;
+    {
+        const double mean = div3(fin[0] + fin[1] + fin[2]);
+        const double a01 = fin[0] - fin[1], a12 = fin[1] - fin[2], a20 = fin[2] - fin[0];
+        const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) +
+                                3.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5]));
+        tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
+    }
     double eps[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) eps[c] = active ? in.eps[c] + de[c] : in.eps[c];
@@ -654,19 +695,12 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         ys = in.ys;
     }
 
-    // ---- triaxiality of the final stress (invariant form of :995-1018)
-    double tri;
-    {
-        const double mean = div3(fin[0] + fin[1] + fin[2]);
-        const double a01 = fin[0] - fin[1], a12 = fin[1] - fin[2], a20 = fin[2] - fin[0];
-        const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) +
-                                3.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5]));
-        tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
-    }
     bool kill = false;
     if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
-        const double v_e = gp_all8(xb, k, eqp) * 0.125;  // /8, exact
-        const double t_e = gp_all8(xb, k, tri) * 0.125;
+        double v_e, t_e;
+        gp_all8x2(xb, k, eqp, tri, v_e, t_e);
+        v_e = v_e * 0.125;  // /8, exact
+        t_e = t_e * 0.125;
         if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
     }
 
@@ -786,20 +820,26 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The thread's entry of super-batch b, prefetched a batch ahead; bit 27 of .y (free in the list's
+// encoding) marks a super-batch with a second round of entries, so the pass itself loads nothing
+// unless that round exists (a load inside the pass waits for every prefetch issued before it).
+constexpr int kOwnRound2 = 1 << 27;
 __device__ __forceinline__ int4 own_load(const ElemArgs& a, long long b) {
     const int o0 = a.own_off[b], o1 = a.own_off[b + 1];
     const int idx = o0 + (int)threadIdx.x;
-    return a.own_list[idx < o1 ? idx : a.own_nop];
+    int4 en = a.own_list[idx < o1 ? idx : a.own_nop];
+    en.y |= (o1 - o0 > kBlock) ? kOwnRound2 : 0;
+    return en;
 }
 
 __device__ __forceinline__ int own_lane(int4 en, int j) {
     const unsigned long long lo = (unsigned long long)(unsigned)en.z | ((unsigned long long)(unsigned)en.w << 32);
-    return j < 7 ? (int)((lo >> (9 * j)) & 511) : (int)(((unsigned)en.y >> 18) & 511);
+    return j < 7 ? (int)((lo >> (9 * j)) & 511) : (int)(((unsigned)en.y >> 18) & 511);  // bits 18-26
 }
 
 __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const double* s_fe, double* s_part) {
 #pragma clang fp contract(off)
-    const int slot = en.y & 1023, flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;
+    const int slot = en.y & 1023, flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;  // (bit 27: kOwnRound2)
     double* dump = a.own_dump + 8 * (long long)blockIdx.x;
     double v[3];
     if (flags & (kOwnExp | kOwnNop)) {  // EXP: up to kOwnExpRows contributions -> rows target, target+1, ...
@@ -835,8 +875,8 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
                                          double* s_part) {
     lds_barrier();  // the super-batch's forces are in s_fe, the previous pass is done with s_part
     own_entry(a, en, s_fe, s_part);
-    const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
-    if (o1 - o0 > kBlock) {  // block-uniform
+    if (en.y & kOwnRound2) {  // block-uniform
+        const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
         const int idx = o0 + kBlock + (int)threadIdx.x;
         own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe, s_part);
     }
@@ -901,12 +941,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     int4 ent_cur = {0, 0, 0, 0}, ent_nxt = {0, 0, 0, 0};
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
-    if (EXACT) {
-#ifndef HK_EXACT_NO_NODE_PREFETCH
-        load_node(a, cur);
-#endif
-    } else
-        load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
+    if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // its first batch)
     constexpr int S = OS > 0 ? OS : 1;
@@ -915,25 +950,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
-        // (reference-order mode: its longer arithmetic holds more registers, so only the node
-        // gathers run a batch ahead; the Gauss-point state is loaded at the start of the step and
-        // first used after the Jacobian, B-bar and strain passes)
-#ifdef HK_EXACT_NO_NODE_PREFETCH
-        if (EXACT)
-            ;
-        else
-#else
-        if (EXACT)
-            load_node(a, nxt);
-        else
-#endif
-            load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
+        // (reference-order mode: its longer arithmetic holds more registers, so nothing of the
+        // current batch's nodes or Gauss points is loaded a batch ahead -- only connectivity and
+        // flags, two batches ahead. The node gathers are issued at the start of the batch and
+        // first used by the Jacobian, the Gauss-point state first after the B-bar and strain passes.
+        // Measured on C3, one box: 1.090 against 1.120 ms per step with the node gathers a batch ahead.)
+        if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
-#ifdef HK_EXACT_NO_NODE_PREFETCH
             load_node(a, cur);
-#endif
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                                  cur, sfe);

@@ -248,7 +248,9 @@ int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128])
 /* In-process group: contexts in one process that pass the same group_key exchange interface
  * forces with device copies instead of RCCL (several subdomains on one device; the same pack /
  * sum / fix kernels as the RCCL path). The host must step all ranks in lockstep (rank 0..n-1,
- * one hakai_step call of equal length each) on the same device. */
+ * one hakai_step call of equal length each) on the same device: a context on another device than
+ * the group's members is rejected with HAKAI_ERR_ARG (the group's kernels read the peers' buffers
+ * directly; across devices use hakai_comm_init). */
 int hakai_comm_init_local(hakai_ctx* ctx, int rank, int nranks, int64_t group_key);
 /* Steps an in-process group (the n contexts of hakai_comm_init_local, ctxs[r] = rank r) in lockstep,
  * n_steps steps from t_first: per step every rank's contact search (phase A) runs before any rank's

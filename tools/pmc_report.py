@@ -2,11 +2,15 @@
 """Turn rocprofv3 outputs into the bench's roofline evidence (profiles/).
 
 1. Calibration (tools/pmc_calib.hip): FETCH_SIZE / WRITE_SIZE per known byte for each access width.
-2. Element kernel: average FETCH_SIZE / WRITE_SIZE per launch over the LAST `--steps` dispatches
-   (the bench's timed region), corrected by the factor of the kernel's dominant access pattern
-   (8-B-per-lane coalesced SoA loads / stores) -> HBM bytes per launch ("traffic").
-3. Kernel trace: average duration of the same last `--steps` element dispatches, to compare with the
-   HIP-event average the bench reports.
+2. Element kernel: average FETCH_SIZE / WRITE_SIZE per launch over the hot instantiation's
+   dispatches of the bench's timed region -- k_element_pipe with STORE_TRIAX = false (a call's last
+   step stores triaxiality and the element forces too, a different, heavier instantiation), the last
+   `--steps - 1` of them (bench.py --breakdown 0 --compare-fused 0: nothing runs after the timed
+   call) -- corrected by the factor of the kernel's dominant access pattern (8-B-per-lane coalesced
+   SoA loads / stores) -> HBM bytes per launch ("traffic"), reported against the algorithmic bytes
+   both without and with the owner-assembly outputs (entry lists, Q, exported rows).
+3. Kernel trace: average duration of the same dispatches, to compare with the HIP-event average the
+   bench reports.
 Writes profiles/element_pmc.json (read by bench.py) and prints a summary.
 """
 import argparse
@@ -58,18 +62,26 @@ def calib_factors(fetch_dir, write_dir):
     return {p: min(v) if v else None for p, v in fac.items()}  # min over the two repetitions
 
 
+def hot(name):
+    """The timed region's instantiation: k_element_pipe<DO_DELETE, STORE_TRIAX = false, ...>."""
+    if "k_element_pipe<" not in name:
+        return False
+    args = name.split("k_element_pipe<", 1)[1].split(">", 1)[0].split(",")
+    return len(args) > 1 and args[1].strip() == "false"
+
+
 def last_element(d, cn, steps):
-    vals = [cs[cn] for name, cs in counters(d) if "k_element" in name and cn in cs]
-    vals = vals[-steps:]
+    vals = [cs[cn] for name, cs in counters(d) if hot(name) and cn in cs]
+    vals = vals[-(steps - 1):]
     return sum(vals) / len(vals) * 1024.0 if vals else None
 
 
 def trace_avg_ms(kt_dir, steps):
-    rows = [r for r in _rows(kt_dir, "kernel_trace.csv") if "k_element" in r["Kernel_Name"]]
+    rows = [r for r in _rows(kt_dir, "kernel_trace.csv") if hot(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    rows = rows[-steps:]
+    rows = rows[-(steps - 1):]
     ns = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-    return sum(ns) / len(ns) / 1e6, rows[-1]["Kernel_Name"] if rows else ""
+    return sum(ns) / len(ns) / 1e6, rows[-1]["Kernel_Name"] if rows else "", len(rows)
 
 
 def main():
@@ -82,6 +94,9 @@ def main():
     ap.add_argument("--pmc-steps", type=int, required=True, help="timed steps of the PMC bench runs")
     ap.add_argument("--kt-steps", type=int, required=True, help="timed steps of the kernel-trace bench run")
     ap.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per element launch")
+    ap.add_argument("--alg-bytes-own", type=float, default=None,
+                    help="the same plus the owner-assembly outputs (entry lists, Q, exported rows)")
+    ap.add_argument("--element-mode", default=None, help="bench element mode the counters were taken in")
     ap.add_argument("--elements", type=int, default=None, help="elements of the profiled model (bench checks it)")
     ap.add_argument("--out", default="profiles/element_pmc.json")
     a = ap.parse_args()
@@ -92,9 +107,10 @@ def main():
     traffic = None
     if fr and fw and raw_f is not None and raw_w is not None:
         traffic = raw_f / fr + raw_w / fw
-    avg_ms, kname = trace_avg_ms(a.kt, a.kt_steps)
+    avg_ms, kname, n_kt = trace_avg_ms(a.kt, a.kt_steps)
     res = {
         "kernel": kname,
+        "element_mode": a.element_mode,
         "elements": a.elements,
         "calibration_counter_bytes_per_byte": fac,
         "fetch_size_bytes_raw_per_launch": raw_f,
@@ -107,7 +123,12 @@ def main():
         if fac.get("read 8B/lane nontemporal") and fac.get("write 8B/lane nontemporal") and raw_f and raw_w else None,
         "algorithmic_bytes_per_launch": a.alg_bytes,
         "traffic_over_algorithmic": traffic / a.alg_bytes if traffic and a.alg_bytes else None,
-        "kernel_trace_avg_ms_timed_region": avg_ms,
+        "algorithmic_bytes_per_launch_with_assembly_outputs": a.alg_bytes_own,
+        "traffic_over_algorithmic_with_assembly_outputs": traffic / a.alg_bytes_own
+        if traffic and a.alg_bytes_own else None,
+        "kernel_trace_avg_ms": avg_ms,
+        "kernel_trace_dispatches": n_kt,
+        "dispatches_used": "the hot instantiation (STORE_TRIAX=false) of the timed call, no breakdown pass",
     }
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
