@@ -69,6 +69,8 @@ namespace hkc {
 
 static void own_free(hakai_ctx* c) {
     dfree(c->d_own_off);
+    dfree(c->d_own_seq);
+    dfree(c->d_own_bstart);
     dfree(c->d_own_list);
     dfree(c->d_own_q);
     dfree(c->d_own_rp);
@@ -777,42 +779,195 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Owner-computed assembly (tuning "own_assembly"). Logical block lb of the persistent element
-// kernel (grid G) walks batches [lb*nb/G, (lb+1)*nb/G) in order. A node's incidences, in ascending
-// element order (the reference's serial sum, v2/HAKAI_j.jl:668-675), split into consecutive
-// per-block segments. The block holding the FIRST segment sums it in an LDS slot, starting from
-// 0.0 exactly like the nodal gather, and stores the result into own_q[n] (the whole Q when the
-// segment is all of them). Every contribution of a later segment is copied unchanged to its own
-// row, rows of a node consecutive in element order, and the nodal kernel forms
-// ((own_q[n] + row) + row) ... -- the same additions in the same order as the gather of fe, so the
-// result is bit-identical. Rows are numbered by super-batch (an export entry carries up to 4
-// contributions of any nodes to consecutive rows); own_ridx lists each node's rows in element order.
-// One 16-B entry per node segment piece (or exported
-// contribution) per super-batch of S = 2 batches (1 when 2 would need more than 512 entries),
-// one or two per thread (layout: hakai_kernels.hip
-// own_pass). Slots are allocated per block over the super-batches a sum is open; a mesh needing more than kOwnSlots open
-// sums in one block, or a node with > 8 incidences, does not use the mode.
+// Owner-computed assembly (tuning "own_assembly"). Block lb of the persistent element kernel walks
+// a SCHEDULE: the batches at positions [bstart[lb], bstart[lb+1]) of seq, ascending in batch id.
+// A node's incidences, in ascending element order (the reference's serial sum,
+// v2/HAKAI_j.jl:668-675), start with a run held by one block (the head segment). That block sums
+// the run in an LDS slot, starting from 0.0 exactly like the nodal gather, and stores the result
+// into own_q[n] (the whole Q when the run is all of them). Every later contribution is copied
+// unchanged to its own row, rows of a node consecutive in element order, and the nodal kernel
+// forms ((own_q[n] + row) + row) ... -- the same additions in the same order as the gather of fe,
+// so the result is bit-identical whatever the schedule. Rows are numbered by super-batch (an
+// export entry carries up to 4 contributions of any nodes to consecutive rows); own_ridx lists
+// each node's rows in element order. One 16-B entry per node segment piece (or exported
+// contribution) per super-batch of S = 2 schedule positions (1 when 2 would need more than 512
+// entries), one or two per thread (layout: hakai_kernels.hip own_pass). Slots are allocated per
+// block over the super-batches a sum is open; a schedule needing more than kOwnSlots open sums in
+// one block, or a node with > 8 incidences, does not use the mode.
+//
+// Schedules (own_use picks the cheapest that fits):
+//  * contiguous: block lb holds batches [lb*nb/G, (lb+1)*nb/G) -- a slender section (C3) keeps all
+//    of a node layer's sums open in one block;
+//  * banded: on a structured region (element ids x-fastest: the +y neighbour is id+nx, the +z one
+//    id+L) a wide section (C4's 200x200 plate, C5's 100x100 bar) would keep one whole node layer
+//    open (10-40 k sums > 1024 slots), so most contributions became rows. The banded schedule
+//    splits each layer into bands of R element rows and gives each block one band over a run of
+//    layers: a node's 8 incidences then fall in one block unless it sits on a band or run edge.
 // ---------------------------------------------------------------------------------------------
 static constexpr int kOwnSlotsHost = 1024;  // = kOwnSlots in hakai_kernels.hip
 static constexpr int kOwnExpRowsHost = 4;   // = kOwnExpRows: contributions per exported entry
 enum { kOwnInitH = 1, kOwnFinH = 2, kOwnExpH = 4, kOwnNopH = 8 };
 
-static bool own_build(hakai_ctx* c, long long G, int S) {
-    hkc::own_free(c);
+struct OwnSched {
+    std::vector<int> seq;          // [nb] batch at each position
+    std::vector<long long> bstart; // [G+1]
+    bool banded = false;
+};
+
+struct OwnPlan {
+    int S = 2;
+    std::vector<int> off, list, rp, ridx;
+    long long rows = 0, ne = 0;
+    int max_slots = 1;
+    // per-step bytes the lists add beyond the element/nodal kernels' own (entries read, rows
+    // written and read back, row indices): what own_use compares between schedules
+    double cost() const { return 16.0 * (double)ne + 52.0 * (double)rows; }
+};
+
+static OwnSched own_contiguous(long long nb, long long G) {
+    OwnSched sc;
+    sc.seq.resize(nb);
+    for (long long b = 0; b < nb; ++b) sc.seq[b] = (int)b;
+    sc.bstart.resize(G + 1);
+    for (long long lb = 0; lb <= G; ++lb) sc.bstart[lb] = lb * nb / G;
+    return sc;
+}
+
+// Lattice strides of structured regions: element e's (nx, L) from a node whose 8 incidences start
+// with e, {e, e+1, e+nx, e+nx+1, e+L, e+L+1, e+L+nx, e+L+nx+1}; elements without such a node (the
+// last of a row, layer or region) take the previous element's. Regions = runs of equal strides.
+// Returns false when the mesh shows no such lattice.
+static bool lattice_strides(const hakai_ctx* c, std::vector<int>& nx, std::vector<int>& L) {
+    const long long nE = c->nE;
+    nx.assign(nE, -1);
+    L.assign(nE, -1);
+    long long found = 0;
+    for (long long e = 0; e < nE; ++e) {
+        for (int k = 0; k < 8; ++k) {
+            const int n = c->h_conn[8 * e + k];
+            const int j0 = c->h_ptr[n];
+            if (c->h_ptr[n + 1] - j0 != 8 || c->h_inc0[j0] / 8 != e) continue;
+            long long q[8];
+            for (int i = 0; i < 8; ++i) q[i] = c->h_inc0[j0 + i] / 8 - e;
+            const long long a = q[2], l = q[4];
+            if (q[1] == 1 && a > 1 && q[3] == a + 1 && l > a + 1 && q[5] == l + 1 && q[6] == l + a &&
+                q[7] == l + a + 1 && l % a == 0 && l < (1LL << 30)) {
+                nx[e] = (int)a;
+                L[e] = (int)l;
+                ++found;
+                break;
+            }
+        }
+    }
+    if (found * 2 < nE) return false;
+    long long first = -1;
+    for (long long e = 0; e < nE; ++e)
+        if (nx[e] > 0) {
+            first = e;
+            break;
+        }
+    for (long long e = 0; e < nE; ++e) {
+        if (nx[e] > 0) continue;
+        const long long src = e < first ? first : e - 1;
+        nx[e] = nx[src];
+        L[e] = L[src];
+    }
+    return true;
+}
+
+// Banded schedule: each batch goes to the band of its first element, (region, row / R); a band's
+// batches (ascending) are cut into runs, about G * (band batches) / nb of them per band.
+static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& nx, const std::vector<int>& L,
+                       int slot_budget, OwnSched& sc) {
+    const long long nb = c->nEp / 32, nE = c->nE;
+    std::vector<long long> key(nb);
+    long long base = 0;
+    bool any_split = false;
+    long long region = 0, e_prev = -1;
+    for (long long b = 0; b < nb; ++b) {
+        const long long e = std::min(32 * b, nE - 1);
+        // region starts: strides change (regions are contiguous id ranges)
+        for (long long x = e_prev + 1; x <= e; ++x)
+            if (x > 0 && (nx[x] != nx[x - 1] || L[x] != L[x - 1])) {
+                base = x;
+                ++region;
+            }
+        e_prev = e;
+        const long long rows = L[e] / nx[e];
+        long long R = std::max(1, slot_budget / (nx[e] + 1) - 1);
+        if (R >= rows) R = rows;
+        else any_split = true;
+        const long long row = ((e - base) % L[e]) / nx[e];
+        key[b] = (region << 32) | (row / R);
+    }
+    if (!any_split) return false;  // one band per layer everywhere: the contiguous schedule
+    std::vector<int> order(nb);
+    for (long long b = 0; b < nb; ++b) order[b] = (int)b;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
+    // bands: [p, q) ranges of the sorted order; runs per band apportioned to exactly G blocks in
+    // total (largest remainders, at least one per band): more blocks than the persistent grid would
+    // run in a second wave (a whole extra block time)
+    std::vector<std::pair<long long, long long>> bands;
+    for (long long p = 0; p < nb;) {
+        long long q = p;
+        while (q < nb && key[order[q]] == key[order[p]]) ++q;
+        bands.emplace_back(p, q);
+        p = q;
+    }
+    const long long nbands = (long long)bands.size();
+    if (nbands > G) return false;
+    std::vector<long long> runs(nbands);
+    std::vector<std::pair<double, long long>> rem;
+    long long used = 0;
+    for (long long i = 0; i < nbands; ++i) {
+        const long long m = bands[i].second - bands[i].first;
+        const double want = (double)G * (double)m / (double)nb;
+        runs[i] = std::max<long long>(1, std::min<long long>(m, (long long)want));
+        used += runs[i];
+        rem.emplace_back(want - (double)runs[i], i);
+    }
+    std::sort(rem.begin(), rem.end(), [](const std::pair<double, long long>& x, const std::pair<double, long long>& y) {
+        return x.first > y.first || (x.first == y.first && x.second < y.second);
+    });
+    for (size_t r = 0; used < G && r < rem.size(); ++r) {
+        const long long i = rem[r].second;
+        if (runs[i] < bands[i].second - bands[i].first) {
+            ++runs[i];
+            ++used;
+        }
+    }
+    for (long long i = 0; used > G && i < nbands; ++i)  // (the minimum of one run per band overshot)
+        while (runs[i] > 1 && used > G) {
+            --runs[i];
+            --used;
+        }
+    sc.seq = order;
+    sc.bstart.assign(1, 0);
+    for (long long i = 0; i < nbands; ++i) {
+        const long long p = bands[i].first, m = bands[i].second - p;
+        for (long long r = 1; r <= runs[i]; ++r) sc.bstart.push_back(p + r * m / runs[i]);
+    }
+    sc.banded = true;
+    return true;
+}
+
+static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, OwnPlan& pl) {
     const long long nb = c->nEp / 32, nN = c->nN;
-    c->own_built_g = -2;
+    const long long G = (long long)sc.bstart.size() - 1;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
+    pl.S = S;
     struct Ent { int target, slot, flags, n; int lanes[8]; };
-    // super-batches: runs of S batches from each block's first batch (the last one may be short);
-    // sb_first[b] = first batch of b's super-batch, which also indexes the entry lists
-    std::vector<long long> bstart(G + 1);
-    for (long long lb = 0; lb <= G; ++lb) bstart[lb] = lb * nb / G;
-    std::vector<int> block_of(nb);
-    std::vector<long long> sb_first(nb);
+    // pos_of[b]: schedule position of batch b; block_of[b]; sb_pos[b] = position of the first batch
+    // of b's super-batch (runs of S positions from each block's first), which indexes the lists
+    std::vector<int> pos_of(nb), block_of(nb);
+    std::vector<long long> sb_pos(nb);
     for (long long lb = 0; lb < G; ++lb)
-        for (long long b = bstart[lb]; b < bstart[lb + 1]; ++b) {
+        for (long long p = sc.bstart[lb]; p < sc.bstart[lb + 1]; ++p) {
+            const int b = sc.seq[p];
+            if (p > sc.bstart[lb] && b <= sc.seq[p - 1]) return false;  // ascending within a block
+            pos_of[b] = (int)p;
             block_of[b] = (int)lb;
-            sb_first[b] = bstart[lb] + (b - bstart[lb]) / S * S;
+            sb_pos[b] = sc.bstart[lb] + (p - sc.bstart[lb]) / S * S;
         }
     std::vector<std::vector<Ent>> per(nb);
     std::vector<int> rp(nN + 1, 0);
@@ -821,6 +976,13 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
     struct Seg { long long s0, s1; std::vector<std::pair<long long, int>> refs; };
     std::vector<std::vector<Seg>> segs(G);
     auto batch_of = [&](int j) { return (long long)(c->h_inc0[j] / 8) / 32; };
+    // LDS lane of incidence j within its super-batch: (position - super-batch position) * 32 +
+    // element within the batch, times 8, + local node
+    auto lane_of = [&](int j) {
+        const long long e = c->h_inc0[j] / 8;
+        const long long b = e / 32;
+        return (int)(((pos_of[b] - sb_pos[b]) * 32 + (e & 31)) * 8 + c->h_inc0[j] % 8);
+    };
     // contributions of later segments: (super-batch, incidence index j); their rows are numbered
     // in super-batch order so that one entry exports up to 4 of them (any nodes) to consecutive rows
     std::vector<std::pair<long long, int>> exports;
@@ -833,7 +995,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
         const int j0 = c->h_ptr[n], j1 = c->h_ptr[n + 1];
         if (j0 == j1) continue;
         if (all_rows[n]) {
-            for (int j = j0; j < j1; ++j) exports.emplace_back(sb_first[batch_of(j)], j);
+            for (int j = j0; j < j1; ++j) exports.emplace_back(sb_pos[batch_of(j)], j);
             continue;
         }
         const int hb = block_of[batch_of(j0)];
@@ -841,13 +1003,11 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
         Seg sg;
         sg.s0 = -1;
         while (j < j1 && block_of[batch_of(j)] == hb) {  // the head segment, super-batch by super-batch
-            const long long sb = sb_first[batch_of(j)];
+            const long long sb = sb_pos[batch_of(j)];
             Ent en{(int)n, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
-            while (j < j1 && sb_first[batch_of(j)] == sb) {
-                const long long e = c->h_inc0[j] / 8;
-                const int k = c->h_inc0[j] % 8;
+            while (j < j1 && sb_pos[batch_of(j)] == sb) {
                 if (en.n == 8) return false;
-                en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + k);
+                en.lanes[en.n++] = lane_of(j);
                 ++j;
             }
             if (sg.s0 < 0) {
@@ -860,7 +1020,7 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
         }
         per[sg.s1][sg.refs.back().second].flags |= kOwnFinH;
         if (sg.s1 > sg.s0) segs[hb].push_back(std::move(sg));
-        for (; j < j1; ++j) exports.emplace_back(sb_first[batch_of(j)], j);
+        for (; j < j1; ++j) exports.emplace_back(sb_pos[batch_of(j)], j);
     }
     // rows: grouped by super-batch (stable: node order, then element order within a node)
     std::stable_sort(exports.begin(), exports.end(),
@@ -871,15 +1031,15 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
         Ent en{(int)rows, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
         while (q < exports.size() && exports[q].first == sb && en.n < kOwnExpRowsHost) {
             const int j = exports[q].second;
-            const long long e = c->h_inc0[j] / 8;
-            en.lanes[en.n++] = (int)((e - 32 * sb) * 8 + c->h_inc0[j] % 8);
+            en.lanes[en.n++] = lane_of(j);
             row_of_inc[j] = (int)rows++;
             ++q;
         }
         per[sb].push_back(en);
     }
     // per node: its rows in element order (CSR rp / ridx)
-    std::vector<int> ridx;
+    std::vector<int>& ridx = pl.ridx;
+    ridx.clear();
     ridx.reserve(exports.size());
     for (long long n = 0; n < nN; ++n) {
         rp[n] = (int)ridx.size();
@@ -917,13 +1077,15 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
             std::push_heap(busy.begin(), busy.end(), cmp);
         }
     }
-    std::vector<int> off(nb + 1, 0);
+    std::vector<int>& off = pl.off;
+    off.assign(nb + 1, 0);
     for (long long b = 0; b < nb; ++b) {
         if (per[b].size() > 512) return false;  // two entries per thread at most (own_pass)
         off[b + 1] = off[b] + (int)per[b].size();
     }
     const long long ne = off[nb];
-    std::vector<int> list(4 * (size_t)(ne + 1), 0);
+    std::vector<int>& list = pl.list;
+    list.assign(4 * (size_t)(ne + 1), 0);
     for (long long b = 0; b < nb; ++b)
         for (size_t i = 0; i < per[b].size(); ++i) {
             const Ent& en = per[b][i];
@@ -938,27 +1100,39 @@ static bool own_build(hakai_ctx* c, long long G, int S) {
         }
     int* nop = &list[4 * (size_t)ne];  // padding entry: reads lane 0, stores to the dump line
     nop[1] = kOwnNopH << 10;
+    pl.rp = std::move(rp);
+    pl.rows = rows;
+    pl.ne = ne;
+    pl.max_slots = max_slots;
+    return true;
+}
+
+static bool own_upload(hakai_ctx* c, const OwnSched& sc, const OwnPlan& pl) {
+    hkc::own_free(c);
+    const long long nN = c->nN, G = (long long)sc.bstart.size() - 1;
+    std::vector<int> bst(sc.bstart.begin(), sc.bstart.end());
     hipStream_t s = c->stream;
-    HIPCHK(dalloc(&c->d_own_off, off.size()));
-    HIPCHK(dalloc(&c->d_own_list, list.size()));
-    HIPCHK(dalloc(&c->d_own_q, 3 * (size_t)nN));
-    HIPCHK(dalloc(&c->d_own_rp, rp.size()));
-    HIPCHK(dalloc(&c->d_own_rows, 3 * (size_t)std::max(rows, 1LL)));
-    HIPCHK(dalloc(&c->d_own_ridx, std::max<size_t>(ridx.size(), 1)));
-    HIPCHK(dalloc(&c->d_own_dump, 8 * (size_t)G));
-    HIPCHK(hipMemcpyAsync(c->d_own_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->d_own_list, list.data(), list.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->d_own_rp, rp.data(), rp.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    if (!ridx.empty())
-        HIPCHK(hipMemcpyAsync(c->d_own_ridx, ridx.data(), ridx.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(c->d_own_q, 0, 3 * (size_t)nN * sizeof(double), s));  // nodes without elements
-    HIPCHK(hipStreamSynchronize(s));
-    c->own_nop = (int)ne;
-    c->own_slots = max_slots;
-    c->own_rows = rows;
-    c->own_entries = ne;
+    auto up = [&](int** d, const std::vector<int>& h) -> hipError_t {
+        hipError_t e = dalloc(d, std::max<size_t>(h.size(), 1));
+        if (e == hipSuccess && !h.empty()) e = hipMemcpyAsync(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice, s);
+        return e;
+    };
+    if (up(&c->d_own_off, pl.off) || up(&c->d_own_seq, sc.seq) || up(&c->d_own_bstart, bst) ||
+        up(&c->d_own_list, pl.list) || up(&c->d_own_rp, pl.rp) || up(&c->d_own_ridx, pl.ridx) ||
+        dalloc(&c->d_own_q, 3 * (size_t)nN) || dalloc(&c->d_own_rows, 3 * (size_t)std::max(pl.rows, 1LL)) ||
+        dalloc(&c->d_own_dump, 8 * (size_t)G) ||
+        hipMemsetAsync(c->d_own_q, 0, 3 * (size_t)nN * sizeof(double), s) ||  // nodes without elements
+        hipStreamSynchronize(s)) {
+        hkc::own_free(c);
+        return false;
+    }
+    c->own_nop = (int)pl.ne;
+    c->own_slots = pl.max_slots;
+    c->own_rows = pl.rows;
+    c->own_entries = pl.ne;
     c->own_built_g = G;
-    c->own_s = S;
+    c->own_s = pl.S;
+    c->own_banded = sc.banded ? 1 : 0;
     return true;
 }
 
@@ -987,6 +1161,44 @@ static int own_materialize(hakai_ctx* c) {
     return 0;
 }
 
+// Candidate schedules, cheapest plan wins (OwnPlan::cost): contiguous at the persistent grid G0,
+// banded at about G0 blocks (when the mesh has a structured wide section), and, if neither fits,
+// contiguous at 8 G0 (finer ranges keep fewer sums open; the blocks run in waves). Super-batches
+// of 2 batches where they fit 512 entries, else 1. Tuning own_schedule: 0 auto, 1 contiguous only,
+// 2 banded only (tests).
+static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best) {
+    const long long nb = c->nEp / 32;
+    bool have = false;
+    auto consider = [&](const OwnSched& sc) {
+        for (int S : {2, 1}) {
+            OwnPlan pl;
+            if (!own_plan(c, sc, S, pl)) continue;
+            if (!have || pl.cost() < best.cost()) {
+                best = std::move(pl);
+                best_sc = sc;
+                have = true;
+            }
+            return;  // S = 2 fits: S = 1 only adds passes
+        }
+    };
+    if (c->own_schedule != 2) consider(own_contiguous(nb, G0));
+    if (c->own_schedule != 1) {
+        std::vector<int> nx, L;
+        if (lattice_strides(c, nx, L)) {
+            OwnSched sc;
+            for (int budget : {900, 600})
+                if (own_banded(c, G0, nx, L, budget, sc)) {
+                    const bool had = have;
+                    const double before = have ? best.cost() : 0.0;
+                    consider(sc);
+                    if (have && (!had || best.cost() < before)) break;  // the wider bands fit
+                }
+        }
+    }
+    if (!have && c->own_schedule != 2 && 8 * G0 <= nb) consider(own_contiguous(nb, 8 * G0));
+    return have;
+}
+
 static bool own_use(hakai_ctx* c) {
     if (!c->own_assembly || c->nmat > hk::kMaxLdsMats || c->nE <= 0)
         return false;
@@ -994,14 +1206,14 @@ static bool own_use(hakai_ctx* c) {
     if (G0 <= 0) return false;
     if (c->own_for_g0 == G0) return c->own_built_g > 0;  // built (or found not to fit) for this grid
     if (c->own_valid && own_materialize(c)) return false;  // (multi-GPU: step_once reports it)
-    const long long nb = c->nEp / 32;
-    bool ok = false;
-    for (long long G : {G0, 8 * G0}) {
-        if (G > nb) break;
-        if ((ok = own_build(c, G, 2) || own_build(c, G, 1))) break;
+    OwnSched sc;
+    OwnPlan pl;
+    const bool ok = own_choose(c, G0, sc, pl) && own_upload(c, sc, pl);
+    if (!ok) {
+        hkc::own_free(c);
+        c->own_built_g = -2;
     }
     c->own_for_g0 = G0;
-    if (!ok) c->own_built_g = -2;
     return ok;
 }
 
@@ -1101,6 +1313,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     if (own) {
         ea.own = c->own_s;
         ea.own_grid = (int)c->own_built_g;
+        ea.own_seq = c->d_own_seq;
+        ea.own_bstart = c->d_own_bstart;
         ea.own_off = c->d_own_off;
         ea.own_list = reinterpret_cast<const int4*>(c->d_own_list);
         ea.own_nop = c->own_nop;
@@ -1316,6 +1530,8 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
     else if (!std::strcmp(key, "own_superbatch")) *value = c->own_built_g > 0 ? c->own_s : 0;
     else if (!std::strcmp(key, "own_slots")) *value = c->own_built_g > 0 ? c->own_slots : 0;
+    else if (!std::strcmp(key, "own_banded")) *value = c->own_built_g > 0 ? c->own_banded : 0;
+    else if (!std::strcmp(key, "own_grid")) *value = c->own_built_g > 0 ? c->own_built_g : 0;
     else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1391,6 +1607,12 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "own_assembly must be 0 or 1");
         c->own_assembly = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "own_schedule")) {  // owner-assembly schedule: 0 auto, 1 contiguous, 2 banded
+        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_schedule must be 0, 1 or 2");
+        if (c->own_schedule != (int)value) c->own_for_g0 = -1;  // re-planned before the next step
+        c->own_schedule = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "graph")) {

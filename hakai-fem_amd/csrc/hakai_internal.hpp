@@ -132,7 +132,11 @@ struct hakai_ctx {
     long long own_built_g = -1;        // grid the lists were built for (-1 none, -2 mesh not suitable)
     long long own_for_g0 = -1;         // persistent-kernel grid that build was for (a change rebuilds)
     bool own_valid = false;            // d_own_q/d_own_rows hold the last element step's sums
-    int* d_own_off = nullptr;          // [nb+1] per-batch entry offsets
+    int* d_own_off = nullptr;          // [nb+1] entry offsets per schedule position (super-batch starts)
+    int* d_own_seq = nullptr;          // [nb] batch at each schedule position (ascending within a block)
+    int* d_own_bstart = nullptr;       // [grid+1] first schedule position of each block
+    int own_banded = 0;                // the schedule walks row bands of a structured cross-section
+    int own_schedule = 0;              // tuning "own_schedule": 0 auto, 1 contiguous only, 2 banded only
     int* d_own_list = nullptr;         // 4 ints per entry (+ one no-op entry at own_nop)
     int own_nop = 0;
     int own_slots = 0;                 // LDS running-sum slots the lists use (the kernel's dynamic LDS)

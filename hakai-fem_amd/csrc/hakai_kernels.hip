@@ -49,6 +49,7 @@ __device__ constexpr double kSz[8] = {-1., -1., -1., -1., 1., 1., 1., 1.};
 struct ElemIn {
     int n, fl, mt, fb;   // stage A: local node, element flag, material, force base offset
     double x[3], du[3];  // stage B: this lane's node: position = coord + u, d_disp = u - u_pre
+    double cx[3], uu[3], up[3];  // reference-order mode: the node's raw coord, u, u_pre (formed at use)
     double sig[6], eps[6], eqp, ys;
 };
 
@@ -120,6 +121,18 @@ __device__ __forceinline__ void load_node(const ElemArgs& a, ElemIn& in) {
         const double uc = at32(a.u, no)[c];
         in.x[c] = at32(a.coord, no)[c] + uc;
         in.du[c] = uc - at32(a.u_pre, no)[c];
+    }
+}
+
+// The same node, raw: the reference-order kernel issues these loads before the previous batch's
+// summing pass and forms x and du only where it stores them to LDS.
+__device__ __forceinline__ void load_node_raw(const ElemArgs& a, ElemIn& in) {
+    const unsigned no = 24u * (unsigned)in.n;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        in.cx[c] = at32(a.coord, no)[c];
+        in.uu[c] = at32(a.u, no)[c];
+        in.up[c] = at32(a.u_pre, no)[c];
     }
 }
 
@@ -515,12 +528,13 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     const int nd = DO_DELETE ? M->nd : 0;
     double eqp = in.eqp, ys = in.ys;
 
-    nd8[6 * k + 0] = in.x[0];
-    nd8[6 * k + 1] = in.x[1];
-    nd8[6 * k + 2] = in.x[2];
-    nd8[6 * k + 3] = in.du[0];
-    nd8[6 * k + 4] = in.du[1];
-    nd8[6 * k + 5] = in.du[2];
+    // position = coord + u, d_disp = u - u_pre (load_node's expressions) from the raw loads
+    nd8[6 * k + 0] = in.cx[0] + in.uu[0];
+    nd8[6 * k + 1] = in.cx[1] + in.uu[1];
+    nd8[6 * k + 2] = in.cx[2] + in.uu[2];
+    nd8[6 * k + 3] = in.uu[0] - in.up[0];
+    nd8[6 * k + 4] = in.uu[1] - in.up[1];
+    nd8[6 * k + 5] = in.uu[2] - in.up[2];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
@@ -786,7 +800,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
     const long long e = vb * kEPB + grp;
     ElemIn in;
     load_stage_a<EXACT>(a, e, k, in);
-    load_stage_b<true>(a, e, k, in);
+    if (EXACT) {
+        load_node_raw(a, in);
+        load_gp<true>(a, e, k, in);
+    } else {
+        load_stage_b<true>(a, e, k, in);
+    }
     if (EXACT)
         elem_step_exact<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride,
                                                                 s_xb + grp * kXbStride, s_pus, in);
@@ -816,7 +835,9 @@ enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
 
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS only: prefetches stay in flight
+#ifndef HK_DIAG_NO_OWN_BARRIER  // (timing diagnostic only: wrong sums)
     __builtin_amdgcn_s_barrier();
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -921,7 +942,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     //    batches that share a node layer (one element layer apart) are processed close in time on
     //    the same L2 (blocks are dealt round-robin over the 8 XCDs; C3 element reads 2.39 -> 2.20 GB).
     long long first, stride, count;
-    if (OWN || gridDim.x % 8 != 0) {
+    if (OWN) {  // the block's run of schedule positions (own_build: contiguous batches, or row bands)
+        first = a.own_bstart[blockIdx.x];
+        stride = 1;
+        count = a.own_bstart[blockIdx.x + 1] - first;
+    } else if (gridDim.x % 8 != 0) {
         first = (long long)blockIdx.x * nb / gridDim.x;
         stride = 1;
         count = ((long long)blockIdx.x + 1) * nb / gridDim.x - first;
@@ -934,7 +959,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     }
     if (count <= 0) return;  // block-uniform
     // iterations past the end are clamped to the last batch (loaded, never computed)
-    auto vb_of = [&](long long i) { return first + (i < count ? i : count - 1) * stride; };
+    auto pos_of = [&](long long i) { return first + (i < count ? i : count - 1) * stride; };
+    auto vb_of = [&](long long i) { return OWN ? (long long)a.own_seq[pos_of(i)] : pos_of(i); };
     auto elem_of = [&](long long i) { return vb_of(i) * kEPB + grp; };
 
     ElemIn cur, nxt;
@@ -942,10 +968,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
     if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
+#ifdef HK_EXACT_EARLY_NODE
+    if (EXACT) load_node_raw(a, cur);
+#endif
+#ifdef HK_EXACT_EARLY_GP
+    if (EXACT) load_gp<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
+#endif
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
-    // its first batch)
+    // the schedule position of its first batch)
     constexpr int S = OS > 0 ? OS : 1;
-    auto sb_of = [&](long long i) { return vb_of((i < count ? i : count - 1) / S * S); };
+    auto sb_of = [&](long long i) { return pos_of((i < count ? i : count - 1) / S * S); };
     if (OWN) ent_cur = own_load(a, sb_of(0));
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
@@ -959,18 +991,32 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
-            load_node(a, cur);
+#ifndef HK_EXACT_EARLY_NODE
+            load_node_raw(a, cur);
+#endif
+#ifndef HK_EXACT_EARLY_GP
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
+#endif
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                                  cur, sfe);
+            // the next batch's nodes / Gauss points, issued before the summing pass and its
+            // barrier (their registers are free once this batch's write-back is issued)
+#ifdef HK_EXACT_EARLY_NODE
+            load_node_raw(a, nxt);
+#endif
+#ifdef HK_EXACT_EARLY_GP
+            load_gp<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
+#endif
         }
         else
             elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, cur, sfe);
         if (OWN) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
+#ifndef HK_DIAG_NO_OWN_PASS  // (timing diagnostic only: no sums)
             if ((i + 1) % S == 0 || i + 1 == count)
                 own_pass(a, ent_cur, sb_of(i), s_fe + ((i / S) & 1) * kOwnFe, s_part);
+#endif
             ent_cur = ent_nxt;
         }
         cur = nxt;
@@ -1054,7 +1100,7 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
     if (nb <= 0) return hipSuccess;
     if (a.own) {  // owner-computed assembly: persistent kernel only (own_build sized its lists for it)
         if (a.own > 2 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
-            !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > 1024)
+            !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > 1024)
             return hipErrorInvalidValue;
         if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;
         if (a.exact)

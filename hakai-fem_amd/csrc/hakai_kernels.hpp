@@ -40,8 +40,8 @@ struct ElemArgs {
     const double* pusai;    // [8 GP][3][8 nodes] cal_Pusai_hexa table (exact mode)
     const int* poison;      // [0] != 0: a contact buffer overflowed in this call; every state-writing
                             // kernel is a no-op from then on (the state stays the last good step's)
-    // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): logical block lb of
-    // the persistent kernel walks batches [lb*nb/G, (lb+1)*nb/G) in order and sums every node force
+    // Owner-computed assembly (tuning "own_assembly", hakai_capi.cpp own_build): block lb of the
+    // persistent kernel walks its schedule positions (own_seq, own_bstart) in order and sums every node force
     // it holds in LDS, in element order, from a per-batch list of 16-B entries
     // (own_list[own_off[b] .. own_off[b+1]), see OwnEntry in hakai_kernels.hip). It stores each
     // node's complete Q, or the prefix partial P of a node whose later incidences belong to later
@@ -49,7 +49,9 @@ struct ElemArgs {
     // except on a call's last step (STORE_TRIAX), which also stores fe so Q/Qe downloads stay valid.
     int own;                // 0 off; 1 or 2: batches per super-batch
     int own_grid;           // blocks of the owner-assembly launch (the lists' partition)
-    const int* own_off;
+    const int* own_seq;     // [nb] batch at each schedule position; block lb walks positions
+    const int* own_bstart;  // [own_bstart[lb], own_bstart[lb+1]) (batches ascending within a block)
+    const int* own_off;     // [nb+1] entry offsets, indexed by the position of a super-batch's first batch
     const int4* own_list;
     int own_nop;            // index of a no-op entry (list padding)
     int own_slots;          // LDS running-sum slots the lists use (1..1024)

@@ -196,3 +196,55 @@ def test_own_grid_change_between_calls_rebuilds():
         assert sv.stat("own_steps") == 600
     assert len(set(seen)) == 3  # three partitions, three list sets
     _same(g1, g0)
+
+
+@pytest.mark.parametrize("shape", [(100, 100, 16), (200, 200, 5)])
+def test_own_banded_wide_sections_bitexact(shape):
+    """Wide cross-sections (C5's 100x100, C4's plate 200x200): the row-band schedule (own_schedule 2:
+    each block walks one band of element rows over a run of layers) exports far fewer rows than the
+    contiguous batch ranges (own_schedule 1) and both are bit-identical to the fe path."""
+    nx, ny, nz = shape
+    m = small_bar(nx, ny, nz, n_steps=120, v_end=5e5)
+    tune = {"elem_pipe_blocks": 64}
+    calls = [(1, 61), (62, 59)]
+    g0, _, _ = _run(m, calls, tune, 0)
+    res = {}
+    for sched in (1, 2, 0):
+        with Solver(m) as sv:
+            for k, v in tune.items():
+                sv.set_tuning(k, v)
+            sv.set_tuning("own_assembly", 1)
+            sv.set_tuning("own_schedule", sched)
+            for t0, n in calls:
+                sv.step(t0, n)
+            g = sv.download()
+            res[sched] = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_banded", "own_grid")}
+        _same(g, g0)
+    assert res[2]["own_steps"] == 120 and res[2]["own_banded"] == 1, res
+    assert res[1]["own_steps"] in (0, 120), res
+    if res[1]["own_steps"]:
+        assert res[2]["own_rows"] < res[1]["own_rows"], res
+    assert res[0]["own_banded"] == 1 and res[0]["own_rows"] == res[2]["own_rows"], res
+
+
+def test_own_banded_two_bodies_contact_bitexact():
+    """C4's shape at small size: a 120x120 plate and an impactor (two structured regions with
+    different strides), contact on, row bands in each region: bit-identical to the fe path."""
+    m = mesh.two_body_model(plate=(120, 120, 3), impactor=(30, 30, 12), gap=0.05, v=-2e4)
+    n = 300
+    tune = {"elem_pipe_blocks": 48}
+    g0, d0, _ = _run(m, [(1, 151), (152, n - 151)], tune, 0)
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("own_assembly", 1)
+        sv.set_tuning("own_schedule", 2)
+        sv.step(1, 151)
+        sv.step(152, n - 151)
+        g1 = sv.download()
+        d1 = [tuple(x) for x in sv.deleted()]
+        assert sv.stat("own_steps") == n and sv.stat("own_banded") == 1
+    assert d1 == d0
+    assert np.all(np.isfinite(g0.disp)) and np.max(np.abs(g0.disp)) > 0
+    assert np.max(np.abs(g0.Q)) > 0
+    _same(g1, g0)

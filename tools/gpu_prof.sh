@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ -z "$NOTEST" ]; then
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
 fi
 export HAKAI_GRAPH=0  # rocprofv3 cannot trace hipGraph launches; the tests keep the default

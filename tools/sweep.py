@@ -18,6 +18,9 @@ from hakai.solver import Solver  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--layers", type=int, default=5000)
+ap.add_argument("--config", choices=("c3", "c4", "c5slab", "c5"), default="c3",
+                help="c3: 20x20xlayers bar; c4: two-body impact with contact; c5slab: 100x100x200; c5: 100x100x1600")
+ap.add_argument("--preload", type=int, default=400)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--variants", default="simple:elem_pipe_blocks=0;pipe512:elem_pipe_blocks=512")
@@ -29,15 +32,20 @@ for spec in a.variants.split(";"):
     settings = [(k, int(v)) for k, v in (x.split("=") for x in kv.split(",") if x)]
     variants.append((name, settings))
 
-m = mesh.bar_model(20, 20, a.layers, mesh.steel_ductile(), lambda z, L: 5e5 * z / L, name="C3")
+if a.config == "c3":
+    m = mesh.bar_model(20, 20, a.layers, mesh.steel_ductile(), lambda z, L: 5e5 * z / L, name="C3")
+elif a.config == "c4":
+    m = mesh.config_c4()
+else:
+    m = mesh.config_c5(layers=200 if a.config == "c5slab" else 1600)
 diag, _ = m.lumped_mass()
 sv = Solver(m, diag_M=diag)
-sv.step(1, 400)
+sv.step(1, a.preload)
 sv.sync()
-t = 401
+t = a.preload + 1
 res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
 DEFAULTS = {"elem_exact": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_pipe_min": 2, "elem_gp_nt": 1,
-            "own_assembly": 1}
+            "own_assembly": 1, "own_schedule": 0}
 for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
@@ -58,6 +66,8 @@ for r in range(a.rounds):
         dt = time.perf_counter() - t0
         t += a.steps
         res[name]["step"].append(dt / a.steps * 1e3)
+        res[name]["own"] = {k: sv.stat(k) for k in ("own_rows", "own_entries", "own_banded", "own_grid")}
 for name, d in res.items():
     print(f"{name:10s} element {statistics.median(d['el']):.4f} ms/step (min {min(d['el']):.4f})  "
-          f"nodal {statistics.median(d['nd']):.4f} ms/step  step {statistics.median(d['step']):.4f} ms (unprofiled wall)")
+          f"nodal {statistics.median(d['nd']):.4f} ms/step  step {statistics.median(d['step']):.4f} ms (unprofiled wall)  "
+          f"{d.get('own')}")
