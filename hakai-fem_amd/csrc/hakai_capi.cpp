@@ -804,11 +804,11 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 //    splits each layer into bands of R element rows and gives each block one band over a run of
 //    layers: a node's 8 incidences then fall in one block unless it sits on a band or run edge.
 // ---------------------------------------------------------------------------------------------
-static constexpr int kOwnSlotsHost = 1024;  // = kOwnSlots in hakai_kernels.hip
 static constexpr int kOwnExpRowsHost = 4;   // = kOwnExpRows: contributions per exported entry
 enum { kOwnInitH = 1, kOwnFinH = 2, kOwnExpH = 4, kOwnNopH = 8 };
 
 struct OwnSched {
+    int epb = 32;                  // elements per batch: 32 (block units) or 8 (wave units)
     std::vector<int> seq;          // [nb] batch at each position
     std::vector<long long> bstart; // [G+1]
     bool banded = false;
@@ -819,13 +819,15 @@ struct OwnPlan {
     std::vector<int> off, list, rp, ridx;
     long long rows = 0, ne = 0;
     int max_slots = 1;
+    long long round2 = 0;  // summing passes with more than one entry per thread
     // per-step bytes the lists add beyond the element/nodal kernels' own (entries read, rows
     // written and read back, row indices): what own_use compares between schedules
     double cost() const { return 16.0 * (double)ne + 52.0 * (double)rows; }
 };
 
-static OwnSched own_contiguous(long long nb, long long G) {
+static OwnSched own_contiguous(long long nb, long long G, int epb) {
     OwnSched sc;
+    sc.epb = epb;
     sc.seq.resize(nb);
     for (long long b = 0; b < nb; ++b) sc.seq[b] = (int)b;
     sc.bstart.resize(G + 1);
@@ -878,14 +880,15 @@ static bool lattice_strides(const hakai_ctx* c, std::vector<int>& nx, std::vecto
 // Banded schedule: each batch goes to the band of its first element, (region, row / R); a band's
 // batches (ascending) are cut into runs, about G * (band batches) / nb of them per band.
 static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& nx, const std::vector<int>& L,
-                       int slot_budget, OwnSched& sc) {
-    const long long nb = c->nEp / 32, nE = c->nE;
+                       int shrink, int epb, int slot_cap, OwnSched& sc) {
+    const long long nb = c->nEp / epb, nE = c->nE;
+    sc.epb = epb;
     std::vector<long long> key(nb);
     long long base = 0;
     bool any_split = false;
     long long region = 0, e_prev = -1;
     for (long long b = 0; b < nb; ++b) {
-        const long long e = std::min(32 * b, nE - 1);
+        const long long e = std::min(epb * b, nE - 1);
         // region starts: strides change (regions are contiguous id ranges)
         for (long long x = e_prev + 1; x <= e; ++x)
             if (x > 0 && (nx[x] != nx[x - 1] || L[x] != L[x - 1])) {
@@ -894,7 +897,11 @@ static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& 
             }
         e_prev = e;
         const long long rows = L[e] / nx[e];
-        long long R = std::max(1, slot_budget / (nx[e] + 1) - 1);
+        // a band of R element rows keeps up to about R + 1 node rows of sums open in its block: the
+        // R - 1 interior rows of the node layer below, closing row by row, while the layer above
+        // opens, plus what a super-batch holds (measured with tools/own_plan_check: 1071 slots at
+        // R = 4 on a 200-wide section, 1264 at R = 5)
+        long long R = std::max(1, (slot_cap - slot_cap / 16) / (nx[e] + 1) - 1 - shrink);
         if (R >= rows) R = rows;
         else any_split = true;
         const long long row = ((e - base) % L[e]) / nx[e];
@@ -951,8 +958,9 @@ static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& 
     return true;
 }
 
-static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, OwnPlan& pl) {
-    const long long nb = c->nEp / 32, nN = c->nN;
+static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap, OwnPlan& pl) {
+    const int epb = sc.epb, bs = 8 * epb;  // elements per batch, threads per block
+    const long long nb = c->nEp / epb, nN = c->nN;
     const long long G = (long long)sc.bstart.size() - 1;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
     pl.S = S;
@@ -975,13 +983,13 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, OwnPlan& pl)
     // open-sum intervals per block in super-batch units: (first, last, entry refs to patch the slot)
     struct Seg { long long s0, s1; std::vector<std::pair<long long, int>> refs; };
     std::vector<std::vector<Seg>> segs(G);
-    auto batch_of = [&](int j) { return (long long)(c->h_inc0[j] / 8) / 32; };
-    // LDS lane of incidence j within its super-batch: (position - super-batch position) * 32 +
+    auto batch_of = [&](int j) { return (long long)(c->h_inc0[j] / 8) / epb; };
+    // LDS lane of incidence j within its super-batch: (position - super-batch position) * epb +
     // element within the batch, times 8, + local node
     auto lane_of = [&](int j) {
         const long long e = c->h_inc0[j] / 8;
-        const long long b = e / 32;
-        return (int)(((pos_of[b] - sb_pos[b]) * 32 + (e & 31)) * 8 + c->h_inc0[j] % 8);
+        const long long b = e / epb;
+        return (int)(((pos_of[b] - sb_pos[b]) * epb + e % epb) * 8 + c->h_inc0[j] % 8);
     };
     // contributions of later segments: (super-batch, incidence index j); their rows are numbered
     // in super-batch order so that one entry exports up to 4 of them (any nodes) to consecutive rows
@@ -1070,7 +1078,7 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, OwnPlan& pl)
             } else {
                 slot = next++;
             }
-            if (slot >= kOwnSlotsHost) return false;
+            if (slot >= slot_cap) return false;
             max_slots = std::max(max_slots, slot + 1);
             for (auto& r : sg.refs) per[r.first][r.second].slot = slot;
             busy.emplace_back(sg.s1, slot);
@@ -1080,7 +1088,8 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, OwnPlan& pl)
     std::vector<int>& off = pl.off;
     off.assign(nb + 1, 0);
     for (long long b = 0; b < nb; ++b) {
-        if (per[b].size() > 512) return false;  // two entries per thread at most (own_pass)
+        if (per[b].size() > 2 * (size_t)bs) return false;  // two entries per thread at most (own_pass)
+        pl.round2 += per[b].size() > (size_t)bs ? 1 : 0;
         off[b + 1] = off[b] + (int)per[b].size();
     }
     const long long ne = off[nb];
@@ -1132,6 +1141,7 @@ static bool own_upload(hakai_ctx* c, const OwnSched& sc, const OwnPlan& pl) {
     c->own_entries = pl.ne;
     c->own_built_g = G;
     c->own_s = pl.S;
+    c->own_round2 = pl.round2;
     c->own_banded = sc.banded ? 1 : 0;
     return true;
 }
@@ -1167,35 +1177,33 @@ static int own_materialize(hakai_ctx* c) {
 // of 2 batches where they fit 512 entries, else 1. Tuning own_schedule: 0 auto, 1 contiguous only,
 // 2 banded only (tests).
 static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best) {
-    const long long nb = c->nEp / 32;
+    const int epb = 32;
+    const long long nb = c->nEp / epb;
+    const int cap = hk::kOwnSlots;
     bool have = false;
     auto consider = [&](const OwnSched& sc) {
         for (int S : {2, 1}) {
             OwnPlan pl;
-            if (!own_plan(c, sc, S, pl)) continue;
+            if (!own_plan(c, sc, S, cap, pl)) continue;
             if (!have || pl.cost() < best.cost()) {
                 best = std::move(pl);
                 best_sc = sc;
                 have = true;
             }
-            return;  // S = 2 fits: S = 1 only adds passes
+            return true;  // S = 2 fits: S = 1 only adds passes
         }
+        return false;
     };
-    if (c->own_schedule != 2) consider(own_contiguous(nb, G0));
+    if (c->own_schedule != 2) consider(own_contiguous(nb, G0, epb));
     if (c->own_schedule != 1) {
         std::vector<int> nx, L;
         if (lattice_strides(c, nx, L)) {
             OwnSched sc;
-            for (int budget : {900, 600})
-                if (own_banded(c, G0, nx, L, budget, sc)) {
-                    const bool had = have;
-                    const double before = have ? best.cost() : 0.0;
-                    consider(sc);
-                    if (have && (!had || best.cost() < before)) break;  // the wider bands fit
-                }
+            for (int shrink : {0, 1, 2, 4})  // the widest bands whose open sums fit a block's slots
+                if (own_banded(c, G0, nx, L, shrink, epb, cap, sc) && consider(sc)) break;
         }
     }
-    if (!have && c->own_schedule != 2 && 8 * G0 <= nb) consider(own_contiguous(nb, 8 * G0));
+    if (!have && c->own_schedule != 2 && 8 * G0 <= nb) consider(own_contiguous(nb, 8 * G0, epb));
     return have;
 }
 
@@ -1204,16 +1212,25 @@ static bool own_use(hakai_ctx* c) {
         return false;
     const long long G0 = own_grid(c);
     if (G0 <= 0) return false;
-    if (c->own_for_g0 == G0) return c->own_built_g > 0;  // built (or found not to fit) for this grid
-    if (c->own_valid && own_materialize(c)) return false;  // (multi-GPU: step_once reports it)
-    OwnSched sc;
-    OwnPlan pl;
-    const bool ok = own_choose(c, G0, sc, pl) && own_upload(c, sc, pl);
-    if (!ok) {
-        hkc::own_free(c);
-        c->own_built_g = -2;
+    bool ok = c->own_built_g > 0;
+    if (c->own_for_g0 != G0) {  // not yet built (or found not to fit) for this grid
+        if (c->own_valid && own_materialize(c)) return false;  // (multi-GPU: step_once reports it)
+        OwnSched sc;
+        OwnPlan pl;
+        ok = own_choose(c, G0, sc, pl) && own_upload(c, sc, pl);
+        if (!ok) {
+            hkc::own_free(c);
+            c->own_built_g = -2;
+        }
+        c->own_for_g0 = G0;
     }
-    c->own_for_g0 = G0;
+    // The reference-order kernel's waves drift apart within a batch more than the fused kernel's, so
+    // its block waits at the pass barrier for its slowest wave; passes that load a second entry
+    // inside that barrier region (wide cross-sections) make the wait long, and there the fe path is
+    // faster for this kernel (C5 slab 1.12 against 1.41 ms per step, C4 2.46 against 3.25,
+    // profiles/r03_wave_units_sweep.log). own_assembly 2 uses the owner sums anyway (tests); a
+    // multi-GPU rank whose owner sums are live keeps them (its interface fix needs the rows).
+    if (ok && c->elem_exact && c->own_round2 > 0 && c->own_assembly == 1 && !(c->comm && c->own_valid)) return false;
     return ok;
 }
 
@@ -1529,6 +1546,7 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     else if (!std::strcmp(key, "own_rows")) *value = c->own_built_g > 0 ? c->own_rows : -1;
     else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
     else if (!std::strcmp(key, "own_superbatch")) *value = c->own_built_g > 0 ? c->own_s : 0;
+    else if (!std::strcmp(key, "own_round2")) *value = c->own_built_g > 0 ? c->own_round2 : 0;
     else if (!std::strcmp(key, "own_slots")) *value = c->own_built_g > 0 ? c->own_slots : 0;
     else if (!std::strcmp(key, "own_banded")) *value = c->own_built_g > 0 ? c->own_banded : 0;
     else if (!std::strcmp(key, "own_grid")) *value = c->own_built_g > 0 ? c->own_built_g : 0;
@@ -1605,7 +1623,7 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         return c->d_inc8 ? 0 : fail(HAKAI_ERR_STATE, "padded incidence table unavailable (>8 incidences)");
     }
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "own_assembly must be 0 or 1");
+        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_assembly must be 0, 1 or 2");
         c->own_assembly = (int)value;
         return 0;
     }

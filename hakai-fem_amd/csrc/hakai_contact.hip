@@ -61,7 +61,8 @@ struct PairParam {
 // the end of step s-1 (or at the state reset, s = 0), so an in-process group stepped rank by rank
 // finds every peer's block ready. The triangle search is divided across the ranks (contact_divide,
 // the reference's triangle-parallel loop :2370, :2386, :2653-2667): rank r tests the candidate
-// triangles j = r (mod N) and the events are all-gathered before the force sums.
+// triangles j with (j / 64) = r (mod N) and the events are all-gathered before the force sums
+// (DESIGN.md §5); the mirror all-gather, boxes, binning and bucket fill stay on every rank.
 // Two node sets travel: X0, the nodes of the entries live from the start (every step, owner
 // packs), and X1, the nodes only a deletion exposes. An X1 node is shipped by every rank that
 // deleted one of its adders (the adder contains the node, so that rank holds it), from the step
@@ -117,7 +118,7 @@ struct Mirror {
     int* d_last_del = nullptr;        // [neo] deletion step of own contact elements at the last pack
     size_t off_x1 = 0, off_x1v0 = 0;  // X1 region (u, u_pre per slot entry); at s = 0 also velo0
     // Divided search (tuning "contact_divide", default on): rank r searches the candidate
-    // triangles j with j % nranks == r; the events of all ranks are all-gathered each step and
+    // triangles j with (j / 64) % nranks == r; the events of all ranks are all-gathered each step and
     // every rank runs the same order-independent double-double sums, so the forces are unchanged.
     int divide = 1;
     bool div_step = false;            // the current step runs divided (set by phase A)
@@ -127,7 +128,11 @@ struct Mirror {
     int* d_evcnt = nullptr;           // [2][2] this rank's (event count, overflow) of step t in slot t & 1
                                       // (double-buffered like d_ev_send: in-process peers read it)
     int* d_evcnt_all = nullptr;       // [2 nranks] every rank's
-    int* h_evcnt = nullptr;           // pinned [2 nranks]: every rank's, read by the host; [2 nranks..] own
+    int* h_evcnt = nullptr;           // pinned [4][2 nranks]: every rank's, read by the host two steps later
+    hipEvent_t ev_ag[4] = {nullptr, nullptr, nullptr, nullptr};  // h_evcnt slot s filled
+    long long ag_cap = 0;             // RCCL: event records per rank in the all-gather (grow-only, the same
+                                      // on every rank: decided from gathered counts)
+    long long ag_seq = 0;             // RCCL phase B calls (h_evcnt slot = ag_seq & 3)
     hipEvent_t ev_evpacked = nullptr; // this rank's events packed (in-process peers wait on it)
     char* d_ev_recv = nullptr;        // [nranks][max events of the step] EvRec
     size_t ev_recv_bytes = 0;
@@ -891,7 +896,9 @@ __device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam
 
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
 // side of the range box along any axis -> candidate record
-// (multi-GPU divided search: only the triangles j with j % own_n == own_r)
+// (multi-GPU divided search: only the triangles j with (j / 64) % own_n == own_r -- runs of 64
+// consecutive ids, so a wave of the live list mostly belongs to one rank, and the contact zone's
+// triangles still spread over every rank)
 __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s, const int* tri_cnt,
                                                 const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                 const int* tri_ele, const PairParam* par,
@@ -901,10 +908,15 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
     __shared__ unsigned s_app[2];
     for (int q0 = bid * blockDim.x; q0 < n; q0 += nb * blockDim.x) {  // block-uniform trip count
         const int q = q0 + (int)threadIdx.x;
-        // every load unconditional (lanes past the end re-read the last entry), so the chain is
-        // three round trips -- live entry; its element, pair and nodes; flag, pair box, positions
-        // and pair parameters -- instead of one per test
-        const int j = tri_live[q < n ? q : n - 1];
+        // every load of an owned triangle unconditional (lanes past the end re-read the last
+        // entry), so the chain is three round trips -- live entry; its element, pair and nodes;
+        // flag, pair box, positions and pair parameters -- instead of one per test. A triangle
+        // another rank owns (divided search) loads nothing past its live entry: it re-reads the
+        // wave's first entry instead, whose lines the wave fetches anyway, so each rank moves about
+        // 1/N of the triangle data.
+        const int j0 = tri_live[q < n ? q : n - 1];
+        const bool mine = own_n <= 1 || (j0 >> 6) % own_n == own_r;
+        const int j = mine ? j0 : __shfl(j0, 0);
         const int ele = tri_ele[j], pr = tri_pair[j];
         const int nd0 = tri_nodes[3 * j], nd1 = tri_nodes[3 * j + 1], nd2 = tri_nodes[3 * j + 2];
         const int fl = s.flag[ele];
@@ -914,7 +926,7 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
         pos(s, nd0, p0);
         pos(s, nd1, p1);
         pos(s, nd2, p2);
-        bool keep = q < n && (own_n <= 1 || j % own_n == own_r) && fl == 1 && !r.empty;  // own triangles only
+        bool keep = q < n && mine && fl == 1 && !r.empty;  // own triangles only
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             keep &= !(p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]);
@@ -1388,13 +1400,16 @@ struct CntPtrs {
     const int* p[kMaxDivRanks];
 };
 
-// rank prefix of the gathered counts in LDS; block 0 publishes the total
-__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const CntPtrs& cp, int nr, long long* s_off) {
+// rank prefix of the gathered counts in LDS; block 0 publishes the total. A count beyond the
+// gathered rows (stride; the step is poisoned then, k_ct_count_g) is clamped to them, so no read
+// leaves its rank's rows.
+__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const CntPtrs& cp, int nr, long long* s_off,
+                                                 long long stride) {
     if (threadIdx.x == 0) {
         long long run = 0;
         for (int q = 0; q < nr; ++q) {
             s_off[q] = run;
-            run += __hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            run += min((long long)__hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), stride);
         }
         s_off[nr] = run;
         if (blockIdx.x == 0) {
@@ -1421,13 +1436,15 @@ __global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long strid
     __shared__ unsigned s_app[2];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         bool over = false;
-        for (int q = 0; q < nr; ++q) over |= __hip_atomic_load(cp.p[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        for (int q = 0; q < nr; ++q)
+            over |= __hip_atomic_load(cp.p[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                    __hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > stride;
         if (over && poison[0] == 0) {
             poison[1] = pstep;
             poison[0] = 1;
         }
     }
-    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off);
+    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off, stride);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
@@ -1448,7 +1465,7 @@ __global__ void k_ct_scatter_g(const EvRec* ev, long long stride, CntPtrs cp, in
                                const int* toff, const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
     __shared__ long long s_off[kMaxDivRanks + 1];
-    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off);
+    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off, stride);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
         const EvRec* r = rank_ev(ev, stride, s_off, nr, e >> 2);
@@ -1871,6 +1888,8 @@ void contact_destroy(hakai_ctx* c) {
         if (M->h_need) (void)hipHostFree(M->h_need);
         for (auto& e : M->ev_need)
             if (e) (void)hipEventDestroy(e);
+        for (auto& e : M->ev_ag)
+            if (e) (void)hipEventDestroy(e);
         delete M;
     }
     delete C;
@@ -2207,25 +2226,39 @@ int contact_step_b(hakai_ctx* c) {
     const EvRec* ev = nullptr;
     long long stride = 1;
     if (comm_is_rccl(c)) {
-        // the counts first (8 B per rank), read back to size the event all-gather exactly
-        int* h = M->h_evcnt;
+        // The counts (8 B per rank) are all-gathered for the kernels, which read them on the device;
+        // the event all-gather moves ag_cap records per rank, a grow-only capacity decided from the
+        // gathered counts of two steps earlier -- the same numbers on every rank, so every rank
+        // sizes the collective alike, and no host round trip stalls the step. A rank with more
+        // events than ag_cap poisons the step on every rank (k_ct_count_g) and the capacity then
+        // grows from that step's counts (contact_after_overflow).
         if (int rc = comm_allgather_raw(c, M->d_evcnt + 2 * (M->div_t & 1), M->d_evcnt_all, 2 * sizeof(int)))
             return rc;
-        HIPCHK(hipMemcpyAsync(h, M->d_evcnt_all, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        long long mx = 0;
-        for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, h[2 * q]);
-        const size_t need = (size_t)nr * (size_t)std::max<long long>(mx, 1) * sizeof(EvRec);
+        if (M->ag_seq >= 2) {
+            const long long sl = (M->ag_seq - 2) & 3;
+            HIPCHK(hipEventSynchronize(M->ev_ag[sl]));  // two steps old: long done
+            long long mx = 0;
+            for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, M->h_evcnt[2 * nr * sl + 2 * q]);
+            if (2 * mx > M->ag_cap) M->ag_cap = std::max(2 * M->ag_cap, 4 * mx);
+        }
+        if (M->ag_cap <= 0) M->ag_cap = 4096;  // records (160 KB per rank)
+        const long long sl = M->ag_seq & 3;
+        HIPCHK(hipMemcpyAsync(M->h_evcnt + 2 * nr * sl, M->d_evcnt_all, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(M->ev_ag[sl], s));
+        ++M->ag_seq;
+        // (the send buffers hold ev_cap records, the event buffer's capacity, which contact_event_cap
+        // sets alike on every rank; a rank cannot pack more)
+        M->ag_cap = std::min(M->ag_cap, std::max<long long>(M->ev_cap, 1));
+        stride = M->ag_cap;
+        const size_t need = (size_t)nr * (size_t)stride * sizeof(EvRec);
         if (need > M->ev_recv_bytes) {
             HIPCHK(hipStreamSynchronize(s));
             dfree(M->d_ev_recv);
             HIPCHK(dalloc(&M->d_ev_recv, need));
             M->ev_recv_bytes = need;
         }
-        stride = std::max<long long>(mx, 1);
-        if (mx > 0)
-            if (int rc = comm_allgather_raw(c, M->d_ev_send[M->div_t & 1], M->d_ev_recv, (size_t)mx * sizeof(EvRec)))
-                return rc;
+        if (int rc = comm_allgather_raw(c, M->d_ev_send[M->div_t & 1], M->d_ev_recv, (size_t)stride * sizeof(EvRec)))
+            return rc;
         for (int q = 0; q < nr; ++q) cp.p[q] = M->d_evcnt_all + 2 * q;
     } else {
         // in-process group: the peers' counts and events are read on the device after a stream
@@ -2290,7 +2323,15 @@ void contact_after_overflow(hakai_ctx* c, long long steps_since_reset) {
     C->force_rebuild = true;
     C->use_velo0 = steps_since_reset == 0;
     C->last_t = -1;
-    if (C->mir) c->poison_halt = true;
+    if (Mirror* M = C->mir) {
+        c->poison_halt = true;
+        // RCCL divided search: grow the event all-gather past every count the call saw (the stream
+        // is drained here; the gathered counts are the same on every rank, so is the new capacity)
+        const int nr = M->nranks;
+        for (long long k = std::max(0LL, M->ag_seq - 4); k < M->ag_seq; ++k)
+            for (int q = 0; q < nr; ++q)
+                M->ag_cap = std::max<long long>(M->ag_cap, 2LL * M->h_evcnt[2 * nr * (k & 3) + 2 * q]);
+    }
 }
 
 void contact_graph_advance(hakai_ctx* c, double t_last) {
@@ -3023,7 +3064,9 @@ int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nE
     for (auto& p : M->d_ev_send) HIPCHK(hipMalloc(&p, (size_t)M->ev_cap * sizeof(EvRec)));
     HIPCHK(dalloc(&M->d_evcnt, 4));
     HIPCHK(dalloc(&M->d_evcnt_all, 2 * (size_t)nr));
-    HIPCHK(hipHostMalloc((void**)&M->h_evcnt, (2 * (size_t)nr + 2) * sizeof(int), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&M->h_evcnt, (8 * (size_t)nr + 2) * sizeof(int), hipHostMallocDefault));
+    std::fill(M->h_evcnt, M->h_evcnt + 8 * (size_t)nr + 2, 0);
+    for (auto& e : M->ev_ag) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&M->ev_evpacked, hipEventDisableTiming));
     for (int p = 0; p < 2; ++p)
         if (int rc = hkc::mir_buffers(c, p)) return rc;

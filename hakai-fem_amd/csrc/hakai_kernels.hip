@@ -833,11 +833,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
 constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
 enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
 
+// LDS-only barrier: the pipeline's global prefetches stay in flight.
 __device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS only: prefetches stay in flight
-#ifndef HK_DIAG_NO_OWN_BARRIER  // (timing diagnostic only: wrong sums)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
-#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -968,12 +967,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
     load_stage_a<EXACT>(a, elem_of(1), k, nxt);
     if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
-#ifdef HK_EXACT_EARLY_NODE
-    if (EXACT) load_node_raw(a, cur);
-#endif
-#ifdef HK_EXACT_EARLY_GP
-    if (EXACT) load_gp<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
-#endif
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // the schedule position of its first batch)
     constexpr int S = OS > 0 ? OS : 1;
@@ -986,37 +979,25 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         // current batch's nodes or Gauss points is loaded a batch ahead -- only connectivity and
         // flags, two batches ahead. The node gathers are issued at the start of the batch and
         // first used by the Jacobian, the Gauss-point state first after the B-bar and strain passes.
-        // Measured on C3, one box: 1.090 against 1.120 ms per step with the node gathers a batch ahead.)
+        // Measured on C3, one box: 1.090 against 1.120 ms per step with the node gathers a batch ahead;
+        // issuing this batch's node and/or Gauss-point loads at the end of the previous batch (before
+        // its summing pass) spills and measured 1.18-1.28 against 1.10 ms, profiles/r03_exact_early_loads_ab.log.)
         if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
-#ifndef HK_EXACT_EARLY_NODE
             load_node_raw(a, cur);
-#endif
-#ifndef HK_EXACT_EARLY_GP
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
-#endif
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
                                                                                  cur, sfe);
-            // the next batch's nodes / Gauss points, issued before the summing pass and its
-            // barrier (their registers are free once this batch's write-back is issued)
-#ifdef HK_EXACT_EARLY_NODE
-            load_node_raw(a, nxt);
-#endif
-#ifdef HK_EXACT_EARLY_GP
-            load_gp<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
-#endif
         }
         else
             elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, cur, sfe);
         if (OWN) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
-#ifndef HK_DIAG_NO_OWN_PASS  // (timing diagnostic only: no sums)
             if ((i + 1) % S == 0 || i + 1 == count)
                 own_pass(a, ent_cur, sb_of(i), s_fe + ((i / S) & 1) * kOwnFe, s_part);
-#endif
             ent_cur = ent_nxt;
         }
         cur = nxt;
@@ -1100,9 +1081,9 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
     if (nb <= 0) return hipSuccess;
     if (a.own) {  // owner-computed assembly: persistent kernel only (own_build sized its lists for it)
         if (a.own > 2 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
-            !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > 1024)
+            !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > kOwnSlots)
             return hipErrorInvalidValue;
-        if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;
+        if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;  // (own_bstart has grid+1 entries)
         if (a.exact)
             launch_pipe_p<true>(a, do_delete, store_triax, (unsigned)a.own_grid, s);
         else

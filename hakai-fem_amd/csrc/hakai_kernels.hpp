@@ -47,7 +47,7 @@ struct ElemArgs {
     // node's complete Q, or the prefix partial P of a node whose later incidences belong to later
     // blocks, into own_q, and those later contributions one by one into own_rows. No fe traffic
     // except on a call's last step (STORE_TRIAX), which also stores fe so Q/Qe downloads stay valid.
-    int own;                // 0 off; 1 or 2: batches per super-batch
+    int own;                // 0 off; 1 or 2: batches of 32 elements per summing pass
     int own_grid;           // blocks of the owner-assembly launch (the lists' partition)
     const int* own_seq;     // [nb] batch at each schedule position; block lb walks positions
     const int* own_bstart;  // [own_bstart[lb], own_bstart[lb+1]) (batches ascending within a block)
@@ -99,6 +99,9 @@ struct NodalArgs {
     const double* own_rows;
 };
 
+
+// LDS running-sum slots one block of the owner-assembly element kernel holds (24 KB; 2 blocks per CU)
+constexpr int kOwnSlots = 1024;
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
 hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s);

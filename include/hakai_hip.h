@@ -123,7 +123,8 @@ int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
  * steps with owner-computed assembly), "own_rows" / "own_entries" (its exported rows / per-batch
  * entries for this mesh), "own_superbatch" (batches of 32 elements per LDS summing pass: 2, or 1
  * for wide meshes), "own_slots" (LDS running sums a block keeps open at most), "own_banded" (1: the
- * blocks walk row bands of a structured wide cross-section), "own_grid" (blocks of that schedule). */
+ * blocks walk row bands of a structured wide cross-section), "own_grid" (blocks of that schedule),
+ * "own_round2" (summing passes that take a second entry per thread). */
 int hakai_stat(hakai_ctx* ctx, const char* key, int64_t* value);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
@@ -180,7 +181,10 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *   "own_assembly"      1 (default; env HAKAI_OWN_ASSEMBLY): the persistent element kernel sums node
  *                       forces in LDS in element order and hands the nodal update Q (+ the rows of
  *                       nodes shared between blocks) instead of the per-element force array; meshes
- *                       it does not fit use that array (hakai_stat "own_steps");
+ *                       it does not fit use that array (hakai_stat "own_steps"), and so does the
+ *                       reference-order kernel where the lists need two entries per thread in some
+ *                       pass (wide sections, hakai_stat "own_round2": the array is faster there);
+ *                       2: the owner sums wherever they fit;
  *   "own_schedule"      its block schedule: 0 (default) the cheapest that fits, 1 contiguous batch
  *                       ranges only, 2 row bands of structured wide sections only;
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;

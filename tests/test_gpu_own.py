@@ -205,7 +205,7 @@ def test_own_banded_wide_sections_bitexact(shape):
     contiguous batch ranges (own_schedule 1) and both are bit-identical to the fe path."""
     nx, ny, nz = shape
     m = small_bar(nx, ny, nz, n_steps=120, v_end=5e5)
-    tune = {"elem_pipe_blocks": 64}
+    tune = {"elem_pipe_blocks": 128}  # (the 200-wide section's 67 row bands need a block each)
     calls = [(1, 61), (62, 59)]
     g0, _, _ = _run(m, calls, tune, 0)
     res = {}
@@ -248,3 +248,20 @@ def test_own_banded_two_bodies_contact_bitexact():
     assert np.all(np.isfinite(g0.disp)) and np.max(np.abs(g0.disp)) > 0
     assert np.max(np.abs(g0.Q)) > 0
     _same(g1, g0)
+
+
+@pytest.mark.parametrize("shape", [(100, 100, 12), (20, 20, 60)])
+def test_own_reference_order_mode_bitexact(shape):
+    """The reference-order kernel with owner sums forced on (own_assembly 2), on a wide section
+    whose lists need second-entry passes (where the default, own_assembly 1, takes the fe path) and
+    on a slender one: bit-identical to the fe path."""
+    m = small_bar(*shape, n_steps=80, v_end=5e5)
+    tune = {"elem_pipe_blocks": 64, "elem_exact": 1}
+    calls = [(1, 41), (42, 39)]
+    g0, _, _ = _run(m, calls, tune, 0)
+    stats = {}
+    for own in (1, 2):
+        g1, _, st = _run(m, calls, tune, own)
+        _same(g1, g0)
+        stats[own] = st
+    assert stats[2]["own_steps"] == 80, stats
