@@ -11,10 +11,13 @@ difference with element-order force assembly, prescribed BCs, hex8 B-bar + J2 re
 force + triaxiality + ductile-deletion check for every active element (and, for N > 1, the
 interface exchange). Inputs are resident in HBM before timing starts.
 
-Element arithmetic (`config.element_mode`): "exact" (default) is the reference-order kernel, whose
-trajectories equal the CPU restatement of the reference bit for bit (tests/test_gpu_exact.py); the
-line also carries `config.fused_mode`, the same workload timed in the same process with the fused
-single-pass kernel (rounding-level differences, the round-2 headline).
+Element arithmetic (`config.element_mode`): "fused" (default) is the single-pass kernel, which meets
+the north star's 1e-6 on the bench workload (tests/test_gpu_fullsize.py, C3 windows against the
+oracle) and drifts on the reference's chaotic contact decks only within those decks' own 1-ulp
+sensitivity (tools/oracle_conditioning.py, profiles/r03_oracle_conditioning.jsonl); "exact" is the
+reference-order kernel, whose trajectories equal the CPU restatement of the reference bit for bit
+(tests/test_gpu_exact.py). The line carries the other mode too (`config.other_mode`), timed on the
+same workload in the same process.
 
 Workloads (BASELINE.json):
   N = 1 (default)  C3, the 2 M-hex elastoplastic tensile bar 20x20x5000 (Tensile5e steel_Ductile,
@@ -65,10 +68,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--preload", type=int, default=-1, help="untimed steps before warm-up (-1: config default)")
     ap.add_argument("--layers", type=int, default=0, help="override z layers (tests / quick runs)")
-    ap.add_argument("--element-mode", choices=("exact", "fused"), default="exact",
-                    help="element arithmetic of the headline: reference order (bit-exact) or fused")
+    ap.add_argument("--element-mode", choices=("exact", "fused"), default="fused",
+                    help="element arithmetic of the headline: fused single pass, or reference order (bit-exact)")
     ap.add_argument("--compare-fused", type=int, default=1,
-                    help="also time the fused element kernel on the same workload (config.fused_mode)")
+                    help="also time the other element mode on the same workload (config.other_mode)")
     ap.add_argument("--strong", action="store_true", help="strong scaling: C5 16 M hex split over the ranks")
     ap.add_argument("--weak-shape", choices=("c3", "c5"), default="c3",
                     help="N > 1 weak scaling: a C3 bar per rank (default) or 2 M-hex slabs of the C5 bar")
@@ -353,7 +356,8 @@ def main():
                  "element_avg_ms": round(sum(x[0] for x in el2) / max(el2[0][1], 1) / len(g.svs), 4),
                  "what": ("fused single-pass element kernel (rounding-level differences from the reference order; "
                           "tests/test_gpu_decks.py bounds, tools/oracle_conditioning.py)" if exact else
-                          "reference-order element kernel (bit-exact)")}
+                          "reference-order element kernel: trajectories bit-identical to the CPU restatement "
+                          "of v2/HAKAI_j.jl (tests/test_gpu_exact.py)")}
 
     # per-kernel breakdown from a short extra pass after the timed regions (reported, not timed)
     k_tot = {}
@@ -468,12 +472,14 @@ def main():
         "config": dict(cfg, element_mode=a.element_mode,
                        element_mode_what=("reference-order element arithmetic: trajectories bit-identical to the "
                                           "CPU restatement of v2/HAKAI_j.jl (tests/test_gpu_exact.py)" if exact else
-                                          "fused single-pass element arithmetic (rounding-level differences)"),
+                                          "fused single-pass element arithmetic: <=1e-6 against the oracle on this "
+                                          "workload (tests/test_gpu_fullsize.py); on the reference's contact decks "
+                                          "within their own 1-ulp sensitivity (profiles/r03_oracle_conditioning.jsonl)"),
                        preload_steps=preload, plastic_gp_frac=round(plastic_frac, 4),
                        deleted_elements=int(n_deleted),
                        whole_step_roofline_frac=round(whole_bytes * a.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)
                        if nparts == 1 else None,
-                       kernel_ms_per_step=k_ms, fused_mode=other, **extra,
+                       kernel_ms_per_step=k_ms, other_mode=other, **extra,
                        assembly=("owner-computed node sums in LDS (own_assembly), element order" if own_steps
                                  else "fe round trip (element forces gathered by the nodal kernel)"),
                        parallelism=(f"dp{world}" if world > 1 else

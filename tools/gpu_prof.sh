@@ -20,7 +20,7 @@ if [ -n "$PROF" ]; then
 P=gpurun_out/prof
 rm -rf $P; mkdir -p $P
 KT=50; PS=10
-BA="--cpu-baseline 0 --breakdown 0 --compare-fused 0 --element-mode ${MODE:-exact}"
+BA="--cpu-baseline 0 --breakdown 0 --compare-fused 0 --element-mode ${MODE:-fused}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $P/kt -o run --output-format csv -- python bench.py --steps $KT --warmup 5 $BA > $P/kt_bench.log 2>&1
 rc=$?; echo "rocprof kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $P/calib_fetch -o run --output-format csv -- tools/_build/pmc_calib > $P/calib_fetch.log 2>&1
@@ -35,7 +35,7 @@ ALG=$(python -c "import json;print(json.loads([l for l in open('$P/kt_bench.log'
 ALGO=$(python -c "import json;print(json.loads([l for l in open('$P/kt_bench.log') if l.startswith('{')][-1])['roofline']['alg_bytes_per_launch_with_assembly_outputs'])")
 NEL=$(python -c "import json;print(json.loads([l for l in open('$P/kt_bench.log') if l.startswith('{')][-1])['config']['elements'])")
 python tools/pmc_report.py --calib-fetch $P/calib_fetch --calib-write $P/calib_write --fetch $P/fetch --write $P/write \
-  --kt $P/kt --pmc-steps $PS --kt-steps $KT --alg-bytes $ALG --alg-bytes-own $ALGO --element-mode ${MODE:-exact} \
+  --kt $P/kt --pmc-steps $PS --kt-steps $KT --alg-bytes $ALG --alg-bytes-own $ALGO --element-mode ${MODE:-fused} \
   --elements $NEL --out $P/element_pmc.json > $P/pmc_report.log 2>&1
 echo "pmc_report rc=$?"; cat $P/pmc_report.log
 if [ -n "$SQ" ]; then
