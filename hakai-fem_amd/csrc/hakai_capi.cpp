@@ -792,7 +792,7 @@ int hakai_download_state(hakai_ctx* c, hakai_state_t* st) {
 // each node's rows in element order. One 16-B entry per node segment piece (or exported
 // contribution) per super-batch of S = 2 schedule positions (1 when 2 would need more than 512
 // entries), one or two per thread (layout: hakai_kernels.hip own_pass). Slots are allocated per
-// block over the super-batches a sum is open; a schedule needing more than kOwnSlots open sums in
+// block over the super-batches a sum is open; a schedule needing more than own_slot_cap open sums in
 // one block, or a node with > 8 incidences, does not use the mode.
 //
 // Schedules (own_use picks the cheapest that fits):
@@ -879,33 +879,42 @@ static bool lattice_strides(const hakai_ctx* c, std::vector<int>& nx, std::vecto
 
 // Banded schedule: each batch goes to the band of its first element, (region, row / R); a band's
 // batches (ascending) are cut into runs, about G * (band batches) / nb of them per band.
+// Band height R per region: a band of R element rows keeps up to about R + 1 node rows of sums
+// open in its block -- the R - 1 interior rows of the node layer below, closing row by row while the
+// layer above opens, plus what a super-batch holds (measured with tools/own_plan_check: 1071 slots
+// at R = 4 on a 200-wide section, 1264 at R = 5) -- so R <= slots * 15/16 / (nx + 1) - 1. Within
+// that, the exported rows per node are about 6/R at band edges plus 4 G R / (layers * rows) at run
+// edges, least at R = sqrt(1.5 layers rows / G_region).
 static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& nx, const std::vector<int>& L,
                        int shrink, int epb, int slot_cap, OwnSched& sc) {
     const long long nb = c->nEp / epb, nE = c->nE;
     sc.epb = epb;
+    // regions: contiguous id ranges of equal strides
+    std::vector<long long> rstart{0};
+    for (long long x = 1; x < nE; ++x)
+        if (nx[x] != nx[x - 1] || L[x] != L[x - 1]) rstart.push_back(x);
+    rstart.push_back(nE);
+    std::vector<long long> Rreg(rstart.size() - 1);
+    for (size_t r = 0; r + 1 < rstart.size(); ++r) {
+        const long long e0 = rstart[r], ne = rstart[r + 1] - e0;
+        const long long rows = L[e0] / nx[e0], layers = std::max<long long>(1, ne / L[e0]);
+        const double Gr = std::max(1.0, (double)G * (double)ne / (double)nE);
+        const long long Rcap = (slot_cap - slot_cap / 16) / (nx[e0] + 1) - 1;
+        const long long Ropt = (long long)std::llround(std::sqrt(1.5 * (double)layers * (double)rows / Gr));
+        Rreg[r] = std::max<long long>(1, std::min(Rcap, std::max<long long>(Ropt, 1)) - shrink);
+    }
     std::vector<long long> key(nb);
-    long long base = 0;
     bool any_split = false;
-    long long region = 0, e_prev = -1;
+    size_t region = 0;
     for (long long b = 0; b < nb; ++b) {
         const long long e = std::min(epb * b, nE - 1);
-        // region starts: strides change (regions are contiguous id ranges)
-        for (long long x = e_prev + 1; x <= e; ++x)
-            if (x > 0 && (nx[x] != nx[x - 1] || L[x] != L[x - 1])) {
-                base = x;
-                ++region;
-            }
-        e_prev = e;
+        while (e >= rstart[region + 1]) ++region;
         const long long rows = L[e] / nx[e];
-        // a band of R element rows keeps up to about R + 1 node rows of sums open in its block: the
-        // R - 1 interior rows of the node layer below, closing row by row, while the layer above
-        // opens, plus what a super-batch holds (measured with tools/own_plan_check: 1071 slots at
-        // R = 4 on a 200-wide section, 1264 at R = 5)
-        long long R = std::max(1, (slot_cap - slot_cap / 16) / (nx[e] + 1) - 1 - shrink);
+        long long R = Rreg[region];
         if (R >= rows) R = rows;
         else any_split = true;
-        const long long row = ((e - base) % L[e]) / nx[e];
-        key[b] = (region << 32) | (row / R);
+        const long long row = ((e - rstart[region]) % L[e]) / nx[e];
+        key[b] = ((long long)region << 32) | (row / R);
     }
     if (!any_split) return false;  // one band per layer everywhere: the contiguous schedule
     std::vector<int> order(nb);
@@ -1102,8 +1111,8 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
             for (int q = 0; q < 7; ++q) lo |= (unsigned long long)en.lanes[q] << (9 * q);
             int* w = &list[4 * ((size_t)off[b] + i)];
             w[0] = en.target;
-            w[1] = (int)((unsigned)en.slot | (unsigned)en.flags << 10 | (unsigned)en.n << 14 |
-                         (unsigned)en.lanes[7] << 18);
+            w[1] = (int)(((unsigned)en.slot & 1023u) | (unsigned)en.flags << 10 | (unsigned)en.n << 14 |
+                         (unsigned)en.lanes[7] << 18 | ((unsigned)en.slot & 1024u) << 18);
             w[2] = (int)(unsigned)(lo & 0xffffffffu);
             w[3] = (int)(unsigned)(lo >> 32);
         }
@@ -1179,12 +1188,15 @@ static int own_materialize(hakai_ctx* c) {
 static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best) {
     const int epb = 32;
     const long long nb = c->nEp / epb;
-    const int cap = hk::kOwnSlots;
+    // slots per block: what two blocks per CU leave next to the kernel's own LDS (the wider
+    // passes of S = 2 leave less); row bands are sized for S = 2
+    auto cap_of = [&](int S) { return hk::own_slot_cap(c->elem_exact != 0, S, c->nmat); };
+    const int cap = cap_of(2);
     bool have = false;
     auto consider = [&](const OwnSched& sc) {
         for (int S : {2, 1}) {
             OwnPlan pl;
-            if (!own_plan(c, sc, S, cap, pl)) continue;
+            if (!own_plan(c, sc, S, cap_of(S), pl)) continue;
             if (!have || pl.cost() < best.cost()) {
                 best = std::move(pl);
                 best_sc = sc;

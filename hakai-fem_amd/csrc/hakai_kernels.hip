@@ -425,6 +425,8 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
 //     reference's eigvals agree to rounding; it only enters the deletion test and the output).
 // ---------------------------------------------------------------------------------------------
 constexpr int kXbStride = 74;  // doubles of LDS per element: exchange area [8 nodes][8 lanes] + one scalar row + pad
+static_assert(kEPB * kLdsStride * 8 == 12800 && kEPB * 24 * 8 * 2 == 12288 && kEPB * kXbStride * 8 + 192 * 8 == 20480,
+              "own_slot_cap (hakai_kernels.hpp) assumes these LDS sizes");
 
 // x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
 // q = RN(x*y) with y = RN(1/3), then one exact-remainder correction q + (x - 3q)*y. The exact
@@ -859,7 +861,8 @@ __device__ __forceinline__ int own_lane(int4 en, int j) {
 
 __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const double* s_fe, double* s_part) {
 #pragma clang fp contract(off)
-    const int slot = en.y & 1023, flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;  // (bit 27: kOwnRound2)
+    // slot: bits 0-9 and bit 28 (11 bits); bit 27: kOwnRound2
+    const int slot = (en.y & 1023) | ((en.y >> 18) & 1024), flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;
     double* dump = a.own_dump + 8 * (long long)blockIdx.x;
     double v[3];
     if (flags & (kOwnExp | kOwnNop)) {  // EXP: up to kOwnExpRows contributions -> rows target, target+1, ...
@@ -1081,7 +1084,8 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
     if (nb <= 0) return hipSuccess;
     if (a.own) {  // owner-computed assembly: persistent kernel only (own_build sized its lists for it)
         if (a.own > 2 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
-            !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 || a.own_slots > kOwnSlots)
+            !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 ||
+            a.own_slots > own_slot_cap(a.exact != 0, a.own, a.nmat))
             return hipErrorInvalidValue;
         if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;  // (own_bstart has grid+1 entries)
         if (a.exact)

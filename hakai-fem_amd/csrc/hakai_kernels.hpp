@@ -100,8 +100,17 @@ struct NodalArgs {
 };
 
 
-// LDS running-sum slots one block of the owner-assembly element kernel holds (24 KB; 2 blocks per CU)
-constexpr int kOwnSlots = 1024;
+// LDS running-sum slots one block of the owner-assembly element kernel may hold: what two blocks
+// per CU (80 KB each) leave next to the kernel's static arrays (node area 12.8 KB, force staging
+// 12 KB per batch of a pass, double-buffered, and in reference-order mode the exchange area and
+// the Pusai table, 20 KB; hakai_kernels.hip checks these sizes) and the staged materials; at most
+// 2048 (11-bit slot ids in the entry lists).
+constexpr int kOwnSlotsMax = 2048;
+inline int own_slot_cap(bool exact, int batches_per_pass, int nmat) {
+    const int stat = 12800 + 12288 * batches_per_pass + (exact ? 20480 : 0);
+    const int left = 81920 - 256 - stat - nmat * (int)sizeof(DevMat);
+    return left < 24 ? 0 : (left / 24 > kOwnSlotsMax ? kOwnSlotsMax : left / 24);
+}
 
 hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, hipStream_t s);
 hipError_t launch_negjac(const ElemArgs& a, unsigned long long* count, hipStream_t s);

@@ -19,15 +19,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tools", "_build", "own_plan_check")
 
 CASES = [
-    ("20 20 300", {"banded": 0, "epb": 32}),                        # C3's section, block units
-    ("20 20 300 --exact 1", {"banded": 0}),
+    ("20 20 300", {}),                                              # C3's section
+    ("20 20 300 --exact 1", {}),
     ("100 100 40 --G 32", {"banded": 1, "epb": 32}),              # C5's section: row bands
     ("100 100 40 --G 32 --exact 1", {"banded": 1}),
     ("200 200 5 --G 128 --schedule 2", {"banded": 1}),             # C4 plate's section
     ("30 30 12 --plate 120 120 3 --G 48 --schedule 2", {"banded": 1}),  # two lattices (C4's shape)
     ("40 30 8 --plate 60 50 4 --exact 1", {}),
     ("3 3 200 --G 8 --shuffle 11", {"banded": 0}),                  # shuffled numbering
-    ("40 40 6 --G 1", {"grid": 8}),                                 # too many open sums: 8x finer grid
+    ("60 60 6 --G 1", {"grid": 8}),                                 # too many open sums: 8x finer grid
     ("4 4 40 --G 3", {"grid": 3}),
     ("5 1 1 --G 1", {}),                                            # Tensile5e-sized: one batch
 ]

@@ -140,7 +140,8 @@ int main(int argc, char** argv) {
                 }
             for (int q = pl.off[p0]; q < pl.off[p0 + 1]; ++q) {
                 const int* w = &pl.list[4 * (size_t)q];
-                const int slot = w[1] & 1023, flags = (w[1] >> 10) & 15, n = (w[1] >> 14) & 15;
+                const int slot = (w[1] & 1023) | ((w[1] >> 18) & 1024), flags = (w[1] >> 10) & 15,
+                          n = (w[1] >> 14) & 15;
                 if (flags & kOwnExpH) {
                     for (int j = 0; j < n; ++j) rows[w[0] + j] = stage[lane_of(w, j)];
                     continue;
@@ -171,6 +172,6 @@ int main(int argc, char** argv) {
                 "\"superbatch\": %d, \"banded\": %d, \"rows\": %lld, \"entries\": %lld, \"slots\": %d, "
                 "\"slot_cap\": %d, \"round2\": %lld, \"mismatch\": %lld, \"double_fin\": %lld}\n",
                 ok ? "true" : "false", nE, nN, epb, Gp, S, sc.banded ? 1 : 0, pl.rows, pl.ne, pl.max_slots,
-                hk::kOwnSlots, pl.round2, mismatch, bad);
+                hk::own_slot_cap(exact != 0, S, 1), pl.round2, mismatch, bad);
     return ok ? 0 : 1;
 }
