@@ -83,7 +83,7 @@ def test_own_shuffled_numbering_bitexact():
 def test_own_wide_section_finer_grid_or_fallback():
     """A 40x40 cross-section on 1 block: too many open sums, so the lists are built for 8 blocks
     (blocks then run in waves) -- or the fe path; either way bit-identical. A shuffled wide mesh
-    cannot fit at all."""
+    fits in one block's slots or takes the fe path."""
     m = small_bar(40, 40, 6, n_steps=200, v_end=5e5)
     tune = {**PIPE, "elem_pipe_blocks": 1}
     g0, _, _ = _run(m, [(1, 200)], tune, 0)
@@ -93,7 +93,8 @@ def test_own_wide_section_finer_grid_or_fallback():
     ms = _shuffled(m, seed=3)
     g0, _, _ = _run(ms, [(1, 60)], tune, 0)
     g1, _, s1 = _run(ms, [(1, 60)], tune, 1)
-    assert s1["own_steps"] == 0 and s1["own_rows"] == -1
+    # (since round 3 a block holds up to 2048 sums, what its LDS allows, so this mesh may fit)
+    assert s1["own_steps"] == 60 or (s1["own_steps"] == 0 and s1["own_rows"] == -1), s1
     _same(g1, g0)
 
 
