@@ -818,9 +818,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Owner-computed assembly (ElemArgs::own). The block sums node forces per SUPER-BATCH of OS
 // consecutive batches of its range (the last one may be shorter), one 16-B entry per thread:
-//   x = target (node for ACC entries, row for EXP), y = slot | flags << 10 | n << 14 | lane7 << 18,
-//   z | w << 32 = lanes 0-6, 9 bits each; a lane is (element - 32 * super-batch's first batch) * 8
-//   + local node, in ascending element order.
+//   x = target (node for ACC entries, row for EXP), y = slot bits 0-9 | flags << 10 | n << 14 |
+//   lane7 << 18 | kOwnRound2 (bit 27, set in the kernel) | slot bit 10 << 28,
+//   z | w << 32 = lanes 0-6, 9 bits each; a lane is ((schedule position of the element's batch -
+//   the super-batch's first position) * 32 + element % 32) * 8 + local node, in ascending element
+//   order.
 // An ACC entry continues node `target`'s running sum in LDS slot `slot` (INIT: from 0.0, the nodal
 // gather's own start) with the super-batch's contributions in element order; FIN stores the sum to
 // own_q (the node's Q, or its prefix partial when later blocks hold more incidences); EXP copies one
@@ -828,10 +830,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
 // unconditionally (unused ones to a per-block dump line, which a wave's lanes share) so the loads of
 // the pipeline stay in flight across the pass. The force staging is double-buffered by super-batch, so one barrier per super-batch suffices.
 // ---------------------------------------------------------------------------------------------
-// LDS running sums per block: at most 1024 (24 KB), sized per launch to what the lists use
-// (ElemArgs::own_slots, dynamic LDS next to the staged materials)
+// LDS running sums per block: what two blocks per CU leave (own_slot_cap, up to 2048), sized per
+// launch to what the lists use (ElemArgs::own_slots, dynamic LDS next to the staged materials)
 // batches per super-batch: 2, or 1 for meshes whose 64-element super-batches need more than 512
-// entries; the host picks (own_build), the kernel is instantiated for both
+// entries; the host picks (own_choose), the kernel is instantiated for both
 constexpr int kOwnExpRows = 4;            // contributions of one node per EXP entry
 enum { kOwnInit = 1, kOwnFin = 2, kOwnExp = 4, kOwnNop = 8 };
 
