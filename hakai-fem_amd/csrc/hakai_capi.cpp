@@ -816,10 +816,12 @@ struct OwnSched {
 
 struct OwnPlan {
     int S = 2;
+    int W = 1;  // lists per pass: 1, or 4 = one per wave (lagged passes: a slot belongs to wave slot & 3)
     std::vector<int> off, list, rp, ridx;
+    std::vector<int> wave_counts;  // W > 1: entries per (pass, wave)
     long long rows = 0, ne = 0;
     int max_slots = 1;
-    long long round2 = 0;  // summing passes with more than one entry per thread
+    long long round2 = 0;  // summing passes with more than one entry per thread (W = 4: in some wave)
     // per-step bytes the lists add beyond the element/nodal kernels' own (entries read, rows
     // written and read back, row indices): what own_use compares between schedules
     double cost() const { return 16.0 * (double)ne + 52.0 * (double)rows; }
@@ -967,12 +969,14 @@ static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& 
     return true;
 }
 
-static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap, OwnPlan& pl) {
+static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap, OwnPlan& pl, int W = 1) {
     const int epb = sc.epb, bs = 8 * epb;  // elements per batch, threads per block
     const long long nb = c->nEp / epb, nN = c->nN;
     const long long G = (long long)sc.bstart.size() - 1;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
+    if (W != 1 && (W != bs / 64 || S != 1)) return false;
     pl.S = S;
+    pl.W = W;
     struct Ent { int target, slot, flags, n; int lanes[8]; };
     // pos_of[b]: schedule position of batch b; block_of[b]; sb_pos[b] = position of the first batch
     // of b's super-batch (runs of S positions from each block's first), which indexes the lists
@@ -1094,14 +1098,45 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
             std::push_heap(busy.begin(), busy.end(), cmp);
         }
     }
+    if (W > 1) {
+        // one list per wave: a running sum's entries go to the wave its slot belongs to, so a slot is
+        // only ever touched by one wave, in program order; exported rows fill the least loaded wave
+        for (long long b = 0; b < nb; ++b) {
+            std::vector<std::vector<Ent>> bw(W);
+            for (const Ent& en : per[b])
+                if (!(en.flags & kOwnExpH)) bw[en.slot & (W - 1)].push_back(en);
+            for (const Ent& en : per[b])
+                if (en.flags & kOwnExpH) {
+                    int w = 0;
+                    for (int k = 1; k < W; ++k) w = bw[k].size() < bw[w].size() ? k : w;
+                    bw[w].push_back(en);
+                }
+            std::vector<Ent> cat;
+            for (int w = 0; w < W; ++w) {
+                pl.wave_counts.push_back((int)bw[w].size());
+                cat.insert(cat.end(), bw[w].begin(), bw[w].end());
+            }
+            per[b].swap(cat);
+        }
+    }
     std::vector<int>& off = pl.off;
-    off.assign(nb + 1, 0);
+    off.assign(W * nb + 1, 0);
     for (long long b = 0; b < nb; ++b) {
         if (per[b].size() > 2 * (size_t)bs) return false;  // two entries per thread at most (own_pass)
-        pl.round2 += per[b].size() > (size_t)bs ? 1 : 0;
-        off[b + 1] = off[b] + (int)per[b].size();
+        if (W == 1) {
+            pl.round2 += per[b].size() > (size_t)bs ? 1 : 0;
+            off[b + 1] = off[b] + (int)per[b].size();
+            continue;
+        }
+        bool r2 = false;
+        for (int w = 0; w < W; ++w) {
+            const int cnt = pl.wave_counts[(size_t)b * W + w];
+            r2 = r2 || cnt > 64;
+            off[b * W + w + 1] = off[b * W + w] + cnt;
+        }
+        pl.round2 += r2 ? 1 : 0;
     }
-    const long long ne = off[nb];
+    const long long ne = off[W * nb];
     std::vector<int>& list = pl.list;
     list.assign(4 * (size_t)(ne + 1), 0);
     for (long long b = 0; b < nb; ++b)
@@ -1109,7 +1144,7 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
             const Ent& en = per[b][i];
             unsigned long long lo = 0;
             for (int q = 0; q < 7; ++q) lo |= (unsigned long long)en.lanes[q] << (9 * q);
-            int* w = &list[4 * ((size_t)off[b] + i)];
+            int* w = &list[4 * ((size_t)off[W * b] + i)];
             w[0] = en.target;
             w[1] = (int)(((unsigned)en.slot & 1023u) | (unsigned)en.flags << 10 | (unsigned)en.n << 14 |
                          (unsigned)en.lanes[7] << 18 | ((unsigned)en.slot & 1024u) << 18);
@@ -1150,6 +1185,7 @@ static bool own_upload(hakai_ctx* c, const OwnSched& sc, const OwnPlan& pl) {
     c->own_entries = pl.ne;
     c->own_built_g = G;
     c->own_s = pl.S;
+    c->own_w = pl.W;
     c->own_round2 = pl.round2;
     c->own_banded = sc.banded ? 1 : 0;
     return true;
@@ -1184,19 +1220,22 @@ static int own_materialize(hakai_ctx* c) {
 // banded at about G0 blocks (when the mesh has a structured wide section), and, if neither fits,
 // contiguous at 8 G0 (finer ranges keep fewer sums open; the blocks run in waves). Super-batches
 // of 2 batches where they fit 512 entries, else 1. Tuning own_schedule: 0 auto, 1 contiguous only,
-// 2 banded only (tests).
+// 2 banded only (tests). Lagged passes (own_lag) run one batch per pass from a ring of three
+// force buffers: plans of S = 1 at that LDS budget.
 static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best) {
     const int epb = 32;
     const long long nb = c->nEp / epb;
     // slots per block: what two blocks per CU leave next to the kernel's own LDS (the wider
     // passes of S = 2 leave less); row bands are sized for S = 2
-    auto cap_of = [&](int S) { return hk::own_slot_cap(c->elem_exact != 0, S, c->nmat); };
-    const int cap = cap_of(2);
+    const bool lag = c->own_lag != 0;
+    auto cap_of = [&](int S) { return hk::own_slot_cap(c->elem_exact != 0, S, c->nmat, lag); };
+    const int cap = cap_of(lag ? 1 : 2);
     bool have = false;
     auto consider = [&](const OwnSched& sc) {
         for (int S : {2, 1}) {
+            if (lag && S == 2) continue;
             OwnPlan pl;
-            if (!own_plan(c, sc, S, cap_of(S), pl)) continue;
+            if (!own_plan(c, sc, S, cap_of(S), pl, lag ? 4 : 1 /* waves of a 256-thread block */)) continue;
             if (!have || pl.cost() < best.cost()) {
                 best = std::move(pl);
                 best_sc = sc;
@@ -1242,7 +1281,8 @@ static bool own_use(hakai_ctx* c) {
     // faster for this kernel (C5 slab 1.12 against 1.41 ms per step, C4 2.46 against 3.25,
     // profiles/r03_wave_units_sweep.log). own_assembly 2 uses the owner sums anyway (tests); a
     // multi-GPU rank whose owner sums are live keeps them (its interface fix needs the rows).
-    if (ok && c->elem_exact && c->own_round2 > 0 && c->own_assembly == 1 && !(c->comm && c->own_valid)) return false;
+    if (ok && c->elem_exact && c->own_round2 > 0 && !c->own_lag && c->own_assembly == 1 && !(c->comm && c->own_valid))
+        return false;
     return ok;
 }
 
@@ -1340,7 +1380,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
     if (own) {
-        ea.own = c->own_s;
+        ea.own = c->own_w > 1 ? 3 : c->own_s;  // wave lists are built for lagged passes only
         ea.own_grid = (int)c->own_built_g;
         ea.own_seq = c->d_own_seq;
         ea.own_bstart = c->d_own_bstart;
@@ -1562,6 +1602,7 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     else if (!std::strcmp(key, "own_slots")) *value = c->own_built_g > 0 ? c->own_slots : 0;
     else if (!std::strcmp(key, "own_banded")) *value = c->own_built_g > 0 ? c->own_banded : 0;
     else if (!std::strcmp(key, "own_grid")) *value = c->own_built_g > 0 ? c->own_built_g : 0;
+    else if (!std::strcmp(key, "own_lag")) *value = c->own_lag;
     else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1643,6 +1684,12 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_schedule must be 0, 1 or 2");
         if (c->own_schedule != (int)value) c->own_for_g0 = -1;  // re-planned before the next step
         c->own_schedule = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "own_lag")) {  // owner passes: 0 behind a block barrier, 1 lagged, barrier-free
+        if (value < 0 || value > 1) return fail(HAKAI_ERR_ARG, "own_lag must be 0 or 1");
+        if (c->own_lag != (int)value) c->own_for_g0 = -1;  // re-planned (S = 1, another slot budget)
+        c->own_lag = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "graph")) {

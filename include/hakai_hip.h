@@ -187,6 +187,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       2: the owner sums wherever they fit;
  *   "own_schedule"      its block schedule: 0 (default) the cheapest that fits, 1 contiguous batch
  *                       ranges only, 2 row bands of structured wide sections only;
+ *   "own_lag"           its summing passes: 0 (default) behind a block barrier, 1 one batch per pass,
+ *                       run by each wave one batch late and ordered by LDS counters (no barrier);
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);

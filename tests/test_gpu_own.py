@@ -266,3 +266,26 @@ def test_own_reference_order_mode_bitexact(shape):
         _same(g1, g0)
         stats[own] = st
     assert stats[2]["own_steps"] == 80, stats
+
+
+@pytest.mark.parametrize("exact", [0, 1])
+@pytest.mark.parametrize("case", ["deleting_bar", "wide"])
+def test_own_lagged_passes_bitexact(case, exact):
+    """Lagged, barrier-free owner passes (own_lag 1: waves run their part of batch i's pass after
+    staging batch i + 1, synchronised by LDS counters): bit-identical to the fe path, in both element
+    modes, on a deleting bar over 16 blocks (odd step counts, graphs on) and on a wide section whose
+    passes need second entries."""
+    if case == "deleting_bar":
+        m = fast_deletion_bar(4, 4, 400)
+        calls = [(1, 301), (302, 699)]
+        tune = {**PIPE, "elem_pipe_blocks": 16, "elem_exact": exact}
+    else:
+        m = small_bar(100, 100, 12, n_steps=80, v_end=5e5)
+        calls = [(1, 41), (42, 39)]
+        tune = {"elem_pipe_blocks": 64, "elem_exact": exact}
+    n = sum(c[1] for c in calls)
+    g0, d0, _ = _run(m, calls, tune, 0)
+    g1, d1, st = _run(m, calls, {**tune, "own_lag": 1}, 2)
+    assert st["own_steps"] == n, st
+    assert d1 == d0
+    _same(g1, g0)
