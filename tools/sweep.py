@@ -66,7 +66,7 @@ for r in range(a.rounds):
         dt = time.perf_counter() - t0
         t += a.steps
         res[name]["step"].append(dt / a.steps * 1e3)
-        res[name]["own"] = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_entries", "own_banded", "own_grid", "own_round2")}
+        res[name]["own"] = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_entries", "own_banded", "own_grid", "own_round2", "own_superbatch", "own_slots")}
 for name, d in res.items():
     print(f"{name:10s} element {statistics.median(d['el']):.4f} ms/step (min {min(d['el']):.4f})  "
           f"nodal {statistics.median(d['nd']):.4f} ms/step  step {statistics.median(d['step']):.4f} ms (unprofiled wall)  "
