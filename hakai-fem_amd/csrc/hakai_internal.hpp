@@ -23,7 +23,8 @@ struct EventPair {
 
 // BCs fused into k_nodal up to this many nodes: the per-node lookup (4 B/node, one dependent load)
 // costs more than the k_bc launch it saves on large meshes (C3: nodal 0.165 -> 0.180 ms, measured
-// profiles/r02_assembly_bound_sweep.log), and wins on launch-bound small decks.
+// profiles/r02_assembly_bound_sweep.log), and wins on launch-bound small decks. With owner-computed
+// assembly it neither wins nor loses on C3 / the C5 slab (profiles/r03_fuse_bc_sweep.log).
 constexpr long long kFuseBcMaxNodes = 1 << 18;
 
 struct hakai_ctx {
