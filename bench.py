@@ -89,7 +89,78 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: take the N>1 path (C5 slab, RCCL communicator) even with one rank")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="--gpus N > 1 outside torch.distributed.run: print the N rank environments the "
+                         "launcher would start (one JSON line each) and exit, touching no GPU")
     return ap.parse_args()
+
+
+LAUNCH_KEYS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int) -> list[dict]:
+    """The environment of each of the n rank processes: rank r drives device r (hakai.dist.rank_device),
+    rendezvous on 127.0.0.1 like torch.distributed.run --nnodes=1 --master-addr 127.0.0.1."""
+    return [{"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+             "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)} for r in range(n)]
+
+
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` (N > 1) without a launcher: start N rank processes, one per GPU, and
+    wait for them. This process never touches HIP (it does not even import torch), so it may start
+    children; rank 0 prints the JSON line. Any rank failing ends the others and the launch fails with
+    that rank's status: a run never falls back to fewer ranks."""
+    import signal
+    import subprocess
+    envs = rank_envs(a.gpus, free_port())
+    if a.launch_dry_run:
+        for e in envs:
+            print(json.dumps(e), flush=True)
+        return 0
+    argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = [subprocess.Popen(argv, env=dict(os.environ, **e)) for e in envs]
+    status = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"bench.py launcher: rank pid {p.pid} exited with {rc}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in procs:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for q in procs:          # only reached on an exception in this loop: never leave ranks behind
+            q.kill()
+            q.wait()
+    return status
+
+
+def check_launch(a, world: int, local_world: int) -> None:
+    """Rank count and devices must be what --gpus asks for; every mismatch is fatal (never one rank
+    timed silently)."""
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
+    if world > 1 and os.environ.get("HAKAI_RCCL_SHARED_GPU") != "1":
+        import torch
+        n = torch.cuda.device_count()      # counts devices without initialising the GPU
+        restricted = any(os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                     "CUDA_VISIBLE_DEVICES"))
+        if n < 1 or (n < local_world and not restricted):
+            raise SystemExit(f"bench.py: {local_world} ranks on this node but {n} visible GPU(s); ranks would share "
+                             "a device (set HAKAI_RCCL_SHARED_GPU=1 only for a one-GPU rehearsal)")
 
 
 def c5_strong_model(rank, world, layers_override=0):
@@ -280,12 +351,14 @@ def active_elements(g):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    if a.launch_dry_run:
+        raise SystemExit("bench.py: --launch-dry-run needs --gpus N > 1 outside torch.distributed.run")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    check_launch(a, world, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     import torch
     import torch.distributed as dist
     from hakai._abi import K_ELEMENT, K_EXCHANGE, K_NODAL, K_BC

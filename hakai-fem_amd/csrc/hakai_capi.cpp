@@ -408,6 +408,10 @@ int hakai_upload_model(hakai_ctx* c, int64_t nNode, const double* coordmat, int6
     if (192 * (nElement + 32) >= (int64_t)1 << 32)
         return fail(HAKAI_ERR_ARG, "upload_model: %lld elements exceed one context's 32-bit element-kernel offsets "
                     "(max %lld); split the mesh over ranks", (long long)nElement, (long long)(((int64_t)1 << 32) / 192 - 32));
+    // (node gathers: 24 B per node, load_node / load_node_raw form 24u * n)
+    if (24 * (nNode + 1) >= (int64_t)1 << 32)
+        return fail(HAKAI_ERR_ARG, "upload_model: %lld nodes exceed one context's 32-bit element-kernel offsets "
+                    "(max %lld); split the mesh over ranks", (long long)nNode, (long long)(((int64_t)1 << 32) / 24 - 1));
     HIPCHK(hipSetDevice(c->device));
     (void)hipStreamSynchronize(c->stream);
     hkc::free_model(c);
@@ -621,12 +625,27 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     return 0;
 }
 
+static int own_materialize(hakai_ctx* c);
+
 int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     if (c) hkc::graph_invalidate(c);  // captured steps may hold stale buffers or settings
-    if (c) c->own_valid = false;  // the next nodal update gathers fe (or the uploaded Q)
     if (!c || !st) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok) return fail(HAKAI_ERR_STATE, "upload_state before upload_model");
     HIPCHK(hipSetDevice(c->device));
+    // The next nodal update gathers fe unless the upload brings Q or Qe. After a call whose last
+    // steps a contact overflow skipped, owner-computed assembly left the last element step's forces
+    // only as node sums (fe is an earlier step's): they become the uploaded Q, the same bits, and an
+    // upload that also deletes elements (whose fe rows it would zero) must bring Q or Qe itself.
+    if (c->own_valid && !c->fe_ok && !st->Q && !st->Qe) {
+        bool dels = false;
+        for (long long e = 0; st->element_flag && e < c->nE && !dels; ++e) dels = st->element_flag[e] == 0;
+        if (dels || c->comm)
+            return fail(HAKAI_ERR_STATE, "upload_state: the last element step's forces exist only as owner-computed "
+                        "node sums (a contact overflow skipped the call's last step); upload Q (from "
+                        "hakai_download_state) or Qe with this state");
+        if (int r = own_materialize(c)) return r;
+    }
+    c->own_valid = false;
     hipStream_t s = c->stream;
     const size_t fn = 3 * (size_t)c->nN, nGP = 8 * (size_t)c->nE;
     if (st->disp) HIPCHK(hipMemcpyAsync(c->d_u[c->cur], st->disp, fn * sizeof(double), hipMemcpyHostToDevice, s));
@@ -816,12 +835,10 @@ struct OwnSched {
 
 struct OwnPlan {
     int S = 2;
-    int W = 1;  // lists per pass: 1, or 4 = one per wave (lagged passes: a slot belongs to wave slot & 3)
     std::vector<int> off, list, rp, ridx;
-    std::vector<int> wave_counts;  // W > 1: entries per (pass, wave)
     long long rows = 0, ne = 0;
     int max_slots = 1;
-    long long round2 = 0;  // summing passes with more than one entry per thread (W = 4: in some wave)
+    long long round2 = 0;  // summing passes with more than one entry per thread
     // per-step bytes the lists add beyond the element/nodal kernels' own (entries read, rows
     // written and read back, row indices): what own_use compares between schedules
     double cost() const { return 16.0 * (double)ne + 52.0 * (double)rows; }
@@ -969,14 +986,12 @@ static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& 
     return true;
 }
 
-static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap, OwnPlan& pl, int W = 1) {
+static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap, OwnPlan& pl) {
     const int epb = sc.epb, bs = 8 * epb;  // elements per batch, threads per block
     const long long nb = c->nEp / epb, nN = c->nN;
     const long long G = (long long)sc.bstart.size() - 1;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
-    if (W != 1 && (W != bs / 64 || S != 1)) return false;
     pl.S = S;
-    pl.W = W;
     struct Ent { int target, slot, flags, n; int lanes[8]; };
     // pos_of[b]: schedule position of batch b; block_of[b]; sb_pos[b] = position of the first batch
     // of b's super-batch (runs of S positions from each block's first), which indexes the lists
@@ -1098,45 +1113,14 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
             std::push_heap(busy.begin(), busy.end(), cmp);
         }
     }
-    if (W > 1) {
-        // one list per wave: a running sum's entries go to the wave its slot belongs to, so a slot is
-        // only ever touched by one wave, in program order; exported rows fill the least loaded wave
-        for (long long b = 0; b < nb; ++b) {
-            std::vector<std::vector<Ent>> bw(W);
-            for (const Ent& en : per[b])
-                if (!(en.flags & kOwnExpH)) bw[en.slot & (W - 1)].push_back(en);
-            for (const Ent& en : per[b])
-                if (en.flags & kOwnExpH) {
-                    int w = 0;
-                    for (int k = 1; k < W; ++k) w = bw[k].size() < bw[w].size() ? k : w;
-                    bw[w].push_back(en);
-                }
-            std::vector<Ent> cat;
-            for (int w = 0; w < W; ++w) {
-                pl.wave_counts.push_back((int)bw[w].size());
-                cat.insert(cat.end(), bw[w].begin(), bw[w].end());
-            }
-            per[b].swap(cat);
-        }
-    }
     std::vector<int>& off = pl.off;
-    off.assign(W * nb + 1, 0);
+    off.assign(nb + 1, 0);
     for (long long b = 0; b < nb; ++b) {
         if (per[b].size() > 2 * (size_t)bs) return false;  // two entries per thread at most (own_pass)
-        if (W == 1) {
-            pl.round2 += per[b].size() > (size_t)bs ? 1 : 0;
-            off[b + 1] = off[b] + (int)per[b].size();
-            continue;
-        }
-        bool r2 = false;
-        for (int w = 0; w < W; ++w) {
-            const int cnt = pl.wave_counts[(size_t)b * W + w];
-            r2 = r2 || cnt > 64;
-            off[b * W + w + 1] = off[b * W + w] + cnt;
-        }
-        pl.round2 += r2 ? 1 : 0;
+        pl.round2 += per[b].size() > (size_t)bs ? 1 : 0;
+        off[b + 1] = off[b] + (int)per[b].size();
     }
-    const long long ne = off[W * nb];
+    const long long ne = off[nb];
     std::vector<int>& list = pl.list;
     list.assign(4 * (size_t)(ne + 1), 0);
     for (long long b = 0; b < nb; ++b)
@@ -1144,7 +1128,7 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
             const Ent& en = per[b][i];
             unsigned long long lo = 0;
             for (int q = 0; q < 7; ++q) lo |= (unsigned long long)en.lanes[q] << (9 * q);
-            int* w = &list[4 * ((size_t)off[W * b] + i)];
+            int* w = &list[4 * ((size_t)off[b] + i)];
             w[0] = en.target;
             w[1] = (int)(((unsigned)en.slot & 1023u) | (unsigned)en.flags << 10 | (unsigned)en.n << 14 |
                          (unsigned)en.lanes[7] << 18 | ((unsigned)en.slot & 1024u) << 18);
@@ -1185,7 +1169,6 @@ static bool own_upload(hakai_ctx* c, const OwnSched& sc, const OwnPlan& pl) {
     c->own_entries = pl.ne;
     c->own_built_g = G;
     c->own_s = pl.S;
-    c->own_w = pl.W;
     c->own_round2 = pl.round2;
     c->own_banded = sc.banded ? 1 : 0;
     return true;
@@ -1219,23 +1202,20 @@ static int own_materialize(hakai_ctx* c) {
 // Candidate schedules, cheapest plan wins (OwnPlan::cost): contiguous at the persistent grid G0,
 // banded at about G0 blocks (when the mesh has a structured wide section), and, if neither fits,
 // contiguous at 8 G0 (finer ranges keep fewer sums open; the blocks run in waves). Super-batches
-// of 2 batches where they fit 512 entries, else 1. Tuning own_schedule: 0 auto, 1 contiguous only,
-// 2 banded only (tests). Lagged passes (own_lag) run one batch per pass from a ring of three
-// force buffers: plans of S = 1 at that LDS budget.
-static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best) {
+// of 2 batches where they fit 512 entries, else 1. `only` (the CPU replay harness,
+// tools/own_plan_check.cpp): 0 every schedule, 1 contiguous only, 2 banded only.
+static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& best, int only = 0) {
     const int epb = 32;
     const long long nb = c->nEp / epb;
     // slots per block: what two blocks per CU leave next to the kernel's own LDS (the wider
     // passes of S = 2 leave less); row bands are sized for S = 2
-    const bool lag = c->own_lag != 0;
-    auto cap_of = [&](int S) { return hk::own_slot_cap(c->elem_exact != 0, S, c->nmat, lag); };
-    const int cap = cap_of(lag ? 1 : 2);
+    auto cap_of = [&](int S) { return hk::own_slot_cap(c->elem_exact != 0, S, c->nmat); };
+    const int cap = cap_of(2);
     bool have = false;
     auto consider = [&](const OwnSched& sc) {
         for (int S : {2, 1}) {
-            if (lag && S == 2) continue;
             OwnPlan pl;
-            if (!own_plan(c, sc, S, cap_of(S), pl, lag ? 4 : 1 /* waves of a 256-thread block */)) continue;
+            if (!own_plan(c, sc, S, cap_of(S), pl)) continue;
             if (!have || pl.cost() < best.cost()) {
                 best = std::move(pl);
                 best_sc = sc;
@@ -1245,8 +1225,8 @@ static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& b
         }
         return false;
     };
-    if (c->own_schedule != 2) consider(own_contiguous(nb, G0, epb));
-    if (c->own_schedule != 1) {
+    if (only != 2) consider(own_contiguous(nb, G0, epb));
+    if (only != 1) {
         std::vector<int> nx, L;
         if (lattice_strides(c, nx, L)) {
             OwnSched sc;
@@ -1254,7 +1234,7 @@ static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& b
                 if (own_banded(c, G0, nx, L, shrink, epb, cap, sc) && consider(sc)) break;
         }
     }
-    if (!have && c->own_schedule != 2 && 8 * G0 <= nb) consider(own_contiguous(nb, 8 * G0, epb));
+    if (!have && only != 2 && 8 * G0 <= nb) consider(own_contiguous(nb, 8 * G0, epb));
     return have;
 }
 
@@ -1281,7 +1261,7 @@ static bool own_use(hakai_ctx* c) {
     // faster for this kernel (C5 slab 1.12 against 1.41 ms per step, C4 2.46 against 3.25,
     // profiles/r03_wave_units_sweep.log). own_assembly 2 uses the owner sums anyway (tests); a
     // multi-GPU rank whose owner sums are live keeps them (its interface fix needs the rows).
-    if (ok && c->elem_exact && c->own_round2 > 0 && !c->own_lag && c->own_assembly == 1 && !(c->comm && c->own_valid))
+    if (ok && c->elem_exact && c->own_round2 > 0 && c->own_assembly == 1 && !(c->comm && c->own_valid))
         return false;
     return ok;
 }
@@ -1380,7 +1360,7 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
     hk::ElemArgs ea = elem_args(c);
     ea.step_i = (int)t;
     if (own) {
-        ea.own = c->own_w > 1 ? 3 : c->own_s;  // wave lists are built for lagged passes only
+        ea.own = c->own_s;
         ea.own_grid = (int)c->own_built_g;
         ea.own_seq = c->d_own_seq;
         ea.own_bstart = c->d_own_bstart;
@@ -1476,11 +1456,28 @@ static int step_graph(hakai_ctx* c, double t, double d_time, int len) {
     return 0;
 }
 
+// The host's view of a context before a stepping call's first step (after any owner-assembly
+// re-plan, which hands the last sums over unchanged): what an overflow on that step rolls back to.
+struct CallSnap {
+    int cur = 0;
+    long long done = 0;
+    bool fe_ok = true, triax_ok = true, own_valid = false, q_from_buf = false;
+};
+static CallSnap call_snap(const hakai_ctx* c) {
+    CallSnap s;
+    s.cur = c->cur;
+    s.done = c->steps_done;
+    s.fe_ok = c->fe_ok;
+    s.triax_ok = c->triax_ok;
+    s.own_valid = c->own_valid;
+    s.q_from_buf = c->q_from_buf;
+    return s;
+}
+
 // End of a stepping call: the contact overflow check. An overflow poisoned step p: the device's
 // state-writing kernels of steps p.. were no-ops, so the device holds the state after step p-1;
 // bring the host's view back to that step.
-static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, long long done0, bool fe_ok0,
-                       bool triax_ok0) {
+static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const CallSnap& s0) {
     const int rc = hkc::contact_check(c);
     if (rc && c->contact) {
         int pz[2] = {0, 0};
@@ -1488,11 +1485,17 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, int cur0, 
         if (pz[0]) {
             const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
             if (good >= 0 && good <= n_steps) {
-                c->cur = (good & 1) ? 1 - cur0 : cur0;
-                c->steps_done = done0 + good;
-                // the call's last step (the one that stores fe and triax) did not run
-                c->fe_ok = good == 0 ? fe_ok0 : !c->own_valid;
-                c->triax_ok = good == 0 ? triax_ok0 : false;
+                c->cur = (good & 1) ? 1 - s0.cur : s0.cur;
+                c->steps_done = s0.done + good;
+                if (good == 0) {  // nothing of the call ran: where the Q of the next nodal update is
+                    c->fe_ok = s0.fe_ok;
+                    c->triax_ok = s0.triax_ok;
+                    c->own_valid = s0.own_valid;
+                    c->q_from_buf = s0.q_from_buf;
+                } else {  // the call's last step (the one that stores fe and triax) did not run
+                    c->fe_ok = !c->own_valid;
+                    c->triax_ok = false;
+                }
             }
             hkc::graph_invalidate(c);
             hkc::contact_after_overflow(c, c->steps_done);
@@ -1516,9 +1519,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
                     "step -- raise the capacity and hakai_upload_state / hakai_reset_state on every rank");
     HIPCHK(hipSetDevice(c->device));
     (void)own_use(c);  // owner-assembly lists are built here, never inside a graph capture
-    const int cur0 = c->cur;
-    const long long done0 = c->steps_done;
-    const bool fe_ok0 = c->fe_ok, triax_ok0 = c->triax_ok;
+    const CallSnap s0 = call_snap(c);
     int64_t it = 0;
     while (it < n_steps) {
         const double t = t_first + (double)it;
@@ -1537,16 +1538,14 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
         }
         if (rc) return rc;
     }
-    return finish_call(c, t_first, n_steps, cur0, done0, fe_ok0, triax_ok0);
+    return finish_call(c, t_first, n_steps, s0);
 }
 
 int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
     if (!ctxs || n <= 0) return fail(HAKAI_ERR_ARG, "step_group: no contexts");
     if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step_group: n_steps=%lld d_time=%g",
                                                   (long long)n_steps, d_time);
-    std::vector<int> cur0(n);
-    std::vector<long long> done0(n);
-    std::vector<char> fe0(n), tx0(n);
+    std::vector<CallSnap> s0(n);
     for (int r = 0; r < n; ++r) {
         hakai_ctx* c = ctxs[r];
         if (!c) return fail(HAKAI_ERR_ARG, "step_group: null context %d", r);
@@ -1557,13 +1556,13 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
         if (n > 1 && (!c->comm || hkc::comm_rank(c) != r || hkc::comm_size(c) != n ||
                       hkc::comm_peer_ctx(c, r) != c))
             return fail(HAKAI_ERR_ARG, "step_group: context %d is not rank %d of an in-process group of %d", r, r, n);
-        cur0[r] = c->cur;
-        done0[r] = c->steps_done;
-        fe0[r] = c->fe_ok;
-        tx0[r] = c->triax_ok;
         hkc::graph_invalidate(c);
     }
     HIPCHK(hipSetDevice(ctxs[0]->device));
+    for (int r = 0; r < n; ++r) {
+        (void)own_use(ctxs[r]);  // (re-plans here, as hakai_step does, not inside the first step)
+        s0[r] = call_snap(ctxs[r]);
+    }
     for (int64_t it = 0; it < n_steps; ++it) {
         const double t = t_first + (double)it;
         const bool last = it == n_steps - 1;
@@ -1579,7 +1578,7 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
     }
     int first = 0;
     for (int r = 0; r < n; ++r) {
-        const int rc = finish_call(ctxs[r], t_first, n_steps, cur0[r], done0[r], fe0[r], tx0[r]);
+        const int rc = finish_call(ctxs[r], t_first, n_steps, s0[r]);
         if (rc && !first) first = rc;
     }
     return first;
@@ -1602,7 +1601,6 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     else if (!std::strcmp(key, "own_slots")) *value = c->own_built_g > 0 ? c->own_slots : 0;
     else if (!std::strcmp(key, "own_banded")) *value = c->own_built_g > 0 ? c->own_banded : 0;
     else if (!std::strcmp(key, "own_grid")) *value = c->own_built_g > 0 ? c->own_built_g : 0;
-    else if (!std::strcmp(key, "own_lag")) *value = c->own_lag;
     else return fail(HAKAI_ERR_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1660,6 +1658,20 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     }
     if (!std::strcmp(key, "elem_exact")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "elem_exact must be 0 or 1");
+        if (c->elem_exact != (int)value && c->own_for_g0 != -1) {
+            // the owner-assembly plan was sized for the other kernel's LDS budget (the reference-order
+            // kernel leaves fewer slots): re-planned before the next step (own_use; one context hands
+            // the last sums over through own_materialize). A multi-GPU rank whose sums are live cannot
+            // re-plan mid-run (its next interface fix reads the rows): it keeps a plan that fits the
+            // new kernel, else the switch is refused.
+            if (!(c->comm && c->own_valid)) {
+                c->own_for_g0 = -1;
+            } else if (c->own_built_g > 0 && c->own_slots > hk::own_slot_cap(value != 0, c->own_s, c->nmat)) {
+                return fail(HAKAI_ERR_STATE, "elem_exact: the owner-assembly lists of this multi-GPU rank need %d LDS "
+                            "slots, more than the %s kernel has; switch between calls after hakai_upload_state / "
+                            "hakai_reset_state", c->own_slots, value ? "reference-order" : "fused");
+            }
+        }
         c->elem_exact = (int)value;
         return 0;
     }
@@ -1678,18 +1690,6 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
         if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_assembly must be 0, 1 or 2");
         c->own_assembly = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "own_schedule")) {  // owner-assembly schedule: 0 auto, 1 contiguous, 2 banded
-        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_schedule must be 0, 1 or 2");
-        if (c->own_schedule != (int)value) c->own_for_g0 = -1;  // re-planned before the next step
-        c->own_schedule = (int)value;
-        return 0;
-    }
-    if (!std::strcmp(key, "own_lag")) {  // owner passes: 0 behind a block barrier, 1 lagged, barrier-free
-        if (value < 0 || value > 1) return fail(HAKAI_ERR_ARG, "own_lag must be 0 or 1");
-        if (c->own_lag != (int)value) c->own_for_g0 = -1;  // re-planned (S = 1, another slot budget)
-        c->own_lag = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "graph")) {

@@ -137,9 +137,6 @@ struct hakai_ctx {
     int* d_own_seq = nullptr;          // [nb] batch at each schedule position (ascending within a block)
     int* d_own_bstart = nullptr;       // [grid+1] first schedule position of each block
     int own_banded = 0;                // the schedule walks row bands of a structured cross-section
-    int own_w = 1;                     // lists per pass of the built plan (4: wave lists, lagged)
-    int own_lag = 0;                   // tuning "own_lag": 1 = lagged barrier-free passes (own 3)
-    int own_schedule = 0;              // tuning "own_schedule": 0 auto, 1 contiguous only, 2 banded only
     long long own_round2 = 0;          // summing passes of the built lists that take a second entry per thread
     int* d_own_list = nullptr;         // 4 ints per entry (+ one no-op entry at own_nop)
     int own_nop = 0;

@@ -907,54 +907,6 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
     }
 }
 
-// Lagged, barrier-free passes (ElemArgs::own 3): one batch per pass, forces staged in a ring of
-// three buffers, and the pass of batch i run by every wave right after the wave has computed batch
-// i + 1. The lists are per wave (own_off[4 pos + wave]): a running sum's slot belongs to one wave
-// (slot & 3, hakai_capi.cpp own_plan), so successive passes over a slot are ordered by that wave's
-// program order and need no synchronisation. Two LDS counters per ring slot replace the block
-// barrier: arrivals (a wave has staged batch i) and passes done (a wave has run its part of pass i).
-// A wave waits only for
-//  * every wave's arrival at i before it runs its part of pass i (the pass reads all waves' forces),
-//  * pass i - 3 complete before it restages that ring slot with batch i,
-// so waves drift up to two batches apart; the slowest never waits, and the block always progresses.
-// (Counters only grow: ring slot k's hold 4 x the passes through it so far.)
-__device__ __forceinline__ void lds_wait_ge(const unsigned* c, unsigned target) {
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-        __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-__device__ __forceinline__ void lds_signal(unsigned* c) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // this wave's LDS writes first
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-constexpr unsigned kWavesPerBlock = kBlock / 64;
-
-// this wave's first entry of the pass at schedule position pos (wave lists)
-__device__ __forceinline__ int4 own_load_wave(const ElemArgs& a, long long pos) {
-    const long long w = pos * kWavesPerBlock + (threadIdx.x >> 6);
-    const int o0 = a.own_off[w], o1 = a.own_off[w + 1];
-    const int idx = o0 + (int)(threadIdx.x & 63);
-    int4 en = a.own_list[idx < o1 ? idx : a.own_nop];
-    en.y |= (o1 - o0 > 64) ? kOwnRound2 : 0;
-    return en;
-}
-
-// the lagged pass of batch q (q >= 0) by this wave: en = its first entry of that pass
-__device__ __forceinline__ void own_pass_lag(const ElemArgs& a, int4 en, long long q, long long pos,
-                                             const double* s_fe_q, double* s_part, unsigned* s_cnt) {
-    lds_wait_ge(s_cnt + q % 3, kWavesPerBlock * (unsigned)(q / 3 + 1));  // every wave staged batch q
-    own_entry(a, en, s_fe_q, s_part);
-    if (en.y & kOwnRound2) {  // wave-uniform: more than 64 entries in this wave's list
-        const long long w = pos * kWavesPerBlock + (threadIdx.x >> 6);
-        const int o1 = a.own_off[w + 1];
-        for (int base = a.own_off[w] + 64; base < o1; base += 64) {
-            const int idx = base + (int)(threadIdx.x & 63);
-            own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe_q, s_part);
-        }
-    }
-    lds_signal(s_cnt + 3 + q % 3);
-}
-
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
 // issuing the loads of batch b+2 (connectivity, flags) and b+1 (node gathers, Gauss-point state)
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
@@ -962,13 +914,9 @@ __device__ __forceinline__ void own_pass_lag(const ElemArgs& a, int4 en, long lo
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS = 0>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
-    constexpr bool LAG = OS == 3;                // lagged barrier-free passes, one batch each
-    constexpr int kPassB = LAG ? 1 : OS;         // batches per pass
-    constexpr int kOwnFe = kPassB * kEPB * 24;   // staged forces per pass (doubles)
-    constexpr int kFeBufs = LAG ? 3 : 2;
+    constexpr int kOwnFe = OS * kEPB * 24;       // staged forces per pass (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
-    __shared__ __attribute__((aligned(16))) double s_fe[OWN ? kFeBufs * kOwnFe : 1];
-    __shared__ unsigned s_cnt[LAG ? 6 : 1];      // LAG: arrivals [3], passes done [3]
+    __shared__ __attribute__((aligned(16))) double s_fe[OWN ? 2 * kOwnFe : 1];
     // dynamic LDS (sized by the launch, launch_pipe): [own_slots][3] running sums, then the
     // nmat staged materials
     extern __shared__ __attribute__((aligned(16))) double s_dyn[];
@@ -987,8 +935,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         for (int w = threadIdx.x; w < words; w += kBlock) dst[w] = src[w];
     }
     if (EXACT) stage_pusai(a, s_pus);
-    if (LAG && threadIdx.x < 6) s_cnt[threadIdx.x] = 0u;
-    if (LDS_MATS || EXACT || LAG) __syncthreads();
+    if (LDS_MATS || EXACT) __syncthreads();
     const DevMat* mats = LDS_MATS ? s_mats : a.mats;
     double* nd8 = s_nd + grp * kLdsStride;
     double* xb = s_xb + (EXACT ? grp * kXbStride : 0);
@@ -1027,9 +974,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(0), k, cur);
     // (OWN: super-batch of iteration i starts at iteration i - i % OS; its entries are listed under
     // the schedule position of its first batch)
-    constexpr int S = OS > 0 && !LAG ? OS : 1;
+    constexpr int S = OS > 0 ? OS : 1;
     auto sb_of = [&](long long i) { return pos_of((i < count ? i : count - 1) / S * S); };
-    if (OWN && !LAG) ent_cur = own_load(a, sb_of(0));
+    if (OWN) ent_cur = own_load(a, sb_of(0));
     for (long long i = 0; i < count; ++i) {
         ElemIn nn;
         load_stage_a<EXACT>(a, elem_of(i + 2), k, nn);
@@ -1041,12 +988,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         // issuing this batch's node and/or Gauss-point loads at the end of the previous batch (before
         // its summing pass) spills and measured 1.18-1.28 against 1.10 ms, profiles/r03_exact_early_loads_ab.log.)
         if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
-        // (LAG: this iteration runs pass i - 1; its entry arrives during this batch's compute)
-        if (OWN && !LAG) ent_nxt = own_load(a, sb_of(i + 1));
-        if (LAG) ent_cur = own_load_wave(a, pos_of(i > 0 ? i - 1 : 0));
-        double* sfe = LAG ? s_fe + (i % 3) * kOwnFe : s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
-        if (LAG && i >= 3)  // ring slot free: pass i - 3 done by every wave
-            lds_wait_ge(s_cnt + 3 + i % 3, kWavesPerBlock * (unsigned)(i / 3));
+        if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
+        double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
             load_node_raw(a, cur);
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
@@ -1055,10 +998,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         }
         else
             elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, cur, sfe);
-        if (LAG) {
-            lds_signal(s_cnt + i % 3);  // batch i staged
-            if (i >= 1) own_pass_lag(a, ent_cur, i - 1, pos_of(i - 1), s_fe + ((i - 1) % 3) * kOwnFe, s_part, s_cnt);
-        } else if (OWN) {
+        if (OWN) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
             if ((i + 1) % S == 0 || i + 1 == count)
@@ -1068,9 +1008,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         cur = nxt;
         nxt = nn;
     }
-    if (LAG)  // the last batch's pass
-        own_pass_lag(a, own_load_wave(a, pos_of(count - 1)), count - 1, pos_of(count - 1),
-                     s_fe + ((count - 1) % 3) * kOwnFe, s_part, s_cnt);
 }
 
 // Runtime flags -> template instantiations.
@@ -1126,8 +1063,6 @@ static void launch_pipe_os(const ElemArgs& a, bool do_delete, bool store_triax, 
         launch_pipe_nt<ANY_PLASTIC, true, EXACT, 1>(a, do_delete, store_triax, grid, s);
     else if (a.own == 2)
         launch_pipe_nt<ANY_PLASTIC, true, EXACT, 2>(a, do_delete, store_triax, grid, s);
-    else if (a.own == 3)
-        launch_pipe_nt<ANY_PLASTIC, true, EXACT, 3>(a, do_delete, store_triax, grid, s);
     else
         launch_pipe_nt<ANY_PLASTIC, LDS_MATS, EXACT, 0>(a, do_delete, store_triax, grid, s);
 }
@@ -1150,9 +1085,9 @@ hipError_t launch_element(const ElemArgs& a, bool do_delete, bool store_triax, h
     const long long nb = a.nEp / kEPB;
     if (nb <= 0) return hipSuccess;
     if (a.own) {  // owner-computed assembly: persistent kernel only (own_build sized its lists for it)
-        if (a.own > 3 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
+        if (a.own > 2 || a.vol || a.pipe_blocks <= 0 || a.nmat > kMaxLdsMats || !a.own_off || !a.own_list ||
             !a.own_seq || !a.own_bstart || !a.own_q || !a.own_dump || a.own_slots < 1 ||
-            a.own_slots > own_slot_cap(a.exact != 0, a.own == 3 ? 1 : a.own, a.nmat, a.own == 3))
+            a.own_slots > own_slot_cap(a.exact != 0, a.own, a.nmat))
             return hipErrorInvalidValue;
         if (a.own_grid <= 0 || a.own_grid > nb) return hipErrorInvalidValue;  // (own_bstart has grid+1 entries)
         if (a.exact)
@@ -1454,33 +1389,6 @@ hipError_t launch_own_q(const double* own_q, const int* rp, const int* ridx, con
                         long long nN, hipStream_t s) {
     if (nN <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_own_q, dim3((unsigned)((nN + 255) / 256)), dim3(256), 0, s, own_q, rp, ridx, rows, Q, nN);
-    return hipGetLastError();
-}
-
-// Triaxiality of every Gauss point from the SoA stress, the element kernel's invariant form
-// (elem_step_exact's expression, so the same bits as the reference-order kernel) -- for downloads
-// after a call whose last step did not run (contact overflow).
-__global__ void k_triax_soa(const double* __restrict__ st, double* __restrict__ tx, const int* __restrict__ flag,
-                            long long nGP, long long ld) {
-#pragma clang fp contract(off)
-    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nGP) return;
-    double f[6];
-    for (int c = 0; c < 6; ++c) f[c] = st[c * ld + g];
-    const double x = f[0] + f[1] + f[2];
-    constexpr double y = 1.0 / 3.0;
-    const double q = x * y;
-    const double mean = __builtin_fma(__builtin_fma(-q, 3.0, x), y, q);
-    const double a01 = f[0] - f[1], a12 = f[1] - f[2], a20 = f[2] - f[0];
-    const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) + 3.0 * (f[3] * f[3] + f[4] * f[4] + f[5] * f[5]));
-    tx[g] = (flag[g >> 3] != 1 || oeq < 1e-10) ? 0.0 : mean / oeq;
-}
-
-hipError_t launch_triax_soa(const double* stress, double* triax, const int* flag, long long nGP, long long ld,
-                            hipStream_t s) {
-    if (nGP <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_triax_soa, dim3((unsigned)((nGP + 255) / 256)), dim3(256), 0, s, stress, triax, flag, nGP,
-                       ld);
     return hipGetLastError();
 }
 

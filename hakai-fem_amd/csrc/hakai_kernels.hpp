@@ -47,8 +47,8 @@ struct ElemArgs {
     // node's complete Q, or the prefix partial P of a node whose later incidences belong to later
     // blocks, into own_q, and those later contributions one by one into own_rows. No fe traffic
     // except on a call's last step (STORE_TRIAX), which also stores fe so Q/Qe downloads stay valid.
-    int own;                // 0 off; 1 or 2: batches of 32 elements per summing pass, behind a block
-                            // barrier; 3: one batch per pass, lagged, barrier-free (k_element_pipe)
+    int own;                // 0 off; 1 or 2: batches of 32 elements per summing pass (behind a block
+                            // barrier, k_element_pipe)
     int own_grid;           // blocks of the owner-assembly launch (the lists' partition)
     const int* own_seq;     // [nb] batch at each schedule position; block lb walks positions
     const int* own_bstart;  // [own_bstart[lb], own_bstart[lb+1]) (batches ascending within a block)
@@ -107,9 +107,9 @@ struct NodalArgs {
 // the Pusai table, 20 KB; hakai_kernels.hip checks these sizes) and the staged materials; at most
 // 2048 (11-bit slot ids in the entry lists).
 constexpr int kOwnSlotsMax = 2048;
-inline int own_slot_cap(bool exact, int batches_per_pass, int nmat, bool lagged = false) {
-    // (force staging: 6 KB per batch, two buffers; lagged passes: a ring of three one-batch buffers)
-    const int stat = 12800 + 6144 * batches_per_pass * (lagged ? 3 : 2) + (exact ? 20480 : 0) + 64;
+inline int own_slot_cap(bool exact, int batches_per_pass, int nmat) {
+    // (force staging: 6 KB per batch, two buffers)
+    const int stat = 12800 + 6144 * batches_per_pass * 2 + (exact ? 20480 : 0) + 64;
     const int left = 81920 - 256 - stat - nmat * (int)sizeof(DevMat);
     return left < 24 ? 0 : (left / 24 > kOwnSlotsMax ? kOwnSlotsMax : left / 24);
 }
@@ -127,9 +127,6 @@ hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe,
 // Q from the owner-computed sums: own_q[n] + the node's rows in element order (= k_nodal MODE 3).
 hipError_t launch_own_q(const double* own_q, const int* rp, const int* ridx, const double* rows, double* Q,
                         long long nN, hipStream_t s);
-// Triaxiality of the SoA stress in the element kernel's invariant form (0 for inactive elements).
-hipError_t launch_triax_soa(const double* stress, double* triax, const int* flag, long long nGP, long long ld,
-                            hipStream_t s);
 // AoS [gp][6] <-> SoA [6][ld] conversions used at upload/download.
 hipError_t launch_aos_to_soa6(const double* aos, double* soa, long long nGP, long long ld, hipStream_t s);
 hipError_t launch_soa_to_aos6(const double* soa, double* aos, long long nGP, long long ld, hipStream_t s);

@@ -185,10 +185,6 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       reference-order kernel where the lists need two entries per thread in some
  *                       pass (wide sections, hakai_stat "own_round2": the array is faster there);
  *                       2: the owner sums wherever they fit;
- *   "own_schedule"      its block schedule: 0 (default) the cheapest that fits, 1 contiguous batch
- *                       ranges only, 2 row bands of structured wide sections only;
- *   "own_lag"           its summing passes: 0 (default) behind a block barrier, 1 one batch per pass,
- *                       run by each wave one batch late and ordered by LDS counters (no barrier);
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);

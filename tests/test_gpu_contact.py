@@ -249,3 +249,69 @@ def test_fused_small_deck_phases_bitexact(flag, graph):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
 
 
+
+
+@pytest.mark.parametrize("graph", [0, 16])
+def test_overflow_recovery_paths_keep_q(graph):
+    """The owner-assembly Q survives every way back from a contact overflow:
+    (a) a call whose FIRST step overflows (nothing of it ran) after an upload with Q: the uploaded
+        Q is still the one the next nodal update takes;
+    (b) an upload of the state without Q or Qe after an overflowed call: the owner sums become Q
+        (fe is an earlier step's there);
+    (c) such an upload that also deletes elements is refused (their fe rows cannot be zeroed).
+    Each continuation, with the buffer raised, equals an uninterrupted run bit for bit."""
+    import re
+    from hakai._abi import HakaiError
+    m = mesh.two_body_model(plate=(12, 12, 1), impactor=(8, 8, 1), v=-1e5, perturb=0.03, seed=4, n_steps=60)
+    tune = {"graph": graph, "own_assembly": 1, "elem_pipe_min": 0, "elem_pipe_blocks": 3}
+
+    def solver(cap):
+        sv = Solver(m)
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("contact_event_cap", cap)
+        return sv
+
+    keys = ("disp", "disp_pre", "velo", "integ_stress", "integ_strain", "integ_eq_plastic_strain",
+            "integ_yield_stress", "element_flag", "Q")
+    with solver(1 << 12) as sv:
+        sv.step(1, m.n_steps)
+        full = sv.download()
+        assert sv.stat("own_steps") > 0
+
+    def fail_step(sv, t0):
+        with pytest.raises(HakaiError) as ei:
+            sv.step(t0, m.n_steps - t0 + 1)
+        return int(re.search(r"step (\d+) was not applied", str(ei.value)).group(1))
+
+    # (a) upload with Q, then a call that overflows at once
+    with solver(1) as sv:
+        p = fail_step(sv, 1)
+        st = sv.download(**{k: True for k in keys})
+        sv.upload(st)                              # Q -> the uploaded-Q buffer, owner sums off
+        assert fail_step(sv, p) == p               # good == 0
+        sv.set_tuning("contact_event_cap", 1 << 12)
+        sv.step(p, m.n_steps - p + 1)
+        a = sv.download()
+    # (b) upload without Q / Qe after the overflow
+    with solver(1) as sv:
+        p = fail_step(sv, 1)
+        st = sv.download(**{k: True for k in keys})
+        st_noq = State(st.disp, st.disp_pre, st.velo, None, st.integ_stress, st.integ_strain, st.integ_yield_stress,
+                       st.integ_eq_plastic_strain, None, st.element_flag, None)
+        sv.upload(st_noq)
+        sv.set_tuning("contact_event_cap", 1 << 12)
+        sv.step(p, m.n_steps - p + 1)
+        b = sv.download()
+    # (c) refused with deletions and no Q
+    with solver(1) as sv:
+        fail_step(sv, 1)
+        st = sv.download(**{k: True for k in keys})
+        fl = st.element_flag.copy()
+        fl[0] = 0
+        with pytest.raises(HakaiError, match="upload Q"):
+            sv.upload(State(st.disp, st.disp_pre, st.velo, None, st.integ_stress, st.integ_strain,
+                            st.integ_yield_stress, st.integ_eq_plastic_strain, None, fl, None))
+    for k in keys:
+        assert bitwise_equal(getattr(a, k), getattr(full, k)), ("a", k)
+        assert bitwise_equal(getattr(b, k), getattr(full, k)), ("b", k)

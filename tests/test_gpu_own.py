@@ -201,31 +201,23 @@ def test_own_grid_change_between_calls_rebuilds():
 
 @pytest.mark.parametrize("shape", [(100, 100, 16), (200, 200, 5)])
 def test_own_banded_wide_sections_bitexact(shape):
-    """Wide cross-sections (C5's 100x100, C4's plate 200x200): the row-band schedule (own_schedule 2:
-    each block walks one band of element rows over a run of layers) exports far fewer rows than the
-    contiguous batch ranges (own_schedule 1) and both are bit-identical to the fe path."""
+    """Wide cross-sections (C5's 100x100, C4's plate 200x200): the planner picks the row-band
+    schedule (each block walks one band of element rows over a run of layers; it exports fewer rows
+    than contiguous batch ranges, tests/test_own_plan.py) and the result is bit-identical to the fe
+    path."""
     nx, ny, nz = shape
     m = small_bar(nx, ny, nz, n_steps=120, v_end=5e5)
     tune = {"elem_pipe_blocks": 128}  # (the 200-wide section's 67 row bands need a block each)
     calls = [(1, 61), (62, 59)]
     g0, _, _ = _run(m, calls, tune, 0)
-    res = {}
-    for sched in (1, 2, 0):
-        with Solver(m) as sv:
-            for k, v in tune.items():
-                sv.set_tuning(k, v)
-            sv.set_tuning("own_assembly", 1)
-            sv.set_tuning("own_schedule", sched)
-            for t0, n in calls:
-                sv.step(t0, n)
-            g = sv.download()
-            res[sched] = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_banded", "own_grid")}
-        _same(g, g0)
-    assert res[2]["own_steps"] == 120 and res[2]["own_banded"] == 1, res
-    assert res[1]["own_steps"] in (0, 120), res
-    if res[1]["own_steps"]:
-        assert res[2]["own_rows"] < res[1]["own_rows"], res
-    assert res[0]["own_banded"] == 1 and res[0]["own_rows"] == res[2]["own_rows"], res
+    g1, _, st = _run(m, calls, tune, 1)
+    _same(g1, g0)
+    assert st["own_steps"] == 120, st
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.step(1, 1)
+        assert sv.stat("own_banded") == 1
 
 
 def test_own_banded_two_bodies_contact_bitexact():
@@ -239,7 +231,6 @@ def test_own_banded_two_bodies_contact_bitexact():
         for k, v in tune.items():
             sv.set_tuning(k, v)
         sv.set_tuning("own_assembly", 1)
-        sv.set_tuning("own_schedule", 2)
         sv.step(1, 151)
         sv.step(152, n - 151)
         g1 = sv.download()
@@ -268,24 +259,27 @@ def test_own_reference_order_mode_bitexact(shape):
     assert stats[2]["own_steps"] == 80, stats
 
 
-@pytest.mark.parametrize("exact", [0, 1])
-@pytest.mark.parametrize("case", ["deleting_bar", "wide"])
-def test_own_lagged_passes_bitexact(case, exact):
-    """Lagged, barrier-free owner passes (own_lag 1: waves run their part of batch i's pass after
-    staging batch i + 1, synchronised by LDS counters): bit-identical to the fe path, in both element
-    modes, on a deleting bar over 16 blocks (odd step counts, graphs on) and on a wide section whose
-    passes need second entries."""
-    if case == "deleting_bar":
-        m = fast_deletion_bar(4, 4, 400)
-        calls = [(1, 301), (302, 699)]
-        tune = {**PIPE, "elem_pipe_blocks": 16, "elem_exact": exact}
-    else:
-        m = small_bar(100, 100, 12, n_steps=80, v_end=5e5)
-        calls = [(1, 41), (42, 39)]
-        tune = {"elem_pipe_blocks": 64, "elem_exact": exact}
-    n = sum(c[1] for c in calls)
-    g0, d0, _ = _run(m, calls, tune, 0)
-    g1, d1, st = _run(m, calls, {**tune, "own_lag": 1}, 2)
-    assert st["own_steps"] == n, st
-    assert d1 == d0
-    _same(g1, g0)
+def test_own_elem_exact_switch_mid_run_replans():
+    """Switching the element kernel between calls re-plans the owner lists for the new kernel's LDS
+    budget: on a wide section over 8 blocks the fused kernel's row bands need ~1670 slots,
+    more than the reference-order kernel has (~920), so keeping that plan failed the launch. Fused ->
+    reference order -> fused with owner sums forced on (own_assembly 2) must equal the same switches
+    on the fe path, bit for bit."""
+    m = small_bar(100, 100, 12, n_steps=90, v_end=5e5)
+    res = {}
+    for own in (0, 2):
+        with Solver(m) as sv:
+            sv.set_tuning("elem_pipe_blocks", 8)
+            sv.set_tuning("own_assembly", own)
+            sv.step(1, 30)
+            slots_fused = sv.stat("own_slots")
+            sv.set_tuning("elem_exact", 1)
+            sv.step(31, 30)
+            slots_exact = sv.stat("own_slots")
+            sv.set_tuning("elem_exact", 0)
+            sv.step(61, 30)
+            res[own] = (sv.download(), sv.stat("own_steps"), slots_fused, slots_exact)
+    g2, steps2, sf, se = res[2]
+    assert steps2 == 90, res[2][1:]
+    assert sf > 923 >= se, (sf, se)  # the two kernels really needed different plans
+    _same(g2, res[0][0])

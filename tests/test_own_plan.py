@@ -6,7 +6,7 @@ which node contributions in which order. The replay executes each plan as k_elem
 do and checks that every node's Q equals the reference's serial assembly in ascending element order
 (v2/HAKAI_j.jl:668-675) BIT FOR BIT, for random contributions spanning 60 binades -- for slender and
 wide sections, two bodies with different lattice strides (C4's shape), shuffled numbering, the
-finer fallback grid, tiny grids, and the per-wave lists of the lagged passes. The GPU tests (tests/test_gpu_own.py) then check that the
+finer fallback grid and tiny grids. The GPU tests (tests/test_gpu_own.py) then check that the
 kernels execute the same plans.
 """
 import json
@@ -30,11 +30,6 @@ CASES = [
     ("60 60 6 --G 1", {"grid": 8}),                                 # too many open sums: 8x finer grid
     ("4 4 40 --G 3", {"grid": 3}),
     ("5 1 1 --G 1", {}),                                            # Tensile5e-sized: one batch
-    # lagged passes: one list per wave, a running sum only ever in its slot's wave (checked)
-    ("20 20 300 --lag 1", {"superbatch": 1}),
-    ("100 100 40 --G 32 --exact 1 --lag 1", {"banded": 1, "superbatch": 1}),
-    ("30 30 12 --plate 120 120 3 --G 48 --lag 1", {"superbatch": 1}),
-    ("3 3 200 --G 8 --shuffle 11 --lag 1", {}),
 ]
 
 

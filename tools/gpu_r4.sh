@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-4 GPU command, one file with named stages (runs on the gpurun box from the repo root):
+#   bash tools/gpu_r4.sh STAGE [STAGE ...]
+# Every GPU step has its own time limit; the first failing step ends the call (no retries).
+# Stages:
+#   suite      pytest -m gpu (whole suite, thread timeouts) -> gpurun_out/r4_suite.log
+#   smoke      __graft_entry__.smoke()                      -> gpurun_out/r4_smoke.log
+#   bench      python bench.py (N = 1, driver defaults)     -> gpurun_out/r4_bench.json
+#   rehearse2  python bench.py --gpus 2 with no launcher on the one GPU (ranks share it over RCCL
+#              sockets: HAKAI_RCCL_SHARED_GPU=1)           -> gpurun_out/r4_rehearse2.json
+#   prof       rocprofv3 kernel trace of a short bench     -> gpurun_out/r4_prof/
+#   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r4_tests.log
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() {  # run <seconds> <log> cmd...
+    local t=$1 log=$2
+    shift 2
+    timeout -k 10 "$t" "$@" > "$log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $* -> rc=$rc"
+    tail -n 12 "$log"
+    return $rc
+}
+for st in "$@"; do
+    case "$st" in
+    suite) run 1500 gpurun_out/r4_suite.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
+               --timeout-method thread -p no:cacheprovider || exit $? ;;
+    smoke) run 300 gpurun_out/r4_smoke.log python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run 600 gpurun_out/r4_bench.json python bench.py || exit $? ;;
+    rehearse2) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r4_rehearse2.json python bench.py --gpus 2 \
+                   --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
+    prof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_prof \
+              -o r4 -- python bench.py --steps 50 --warmup 5 --cpu-baseline 0 || exit $? ;;
+    tests:*) run 1200 gpurun_out/r4_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
+                 --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+    esac
+done

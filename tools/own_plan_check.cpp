@@ -11,7 +11,7 @@
 // (v2/HAKAI_j.jl:668-675) for random contributions with mixed signs and magnitudes.
 //
 //   own_plan_check nx ny nz [--plate px py pz] [--G n] [--exact 0|1] [--schedule 0|1|2]
-//                  [--shuffle seed] [--lag 0|1]
+//                  [--shuffle seed]
 // Prints one JSON line: {"ok": ..., "planned": ..., "epb", "grid", "superbatch", "banded", "rows",
 // "entries", "slots", "mismatch"} and exits 0 when the replay matches (or no plan fits: planned false).
 #include "../hakai-fem_amd/csrc/hakai_capi.cpp"
@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int nx = std::atoi(argv[1]), ny = std::atoi(argv[2]), nz = std::atoi(argv[3]);
-    int px = 0, py = 0, pz = 0, exact = 0, schedule = 0, lag = 0;
+    int px = 0, py = 0, pz = 0, exact = 0, schedule = 0;
     long long G0 = 512;
     long long shuffle = -1;
     for (int a = 4; a < argc; ++a) {
@@ -53,7 +53,6 @@ int main(int argc, char** argv) {
         } else if (k == "--G" && a + 1 < argc) G0 = std::atoll(argv[++a]);
         else if (k == "--exact" && a + 1 < argc) exact = std::atoi(argv[++a]);
         else if (k == "--schedule" && a + 1 < argc) schedule = std::atoi(argv[++a]);
-        else if (k == "--lag" && a + 1 < argc) lag = std::atoi(argv[++a]);
         else if (k == "--shuffle" && a + 1 < argc) shuffle = std::atoll(argv[++a]);
         else {
             std::fprintf(stderr, "bad argument %s\n", argv[a]);
@@ -87,8 +86,6 @@ int main(int argc, char** argv) {
     c.h_conn = conn;
     c.nmat = 1;
     c.elem_exact = exact;
-    c.own_schedule = schedule;
-    c.own_lag = lag;
     // node -> (8e + k) CSR in ascending element order (hakai_upload_model)
     std::vector<int> cnt(nN + 1, 0);
     for (long long e = 0; e < nE; ++e)
@@ -106,7 +103,7 @@ int main(int argc, char** argv) {
 
     OwnSched sc;
     OwnPlan pl;
-    const bool planned = own_choose(&c, G, sc, pl);
+    const bool planned = own_choose(&c, G, sc, pl, schedule);
     if (!planned) {
         std::printf("{\"ok\": true, \"planned\": false, \"elements\": %lld, \"nodes\": %d}\n", nE, nN);
         return 0;
@@ -140,15 +137,8 @@ int main(int argc, char** argv) {
                     const long long e = (long long)sc.seq[p] * epb + l / 8;
                     stage[(p - p0) * 8 * epb + l] = e < nE ? f[8 * e + l % 8] : 0.0;
                 }
-            for (int q = pl.off[p0 * pl.W]; q < pl.off[(p0 + 1) * pl.W]; ++q) {
+            for (int q = pl.off[p0]; q < pl.off[p0 + 1]; ++q) {
                 const int* w = &pl.list[4 * (size_t)q];
-                if (pl.W > 1) {  // wave lists: a running sum is only touched by its slot's wave
-                    int wave = 0;
-                    while (q >= pl.off[p0 * pl.W + wave + 1]) ++wave;
-                    const int fl = (w[1] >> 10) & 15;
-                    if (!(fl & (kOwnExpH | kOwnNopH)) && (((w[1] & 1023) | ((w[1] >> 18) & 1024)) & (pl.W - 1)) != wave)
-                        ++bad;
-                }
                 const int slot = (w[1] & 1023) | ((w[1] >> 18) & 1024), flags = (w[1] >> 10) & 15,
                           n = (w[1] >> 14) & 15;
                 if (flags & kOwnExpH) {
@@ -177,17 +167,10 @@ int main(int argc, char** argv) {
         if (std::memcmp(&q, &ref, sizeof q) != 0) ++mismatch;
     }
     const bool ok = mismatch == 0 && bad == 0;
-    int wave_max = 0;
-    long long wave_sum = 0;
-    for (int v : pl.wave_counts) {
-        wave_max = std::max(wave_max, v);
-        wave_sum += v;
-    }
     std::printf("{\"ok\": %s, \"planned\": true, \"elements\": %lld, \"nodes\": %d, \"epb\": %d, \"grid\": %lld, "
                 "\"superbatch\": %d, \"banded\": %d, \"rows\": %lld, \"entries\": %lld, \"slots\": %d, "
-                "\"slot_cap\": %d, \"round2\": %lld, \"wave_max\": %d, \"wave_mean\": %.1f, \"mismatch\": %lld, \"double_fin\": %lld}\n",
+                "\"slot_cap\": %d, \"round2\": %lld, \"mismatch\": %lld, \"double_fin\": %lld}\n",
                 ok ? "true" : "false", nE, nN, epb, Gp, S, sc.banded ? 1 : 0, pl.rows, pl.ne, pl.max_slots,
-                hk::own_slot_cap(exact != 0, S, 1, lag != 0), pl.round2, wave_max,
-                pl.wave_counts.empty() ? 0.0 : (double)wave_sum / (double)pl.wave_counts.size(), mismatch, bad);
+                hk::own_slot_cap(exact != 0, S, 1), pl.round2, mismatch, bad);
     return ok ? 0 : 1;
 }

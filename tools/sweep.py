@@ -45,7 +45,7 @@ sv.sync()
 t = a.preload + 1
 res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
 DEFAULTS = {"elem_exact": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_pipe_min": 2, "elem_gp_nt": 1,
-            "own_assembly": 1, "own_schedule": 0, "own_lag": 0}
+            "own_assembly": 1}
 for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
