@@ -70,6 +70,16 @@ __device__ __forceinline__ T* at32(T* base, unsigned bytes) {
     return reinterpret_cast<T*>(reinterpret_cast<C*>(base) + bytes);
 }
 
+// Orders this wave's LDS accesses around a cross-lane exchange (the 8 lanes of an element write,
+// then read each other's values). A wave's LDS operations execute in order, so this only stops the
+// compiler from moving LDS accesses across it; restricted to the local address space, it leaves
+// the global loads and stores (the pipeline's prefetches, the write-back) free to be scheduled
+// across the exchanges.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
 template <bool EXACT = false>
 __device__ __forceinline__ void load_stage_a(const ElemArgs& a, long long e, int k, ElemIn& in) {
     const unsigned ue = (unsigned)e;
@@ -221,8 +231,7 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     nd8[6 * k + 3] = in.du[0];
     nd8[6 * k + 4] = in.du[1];
     nd8[6 * k + 5] = in.du[2];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
 
     // ---- Relative node slots. Label a node by its sign bits s = (x>0)<<2 | (y>0)<<1 | (z>0); GP k
     // carries its (xi, eta, zeta) signs in the same bits (v2/HAKAI_j.jl:1913-1920). Lane k works on
@@ -458,13 +467,11 @@ __device__ __forceinline__ double div_cr(double a, double b, double rb) {
 __device__ __forceinline__ double gp_sum8(double* w, int k, const double (&v)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[8 * i + k] = v[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double r[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) r[kk] = w[8 * k + kk];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double acc = 0.0 + r[0];
 #pragma unroll
     for (int kk = 1; kk < 8; ++kk) acc += r[kk];
@@ -477,15 +484,13 @@ __device__ __forceinline__ double gp_sum8x(double* w, int k, const double (&v)[8
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[8 * i + k] = v[i];
     w[64 + k] = x;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double r[8], q[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) r[kk] = w[8 * k + kk];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) q[kk] = w[64 + kk];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double acc = 0.0 + r[0], xs = 0.0 + q[0];
 #pragma unroll
     for (int kk = 1; kk < 8; ++kk) {
@@ -500,15 +505,13 @@ __device__ __forceinline__ double gp_sum8x(double* w, int k, const double (&v)[8
 __device__ __forceinline__ void gp_all8x2(double* w, int k, double x, double y, double& xs, double& ys) {
     w[k] = x;
     w[8 + k] = y;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double r[8], q[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) r[kk] = w[kk];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) q[kk] = w[8 + kk];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     double a = 0.0 + r[0], b = 0.0 + q[0];
 #pragma unroll
     for (int kk = 1; kk < 8; ++kk) {
@@ -537,8 +540,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     nd8[6 * k + 3] = in.uu[0] - in.up[0];
     nd8[6 * k + 4] = in.uu[1] - in.up[1];
     nd8[6 * k + 5] = in.uu[2] - in.up[2];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
 
     // ---- Jacobian at GP k in node order, det and inverse (cal_Bfinal :1424-1455; cal_BVbar_hexa
     // computes the same J and det at :1716-1740). The first term starts the sum (0 + x == x).
@@ -587,6 +589,13 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         }
     }
 
+    // P2/3 (cal_BVbar_hexa's P2 / 3 at :1745-1750 and Bfinal's -P2/3 at :1482-1490: the same
+    // correctly rounded quotient), formed once; it becomes t(i,c) below, in place
+    double tk[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tk[i][c] = div3(pd[i][c]);
     // ---- V and BVbar (:1729-1780)
     double V;  // sum of |det| in GP order, in the first component's round trip
     {
@@ -595,7 +604,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         for (int c = 0; c < 3; ++c) {
             double w[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) w[i] = div3(pd[i][c]) * v;
+            for (int i = 0; i < 8; ++i) w[i] = tk[i][c] * v;
             if (c == 0)
                 bs[c] = gp_sum8x(xb, k, w, fabs(v), V);
             else
@@ -606,15 +615,12 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
 #pragma unroll
         for (int c = 0; c < 3; ++c) nd8[6 * k + c] = div_cr(bs[c], V, rV);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_fence();
     // Bfinal rows 1-3 carry t(i,c) = -P2/3 + BVbar (:1482-1490), formed once per node and component
-    // (the 32-bit addressing leaves the registers for all 24 next to P2)
-    double tk[8][3];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) tk[i][c] = nd8[6 * i + c] - div3(pd[i][c]);
+        for (int c = 0; c < 3; ++c) tk[i][c] = nd8[6 * i + c] - tk[i][c];
     auto tq = [&](int i, int c) { return tk[i][c]; };
 
     // ---- de = Bfinal * d_u (:1204): per row, the fma chain over columns j = 3i+c in order.

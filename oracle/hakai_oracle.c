@@ -15,6 +15,16 @@
 #include <omp.h>
 #endif
 
+/* One term of a StaticArrays product chain (v2/HAKAI_j.jl:1204-1205, :1330): muladd, which the
+ * reference's Julia lowers to a fused multiply-add on FMA hosts. HKO_SEPARATE_ROUNDING builds the
+ * sensitivity variant (libhakai_oracle_nofma.so, tools/oracle_muladd_sensitivity.py) with the
+ * product and the sum rounded separately, to measure what that lowering assumption is worth. */
+#ifdef HKO_SEPARATE_ROUNDING
+#define HKO_MULADD(a, b, c) ((a) * (b) + (c))
+#else
+#define HKO_MULADD(a, b, c) fma((a), (b), (c))
+#endif
+
 typedef struct {
     double density, young, poisson, G;
     double Dmat[36];          /* column-major 6x6, v2/HAKAI_j.jl:150-160 */
@@ -345,12 +355,12 @@ static void stress_one_element(const hko_model* m, int64_t e, double* Qe, double
         double de[6], dsig[6];
         for (int r = 0; r < 6; ++r) {
             double acc = Bfinal[r][0] * d_u[0];
-            for (int j = 1; j < 24; ++j) acc = fma(Bfinal[r][j], d_u[j], acc);
+            for (int j = 1; j < 24; ++j) acc = HKO_MULADD(Bfinal[r][j], d_u[j], acc);
             de[r] = acc;
         }
         for (int r = 0; r < 6; ++r) {
             double acc = Dm[r + 0] * de[0];
-            for (int j = 1; j < 6; ++j) acc = fma(Dm[r + 6 * j], de[j], acc);
+            for (int j = 1; j < 6; ++j) acc = HKO_MULADD(Dm[r + 6 * j], de[j], acc);
             dsig[r] = acc;
         }
         const int64_t idx = e * 8 + i;
@@ -393,7 +403,7 @@ static void stress_one_element(const hko_model* m, int64_t e, double* Qe, double
         /* q_vec_i = Bfinal' * final_stress ; Qe[:,e] += W*W*W*detJ*q_vec_i */
         for (int j = 0; j < 24; ++j) {
             double acc = Bfinal[0][j] * fin[0];
-            for (int r = 1; r < 6; ++r) acc = fma(Bfinal[r][j], fin[r], acc);
+            for (int r = 1; r < 6; ++r) acc = HKO_MULADD(Bfinal[r][j], fin[r], acc);
             Qe[24 * e + j] += W * W * W * detJ * acc;
         }
     }

@@ -12,7 +12,10 @@ from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_void_p
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "libhakai_oracle.so")
+# HAKAI_ORACLE_VARIANT=nofma (tools/oracle_muladd_sensitivity.py only): the build whose StaticArrays
+# chains round products and sums separately instead of fusing them
+LIB = os.path.join(HERE, "_build", "libhakai_oracle%s.so" % (
+    "_nofma" if os.environ.get("HAKAI_ORACLE_VARIANT") == "nofma" else ""))
 PD, PI64 = POINTER(c_double), POINTER(c_int64)
 
 

@@ -9,6 +9,7 @@
 #   rehearse2  python bench.py --gpus 2 with no launcher on the one GPU (ranks share it over RCCL
 #              sockets: HAKAI_RCCL_SHARED_GPU=1)           -> gpurun_out/r4_rehearse2.json
 #   prof       rocprofv3 kernel trace of a short bench     -> gpurun_out/r4_prof/
+#   drift      fused-kernel drift on the reference decks  -> gpurun_out/r4_deck_drift.jsonl
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r4_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -32,6 +33,7 @@ for st in "$@"; do
                    --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
     prof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_prof \
               -o r4 -- python bench.py --steps 50 --warmup 5 --cpu-baseline 0 || exit $? ;;
+    drift) run 600 gpurun_out/r4_deck_drift.jsonl python tools/deck_drift.py || exit $? ;;
     tests:*) run 1200 gpurun_out/r4_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
                  --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
