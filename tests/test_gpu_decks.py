@@ -50,13 +50,23 @@ def test_reference_deck_bitexact(name):
     assert np.array_equal(g.disp_pre, z["disp_pre"])
 
 
-@pytest.mark.parametrize("name,tol", [("Charpy_test", 1e-6), ("bullet_impact", 1e-6), ("car_crash_N2k", 5e-3),
-                                      ("car_wall_N2k", 5e-3)])
+# Fused-kernel bounds on the long car decks: the decks' own sensitivity to a one-ulp change of
+# their inputs is 1.1e-3-1.8e-3 of the final displacement (the oracle against itself,
+# profiles/r03_oracle_conditioning.jsonl), and the oracle's own fma/no-fma lowering of the
+# StaticArrays chains moves the crash tube by 2.3e-3 (profiles/r04_oracle_muladd_sensitivity.jsonl);
+# the fused kernel drifts 1.75e-3 (car-crash) and 1.9e-4 (car-wall) over 200 000 steps
+# (profiles/r04_deck_drift_fused.jsonl). 2.5e-3 is that conditioning with a 1.4x margin.
+CAR_DECK_TOL = 2.5e-3
+CRASH_TUBE_TOL = 1.5 * 2.2e-3  # 1.5x the tube's 1-ulp conditioning; the fused run drifts 1.0e-10
+
+
+@pytest.mark.parametrize("name,tol", [("Charpy_test", 1e-6), ("bullet_impact", 1e-6), ("car_crash_N2k", CAR_DECK_TOL),
+                                      ("car_wall_N2k", CAR_DECK_TOL)])
 def test_reference_deck_parity(name, tol):
     """The fused kernel (default for hakai_step): rounding-level element differences, 1e-6 on the
-    short decks. Over the car decks' 200000 steps those differences grow (car-crash: 8.3e-4
-    relative at the end, profiles/r02_decks_gpu_vs_cpu_oracle.jsonl); the exact mode stays bit-exact
-    there (test_reference_deck_bitexact), so the fused bound is the measured drift with margin."""
+    short decks. Over the car decks' 200000 steps those differences grow to the decks' own 1-ulp
+    conditioning (CAR_DECK_TOL above); the exact mode stays bit-exact there
+    (test_reference_deck_bitexact)."""
     z, m = _deck(name)
     steps = int(z["steps"])
     with Solver(m) as sv:
@@ -87,7 +97,8 @@ def test_self_contact_deck_stepwise_parity():
     lane-dependent node order) part after the first such flip, by ~1e-3 relative within 100 steps
     (tools/diag_deck_divergence.py). Parity is therefore checked on the step function: from the
     GPU's own state at checkpoints, the oracle's step and the GPU's step agree (contact force bit
-    for bit, displacement <= 1e-12, stress <= 1e-9 relative), and the trajectories stay within 1e-2."""
+    for bit, displacement <= 1e-12, stress <= 1e-9 relative), and the whole trajectory stays within
+    1.5x the deck's own 1-ulp conditioning (CRASH_TUBE_TOL)."""
     z, m = _deck("crash_tube_80_350_solid")
     steps = int(z["steps"])
     import oracle as O
@@ -111,7 +122,7 @@ def test_self_contact_deck_stepwise_parity():
             assert np.array_equal(g1.element_flag, o.s["element_flag"])
         sv.step(t, steps - t + 1)
         g = sv.download()
-    assert rel_err(g.disp, z["disp"]) < 1e-2
+    assert rel_err(g.disp, z["disp"]) < CRASH_TUBE_TOL
 
 
 def test_charpy_deck_two_ranks_bitexact():
