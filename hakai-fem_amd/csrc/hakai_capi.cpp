@@ -604,7 +604,6 @@ int hakai_reset_state(hakai_ctx* c, int64_t n_ic, const int64_t* ic_dofs, const 
     c->q_from_buf = false;
     c->fe_ok = c->triax_ok = true;
     c->steps_done = 0;
-    c->poison_halt = false;
     HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), s));
     hkc::comm_reset(c);
     if (n_ic > 0) {
@@ -706,7 +705,6 @@ int hakai_upload_state(hakai_ctx* c, const hakai_state_t* st) {
     HIPCHK(hipMemsetAsync(c->d_poison, 0, 2 * sizeof(int), s));
     HIPCHK(hipStreamSynchronize(s));
     c->steps_done = 0;
-    c->poison_halt = false;
     c->fe_ok = c->triax_ok = true;
     hkc::comm_reset(c);
     c->state_ok = true;
@@ -1267,20 +1265,25 @@ static bool own_use(hakai_ctx* c) {
 }
 
 // One explicit step (the loop body :497-764). With c->g_trd set (graph capture) the kernels take
-// the step number from the device counter and the element kernel advances it. phase: 1 = the
-// contact search (phase A), 2 = the rest (contact phase B, nodal, BCs, element, exchange), 3 = both;
-// an in-process group with the divided multi-GPU contact search runs phase 1 on every rank first
-// (hakai_step_group).
-static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase = 3) {
+// the step number from the device counter and the element kernel advances it. Phase bits: the
+// contact search parts A1, A2, A3 (hkc::contact_phase; one GPU: all of it in A1) and the rest
+// (contact phase B, nodal, BCs, element, exchange). An in-process group with multi-GPU contact runs
+// each part on every rank before the next (hakai_step_group).
+enum { kPhaseA1 = 1, kPhaseRest = 2, kPhaseA2 = 4, kPhaseA3 = 8, kPhaseAll = 15 };
+static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase = kPhaseAll) {
     hipStream_t s = c->stream;
     EventPair ep;
-    if ((phase & 1) && c->contact) {  // contact force into external_force (:500-560), search part
-        hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
-        const int rc = hkc::contact_step_a(c, t, d_time);
-        hkc::prof_end(c, &ep);
-        if (rc) return rc;
+    if (c->contact) {  // contact force into external_force (:500-560), search parts
+        const int part_bit[3] = {kPhaseA1, kPhaseA2, kPhaseA3};
+        for (int part = 1; part <= 3; ++part) {
+            if (!(phase & part_bit[part - 1]) || (part > 1 && !hkc::contact_multi(c))) continue;
+            hkc::prof_begin(c, HAKAI_K_CONTACT, &ep);
+            const int rc = hkc::contact_phase(c, part, t, d_time);
+            hkc::prof_end(c, &ep);
+            if (rc) return rc;
+        }
     }
-    if (!(phase & 2)) return 0;
+    if (!(phase & kPhaseRest)) return 0;
     const int par = c->cur;  // graph mode: this step reads counter slot 1-par, writes slot par
     // nodal update (:562-567), Q from the previous step's element forces (:668-675)
     hk::NodalArgs na;
@@ -1331,8 +1334,8 @@ static int step_once(hakai_ctx* c, double t, double d_time, bool last, int phase
         na.bc = ba;
     }
     int rc = 0;
-    if (c->contact) {  // divided multi-GPU search: event exchange and force sums
-        if (hkc::contact_divided(c)) {
+    if (c->contact) {  // multi-GPU search: event exchange and force sums
+        if (hkc::contact_multi(c)) {
             hkc::prof_begin(c, HAKAI_K_CONTACT_SUM, &ep);
             rc = hkc::contact_step_b(c);
             hkc::prof_end(c, &ep);
@@ -1483,6 +1486,7 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const Call
         int pz[2] = {0, 0};
         HIPCHK(hipMemcpy(pz, c->d_poison, sizeof pz, hipMemcpyDeviceToHost));
         if (pz[0]) {
+            c->poison_step = pz[1];
             const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
             if (good >= 0 && good <= n_steps) {
                 c->cur = (good & 1) ? 1 - s0.cur : s0.cur;
@@ -1508,16 +1512,27 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const Call
     return rc;
 }
 
+static int step_call(hakai_ctx* c, double t_first, int64_t n_steps, double d_time);
+static constexpr int kExchangeRetries = 8;
+
 int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (!c) return fail(HAKAI_ERR_ARG, "null");
     if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step before upload_model/reset_state");
     if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step: n_steps=%lld d_time=%g", (long long)n_steps, d_time);
     if (n_steps > 1 && hkc::comm_is_local(c))
         return fail(HAKAI_ERR_ARG, "step: an in-process group is stepped one step per call, rank by rank");
-    if (c->poison_halt)
-        return fail(HAKAI_ERR_STATE, "step: a multi-GPU contact buffer overflowed; the state is that of the last good "
-                    "step -- raise the capacity and hakai_upload_state / hakai_reset_state on every rank");
     HIPCHK(hipSetDevice(c->device));
+    // a step that overflowed a multi-GPU contact exchange runs again once its capacity has grown
+    // (every rank takes the same decision from the same gathered counts)
+    for (int attempt = 0;; ++attempt) {
+        const int rc = step_call(c, t_first, n_steps, d_time);
+        if (!rc || attempt >= kExchangeRetries || !hkc::contact_exchange_retry(c)) return rc;
+        n_steps -= (int64_t)(c->poison_step - (long long)t_first);
+        t_first = (double)c->poison_step;
+    }
+}
+
+static int step_call(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     (void)own_use(c);  // owner-assembly lists are built here, never inside a graph capture
     const CallSnap s0 = call_snap(c);
     int64_t it = 0;
@@ -1541,40 +1556,23 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     return finish_call(c, t_first, n_steps, s0);
 }
 
-int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
-    if (!ctxs || n <= 0) return fail(HAKAI_ERR_ARG, "step_group: no contexts");
-    if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step_group: n_steps=%lld d_time=%g",
-                                                  (long long)n_steps, d_time);
+static int step_group_call(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
     std::vector<CallSnap> s0(n);
-    for (int r = 0; r < n; ++r) {
-        hakai_ctx* c = ctxs[r];
-        if (!c) return fail(HAKAI_ERR_ARG, "step_group: null context %d", r);
-        if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step_group: rank %d has no model/state", r);
-        if (c->poison_halt)
-            return fail(HAKAI_ERR_STATE, "step_group: rank %d: a contact buffer overflowed; upload or reset the "
-                        "state on every rank", r);
-        if (n > 1 && (!c->comm || hkc::comm_rank(c) != r || hkc::comm_size(c) != n ||
-                      hkc::comm_peer_ctx(c, r) != c))
-            return fail(HAKAI_ERR_ARG, "step_group: context %d is not rank %d of an in-process group of %d", r, r, n);
-        hkc::graph_invalidate(c);
-    }
-    HIPCHK(hipSetDevice(ctxs[0]->device));
     for (int r = 0; r < n; ++r) {
         (void)own_use(ctxs[r]);  // (re-plans here, as hakai_step does, not inside the first step)
         s0[r] = call_snap(ctxs[r]);
     }
+    // per step: each contact part on every rank before the next part on any, then the rest
+    const int phases[4] = {kPhaseA1, kPhaseA2, kPhaseA3, kPhaseRest};
     for (int64_t it = 0; it < n_steps; ++it) {
         const double t = t_first + (double)it;
         const bool last = it == n_steps - 1;
-        for (int r = 0; r < n; ++r) {  // every rank's contact search before any rank's exchange
-            if (int rc = step_once(ctxs[r], t, d_time, last, 1)) return rc;
-            if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
-        }
-        for (int r = 0; r < n; ++r) {
-            if (int rc = step_once(ctxs[r], t, d_time, last, 2)) return rc;
-            ctxs[r]->tdev_next = -1;
-            if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
-        }
+        for (int ph : phases)
+            for (int r = 0; r < n; ++r) {
+                if (int rc = step_once(ctxs[r], t, d_time, last, ph)) return rc;
+                if (ph == kPhaseRest) ctxs[r]->tdev_next = -1;
+                if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
+            }
     }
     int first = 0;
     for (int r = 0; r < n; ++r) {
@@ -1582,6 +1580,32 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
         if (rc && !first) first = rc;
     }
     return first;
+}
+
+int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time) {
+    if (!ctxs || n <= 0) return fail(HAKAI_ERR_ARG, "step_group: no contexts");
+    if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step_group: n_steps=%lld d_time=%g",
+                                                  (long long)n_steps, d_time);
+    for (int r = 0; r < n; ++r) {
+        hakai_ctx* c = ctxs[r];
+        if (!c) return fail(HAKAI_ERR_ARG, "step_group: null context %d", r);
+        if (!c->model_ok || !c->state_ok) return fail(HAKAI_ERR_STATE, "step_group: rank %d has no model/state", r);
+        if (n > 1 && (!c->comm || hkc::comm_rank(c) != r || hkc::comm_size(c) != n ||
+                      hkc::comm_peer_ctx(c, r) != c))
+            return fail(HAKAI_ERR_ARG, "step_group: context %d is not rank %d of an in-process group of %d", r, r, n);
+        hkc::graph_invalidate(c);
+    }
+    HIPCHK(hipSetDevice(ctxs[0]->device));
+    for (int attempt = 0;; ++attempt) {
+        const int rc = step_group_call(ctxs, n, t_first, n_steps, d_time);
+        if (!rc || attempt >= kExchangeRetries) return rc;
+        bool retry = true;  // (the same on every rank: they read the same headers)
+        for (int r = 0; r < n; ++r) retry = hkc::contact_exchange_retry(ctxs[r]) && retry;
+        if (!retry) return rc;
+        const long long p = ctxs[0]->poison_step;
+        n_steps -= (int64_t)(p - (long long)t_first);
+        t_first = (double)p;
+    }
 }
 
 int hakai_graph_steps(hakai_ctx* c, int64_t* n) {

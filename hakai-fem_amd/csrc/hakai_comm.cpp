@@ -49,10 +49,7 @@ struct Comm {
     std::vector<int> h_dn;                       // host copy of d_dn (owner-computed assembly)
     bool pending = false;
     int pending_par = 0;
-    // all-gather of equal-size blocks (the contact mirror, hakai_contact.hip): per-parity send
-    // buffers registered by their owner, "packed" events recorded on the context's stream
-    void* ag_send[2] = {nullptr, nullptr};
-    hipEvent_t ev_ag[2] = {nullptr, nullptr};
+    // collectives of the multi-GPU contact (hakai_contact.hip) on cs, handed over by events
     hipEvent_t ev_ag_ready = nullptr, ev_ag_done = nullptr;
 };
 
@@ -268,8 +265,6 @@ int comm_common_init(hakai_ctx* c, hkc::Comm* m) {
     if (hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_packed[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_packed[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_ag[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_ag[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_ag_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_ag_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming) != hipSuccess) {
@@ -331,10 +326,8 @@ void comm_destroy(hakai_ctx* c) {
             delete m->group;
         }
     }
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < 2; ++p)
         if (m->ev_packed[p]) (void)hipEventDestroy(m->ev_packed[p]);
-        if (m->ev_ag[p]) (void)hipEventDestroy(m->ev_ag[p]);
-    }
     if (m->ev_ag_ready) (void)hipEventDestroy(m->ev_ag_ready);
     if (m->ev_ag_done) (void)hipEventDestroy(m->ev_ag_done);
     if (m->ev_done) (void)hipEventDestroy(m->ev_done);
@@ -344,55 +337,11 @@ void comm_destroy(hakai_ctx* c) {
 }
 
 bool comm_is_local(const hakai_ctx* c) {
-    return c->comm && c->comm->mode == 1 && (c->comm->n_up + c->comm->n_dn > 0 || c->comm->ag_send[0]);
+    return c->comm && c->comm->mode == 1 && (c->comm->n_up + c->comm->n_dn > 0 || c->contact);
 }
 
 int comm_rank(const hakai_ctx* c) { return c->comm ? c->comm->rank : 0; }
 int comm_size(const hakai_ctx* c) { return c->comm ? c->comm->nranks : 1; }
-
-int comm_gather_register(hakai_ctx* c, void* send0, void* send1) {
-    Comm* m = c->comm;
-    if (!m) return send0 ? fail(HAKAI_ERR_STATE, "all-gather without a communicator") : 0;
-    m->ag_send[0] = send0;
-    m->ag_send[1] = send1;
-    return 0;
-}
-
-int comm_gather_mark(hakai_ctx* c, int par) {
-    Comm* m = c->comm;
-    if (!m) return fail(HAKAI_ERR_STATE, "all-gather without a communicator");
-    HIPCHK(hipEventRecord(m->ev_ag[par], c->stream));
-    return 0;
-}
-
-// recv[q*bytes .. (q+1)*bytes) = rank q's send block of parity par, ordered on c->stream. RCCL runs
-// on the communicator's own stream, like the interface exchange, so every RCCL operation of a
-// rank is issued to ONE stream in one order (no cross-stream interleaving between ranks).
-int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes) {
-    Comm* m = c->comm;
-    if (!m || !m->ag_send[par]) return fail(HAKAI_ERR_STATE, "all-gather: no registered send buffer");
-    if (m->mode == 0) {
-        HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
-        HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
-        NCCLCHK(ncclAllGather(m->ag_send[par], recv, bytes, ncclUint8, m->nc, m->cs));
-        HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
-        HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
-        return 0;
-    }
-    // in-process group: pull every rank's block (the peers packed it at the end of their previous
-    // step, or at their state reset / set_contact_global; see hakai_contact.hip, "mirror")
-    if (m->nranks > kMaxLocalGather) return fail(HAKAI_ERR_COMM, "local group: more than %d ranks", kMaxLocalGather);
-    LocalGather g{};
-    for (int q = 0; q < m->nranks; ++q) {
-        Comm* p = q == m->rank ? m : peer(m, q);
-        if (!p || !p->ag_send[par]) return fail(HAKAI_ERR_COMM, "local group: rank %d has no contact mirror", q);
-        HIPCHK(hipStreamWaitEvent(c->stream, p->ev_ag[par], 0));
-        g.src[q] = (const char*)p->ag_send[par];
-        g.bytes[q] = (long long)bytes;
-        g.off[q] = (long long)q * (long long)bytes;
-    }
-    return gather_local(c, g, m->nranks, recv);
-}
 
 // RCCL only: recv[q*bytes .. (q+1)*bytes) = rank q's `send`, ordered on c->stream (the divided
 // contact search's per-step event exchange, hakai_contact.hip)
@@ -403,6 +352,20 @@ int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes)
     HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
     HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
     NCCLCHK(ncclAllGather(send, recv, bytes, ncclUint8, m->nc, m->cs));
+    HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
+    HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
+    return 0;
+}
+
+// RCCL only: recv = elementwise MIN over the ranks of send (uint64 words), ordered on c->stream
+// (the multi-GPU contact's pair boxes, hakai_contact.hip)
+int comm_allreduce_min_u64(hakai_ctx* c, const void* send, void* recv, size_t count) {
+    Comm* m = c->comm;
+    if (!m || m->mode != 0) return fail(HAKAI_ERR_STATE, "all-reduce: not an RCCL communicator");
+    if (count == 0) return 0;
+    HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
+    HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
+    NCCLCHK(ncclAllReduce(send, recv, count, ncclUint64, ncclMin, m->nc, m->cs));
     HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
     HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
     return 0;

@@ -50,95 +50,75 @@ struct PairParam {
     int pad;
 };
 
-// Multi-GPU contact (hakai_set_contact_global, §8f-3). Every rank keeps a mirror of the GLOBAL
-// contact model -- coordinates, connectivity, masses of the whole mesh (static), plus the
-// displacements of the contact nodes and the deletion state of the contact elements (per step) --
-// and runs the single-GPU kernels below on it, so every rank computes the same events and the same
-// correctly rounded nodal sums as one GPU: N ranks are bit-identical to one. Per step each rank
-// packs, for the contact nodes it owns (owner = rank of the lowest incident element) and its own
-// contact elements, one fixed-size block; the blocks are all-gathered (RCCL over xGMI, or device
-// copies in an in-process group) and scattered into the mirror. The block of step s is packed at
-// the end of step s-1 (or at the state reset, s = 0), so an in-process group stepped rank by rank
-// finds every peer's block ready. The triangle search is divided across the ranks (contact_divide,
-// the reference's triangle-parallel loop :2370, :2386, :2653-2667): rank r tests the candidate
-// triangles j with (j / 64) = r (mod N) and the events are all-gathered before the force sums
-// (DESIGN.md §5); the mirror all-gather, boxes, binning and bucket fill stay on every rank.
-// Two node sets travel: X0, the nodes of the entries live from the start (every step, owner
-// packs), and X1, the nodes only a deletion exposes. An X1 node is shipped by every rank that
-// deleted one of its adders (the adder contains the node, so that rank holds it), from the step
-// after that deletion on, together with its u_pre; X1 nodes travel in chunks of 64 (rank segment,
-// ascending global id), and a chunk is sent once any of its nodes is. Sender and receivers mark
-// chunks from the same deletion steps, so both sides agree on the slot order.
-// Block layout of one step's exchange (see the kernels, "multi-GPU mirror")
-struct MirLayout {
-    int capc = 0, capd = 0;  // X1 chunks, deletion-list entries
-    size_t off_u = 0, off_dl = 0, off_x1 = 0, blk_step = 0, off_upre = 0, off_v0 = 0, off_del = 0, off_x1v0 = 0,
-           blk_full = 0;
+// Multi-GPU contact (hakai_set_contact_global, §8f-3): owner-computed search. Every rank sets up
+// the contact model of the GLOBAL mesh (the same host enumeration, so the same entries, pairs and
+// hash tables on every rank) and keeps the entries it owns: the triangles of its own elements and
+// the node entries of the nodes it owns (owner = the rank of the node's lowest incident element),
+// with local node ids, so every position, velocity and element flag the search reads is local. Per
+// step (hkc::Xrank, "exchange" kernels below):
+//   A1  the previous step's deletions of every rank (global element, step) are all-gathered into a
+//       global deletion-step array (live lists: an entry's adders may sit on a neighbour rank);
+//       live-list update of the own entries; pair boxes over the own live node entries;
+//   A2  the partial boxes are combined (an all-reduce of min/max words, exact); the own live
+//       i-nodes inside the pair's range box are binned into compact 96-B records (cell, global
+//       node, position, velocity, the mass the damping term reads);
+//   A3  the records of every rank are gathered into one hash grid (count, scan, fill), and each
+//       rank tests its own candidate triangles (the reference's triangle-parallel loop :2370,
+//       per-thread force columns :2386) against every binned i-node: the same candidate set and the
+//       same FP64 expressions as one GPU;
+//   B   the events of all ranks are all-gathered and every rank forms the same order-independent
+//       double-double sums (:2653-2667, :511-517), then takes its own nodes' forces.
+// So N ranks are bit-identical to one, and nothing of the model's surface travels per step: only
+// deletions, the boxes, the binned contact-zone nodes and the events. Blocks are double-buffered by
+// step parity; an in-process group reads its peers' blocks directly (after a stream wait on their
+// "packed" events), RCCL all-gathers them. Block capacities (RCCL collectives need host-known
+// sizes) are the same on every rank and grow between steps from the counts every rank gathered
+// two steps earlier; a burst beyond a capacity poisons that step on every rank, and hakai_step
+// grows the capacity and runs the step again (contact_exchange_retry).
+// Exchange blocks of every rank: rank q's block at p[q] (RCCL receive buffer or in-process peer)
+constexpr int kMaxXRanks = 64;
+struct XBlk {
+    const char* p[kMaxXRanks];
 };
 
-struct Mirror {
+struct Xrank {
     int rank = 0, nranks = 1;
-    int maxx = 0, maxe = 0;           // block capacity: owned contact nodes, contact elements per rank
-    int nxo = 0, neo = 0;             // this rank's counts
-    int* d_xo = nullptr;              // [nxo] local node ids of the owned contact nodes (ascending global id)
-    int* d_eo = nullptr;              // [neo] local element ids of this rank's contact elements
-    int* d_xg = nullptr;              // [nranks*maxx] global node id of each block slot (-1: padding)
-    int* d_eg = nullptr;              // [nranks*maxe] global element id of each block slot (-1: padding)
-    int* d_g2l = nullptr;             // [nN global] local node id or -1
-    double* g_coord = nullptr;        // [nN][3] global mesh (static)
-    double* g_mass = nullptr;         // [nN]
-    int* g_conn = nullptr;            // [nE][8]
-    double* g_u[2] = {nullptr, nullptr};  // displacement of step s in g_u[s&1], of step s-1 in the other
-    int* g_flag = nullptr;            // [nE] 1 active, 0 deleted (derived from the deletion step)
-    int* g_del = nullptr;             // [nE+2] deletion step; [nE+1] last step with any deletion
-    double* g_fext = nullptr;         // [nN][3] contact force on the global node space
-    double* d_velo0_loc = nullptr;    // [nN local][3] velocity before the first step (packed at s = 0)
-    char* d_send[2] = {nullptr, nullptr};
-    char* d_recv = nullptr;           // [nranks] blocks
-    size_t send_bytes[2] = {0, 0}, recv_bytes = 0;
-    // layout of the block of step s in lay[s&1]: capacities grow between steps, identically on all
-    // ranks, from the needs every rank computes at the unpack two steps earlier (h_need ring)
-    MirLayout lay[2];
-    int* h_need = nullptr;            // pinned [4][2]: max X1 chunks, max deletions of the unpack of step s; [8] = 1
-    hipEvent_t ev_need[4] = {nullptr, nullptr, nullptr, nullptr};
-    long long seq = 0;                // step index since the last state reset (the block a step consumes)
-    // X1: entries j = (rank segment q, node), chunks of 64 entries inside a segment
-    int nx1 = 0, nchunk = 0, maxseg = 0, slot_cap = 0;  // entries, chunks (all ranks), largest segment, slot table
-    int* d_seg_chunk = nullptr;       // [nranks+1] first chunk of each rank's segment
-    int* d_chunk_first = nullptr;     // [nchunk] first entry
-    int* d_chunk_end = nullptr;       // [nchunk] one past the last entry
-    int* d_x1_gid = nullptr;          // [nx1] global node
-    int* d_x1_loc = nullptr;          // [nx1] local node of this rank's entries, else -1
-    int* d_x1_chunk = nullptr;        // [nx1] chunk of each entry
-    int *d_el2x_ptr = nullptr, *d_el2x = nullptr;  // global element -> X1 entries it is an adder of
-    int* d_chunk_flag = nullptr;      // [nchunk] 1 once the chunk travels
-    int* d_slot_chunk = nullptr;      // [nranks*capc] chunk of each block slot
-    int* d_counts = nullptr;          // [nranks] chunks each rank sends
-    int* d_x1ctl = nullptr;           // [4] new marks since the last slot scan, max chunks needed, -, -
-    int* d_last_del = nullptr;        // [neo] deletion step of own contact elements at the last pack
-    size_t off_x1 = 0, off_x1v0 = 0;  // X1 region (u, u_pre per slot entry); at s = 0 also velo0
-    // Divided search (tuning "contact_divide", default on): rank r searches the candidate
-    // triangles j with (j / 64) % nranks == r; the events of all ranks are all-gathered each step and
-    // every rank runs the same order-independent double-double sums, so the forces are unchanged.
-    int divide = 1;
-    bool div_step = false;            // the current step runs divided (set by phase A)
-    void* d_ev_send[2] = {nullptr, nullptr};  // [ev_cap] EvRec, this rank's events of step t in [t&1]
-                                      // (in-process peers copy them while this rank moves on)
-    long long ev_cap = 0;
-    int* d_evcnt = nullptr;           // [2][2] this rank's (event count, overflow) of step t in slot t & 1
-                                      // (double-buffered like d_ev_send: in-process peers read it)
-    int* d_evcnt_all = nullptr;       // [2 nranks] every rank's
-    int* h_evcnt = nullptr;           // pinned [4][2 nranks]: every rank's, read by the host two steps later
-    hipEvent_t ev_ag[4] = {nullptr, nullptr, nullptr, nullptr};  // h_evcnt slot s filled
-    long long ag_cap = 0;             // RCCL: event records per rank in the all-gather (grow-only, the same
-                                      // on every rank: decided from gathered counts)
-    long long ag_seq = 0;             // RCCL phase B calls (h_evcnt slot = ag_seq & 3)
-    hipEvent_t ev_evpacked = nullptr; // this rank's events packed (in-process peers wait on it)
-    char* d_ev_recv = nullptr;        // [nranks][max events of the step] EvRec
-    size_t ev_recv_bytes = 0;
-    long long ev_stride = 0;          // records per rank in d_ev_recv this step
-    int div_t = 0;                    // step number of the last phase A
-    long long div_seq = 0;            // divided phase A calls (equal on the ranks of a lockstep group)
+    long long E0 = 0, nEloc = 0, nN_g = 0, nE_g = 0;
+    int maxEloc = 1;                  // the largest rank's element count (full deletion blocks)
+    long long* d_eoff = nullptr;      // [nranks+1] element ranges
+    int* d_l2g = nullptr;             // [nN local] global node id
+    int* d_g2l = nullptr;             // [nN_g] local node id or -1
+    double* g_mass = nullptr;         // [nN_g] lumped node mass (diag_M[i] with a node id i, :2592)
+    int* g_del = nullptr;             // [nE_g + 2] deletion step; [nE_g + 1] last step with any deletion
+    double* g_fext = nullptr;         // [nN_g][3] contact force in the global node space (sums of phase B)
+    int* d_last_del = nullptr;        // [nEloc] local deletion steps at the last pack
+    // exchange blocks: int4 header (count, overflow, last deletion step, full) + records
+    static constexpr int kNx = 3;     // 0 deletions, 1 binned i-nodes, 2 events
+    char* d_send[kNx][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
+    size_t send_bytes[kNx] = {0, 0, 0};
+    char* d_recv[kNx] = {nullptr, nullptr, nullptr};   // RCCL: [nranks] blocks
+    size_t recv_bytes[kNx] = {0, 0, 0};
+    long long cap[kNx] = {0, 0, 0};   // records per rank block (the same on every rank)
+    long long cap_max[kNx] = {0, 0, 0};
+    hipEvent_t ev_sent[kNx][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
+    bool full_del = true;             // the next deletion block carries every local deletion step
+    // partial pair boxes of this rank, by parity (in-process peers read them), and the combined boxes
+    unsigned long long* d_box[2] = {nullptr, nullptr};
+    unsigned long long* d_boxg = nullptr;
+    hipEvent_t ev_box[2] = {nullptr, nullptr};
+    int* d_bq = nullptr;              // [nranks * cap[1]] bucket of each gathered i-node record
+    long long bq_len = 0;
+    int* d_xctl = nullptr;            // [0] exchange overflow bits of the current call (1 del, 2 bins, 4 events);
+                                      // [4 ..] the step's gathered counts [kNx][nranks]
+    XBlk xb_last[kNx] = {};           // the blocks of the current step (counts, overflow growth)
+    bool retry = false;               // the last poisoned call overflowed an exchange, now grown
+    int* h_cnt = nullptr;             // pinned [4][kNx][nranks] gathered counts, read two steps later
+    hipEvent_t ev_cnt[4] = {nullptr, nullptr, nullptr, nullptr};
+    long long seq = 0;                // steps since the last state reset: block parity, count ring
+    long long cnt_seq = 0;            // count-ring entries written
+    int t_a = 0;                      // step of the current phase A
+    long long phase_a = 0;            // phase-A3 calls (equal on the ranks of a lockstep group)
+    int par_a = 0;                    // parity of the blocks of the current step
 };
 
 // A hash-bucket entry: the i-node's cell, node id and position (coord + u of this step, the value
@@ -153,10 +133,24 @@ struct alignas(16) BEnt {
 };
 static_assert(sizeof(BEnt) == 64, "BEnt: four 16-B vectors");
 
+// What an event's force needs from its i-node besides the position: the velocity (d_disp / d_time
+// of the previous step, :628, or the initial velocity) and the mass the damping term reads
+// (diag_M[i] with the node id i, :2592). Formed by the binning (same expressions, same bits) and
+// kept beside the bucket list, so the search loads it only for an event.
+struct alignas(16) BVel {
+    double v[3], mq;
+};
+// A binned i-node as it travels between ranks (multi-GPU, A2 -> A3); pad of BEnt = the pair.
+struct alignas(16) BRec {
+    BEnt e;
+    BVel w;
+};
+static_assert(sizeof(BRec) == 96, "BRec: six 16-B vectors");
+
 struct Contact {
     // node / element space of the kernels: the context's own (one GPU) or the global mirror
     long long nN = 0, nE = 0;
-    Mirror* mir = nullptr;
+    Xrank* xr = nullptr;             // multi-GPU (hakai_set_contact_global), else null
     int npairs = 0;
     std::vector<PairParam> h_par;
     PairParam* d_par = nullptr;
@@ -193,8 +187,10 @@ struct Contact {
     // hash grid over i-nodes
     int htot = 0;
     int *d_bcnt = nullptr, *d_boff = nullptr, *d_qbucket = nullptr;
-    BEnt* d_blist = nullptr;
-    BEnt* d_qrec = nullptr;  // [n_ni] by live-list position: the binned i-node's cell and node (bin -> fill)
+    BEnt* d_blist = nullptr;        // [blist_cap] bucket lists
+    BVel* d_bvel = nullptr;         // [blist_cap] beside them
+    long long blist_cap = 0;
+    BRec* d_qrec = nullptr;  // [n_ni] by live-list position: the binned i-node (bin -> fill)
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
     // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
     bool small = false;
@@ -236,6 +232,8 @@ namespace {
 using hkc::Contact;
 using hkc::PairParam;
 using hkc::BEnt;
+using hkc::BRec;
+using hkc::BVel;
 
 constexpr int kB = 256;
 
@@ -378,12 +376,23 @@ struct StepIn {
     const double* u_pre;   // disp_pre
     const double* velo0;   // non-null before the first step
     double d_time;
-    const int* del_step;
+    const int* del_step;   // (multi-GPU: the global deletion steps)
     const int* flag;
     const int* conn;
-    const double* mass;
+    const double* mass;    // per node, indexed by global node id (multi-GPU: the global array)
+    const int* l2g;        // multi-GPU: local -> global node id (null: the ids are global)
     int t;
 };
+
+__device__ __forceinline__ int gid(const StepIn& s, int n) { return s.l2g ? s.l2g[n] : n; }
+
+// velocity of node n at the start of step t: the initial one before the first step, else d_disp /
+// d_time of the previous step (:628)
+__device__ __forceinline__ void velo(const StepIn& s, int n, double v[3]) {
+#pragma clang fp contract(off)
+    for (int c = 0; c < 3; ++c)
+        v[c] = s.velo0 ? s.velo0[3 * n + c] : (s.u[3 * n + c] - s.u_pre[3 * n + c]) / s.d_time;
+}
 
 __device__ __forceinline__ void pos(const StepIn& s, int n, double p[3]) {
 #pragma clang fp contract(off)
@@ -661,9 +670,23 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
 // cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts.
 // sb blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
 // vb = virtual block (segment vb / sb, part vb % sb); a launch of nseg * sb workgroups has one each
+// the hash record of live i-node nd (local id) of pair pr at position p inside the range box r
+__device__ __forceinline__ void bin_rec(const StepIn& s, const Range& r, const PairParam& pp, int pr, int nd,
+                                        const double p[3], BRec& e) {
+#pragma clang fp contract(off)
+    for (int d = 0; d < 3; ++d) e.e.m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
+    const int g = gid(s, nd);
+    e.e.node = g;
+    e.e.pad = pr;
+    for (int d = 0; d < 3; ++d) e.e.p[d] = p[d];
+    e.e.pad2 = 0.0;
+    velo(s, nd, e.w.v);
+    e.w.mq = s.mass[g / 3];  // diag_M[i] with the node id i (:2592)
+}
+
 __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* segs, const int* reg, const int* ni_live,
                                          const int* ni_pair, const int* ni_node, const PairParam* par,
-                                         const unsigned long long* bbox, int* qbucket, BEnt* qrec, int* bcnt,
+                                         const unsigned long long* bbox, int* qbucket, BRec* qrec, int* bcnt,
                                          int sb) {
 #pragma clang fp contract(off)
     const Seg sg = segs[vb / sb];
@@ -683,14 +706,10 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
             qbucket[base + q] = -1;
             continue;
         }
-        BEnt e;
-        for (int d = 0; d < 3; ++d) e.m[d] = (long long)ceil((p[d] - r.amn[d]) / pp.ddiv);
-        e.node = nd;
-        e.pad = 0;
-        for (int d = 0; d < 3; ++d) e.p[d] = p[d];
-        e.pad2 = 0.0;
+        BRec e;
+        bin_rec(s, r, pp, pr, nd, p, e);
         qrec[base + q] = e;  // coalesced by live position; the fill moves it into the bucket list
-        const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
+        const int b = pp.hash_off + (int)(hash3(e.e.m[0], e.e.m[1], e.e.m[2]) & (unsigned)(pp.hash_size - 1));
         qbucket[base + q] = b;
         atomicAdd(&bcnt[b], 1);
     }
@@ -698,7 +717,7 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
 
 __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                const int* ni_pair, const int* ni_node, const PairParam* par,
-                                               const unsigned long long* bbox, int* qbucket, BEnt* qrec,
+                                               const unsigned long long* bbox, int* qbucket, BRec* qrec,
                                                int* bcnt, int sb) {
     bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
 }
@@ -742,8 +761,8 @@ __device__ __forceinline__ void scan_small_body(const int* in, int* out, int n) 
 __global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) { scan_small_body(in, out, n); }
 
 __device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* reg, const int* ni_live,
-                                          const int* qbucket, const int* boff, int* bcnt, BEnt* blist, int sb,
-                                          const BEnt* qrec) {
+                                          const int* qbucket, const int* boff, int* bcnt, BEnt* blist, BVel* bvel,
+                                          int sb, const BRec* qrec) {
     const Seg sg = segs[vb / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
@@ -752,14 +771,15 @@ __device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* re
         const int b = qbucket[base + q];
         if (b < 0) continue;
         const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-        blist[slot] = qrec[base + q];
+        blist[slot] = qrec[base + q].e;
+        bvel[slot] = qrec[base + q].w;
     }
 }
 
 __global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* qbucket, const int* boff, int* bcnt, BEnt* blist, int sb,
-                                                const BEnt* qrec) {
-    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, sb, qrec);
+                                                const int* qbucket, const int* boff, int* bcnt, BEnt* blist,
+                                                BVel* bvel, int sb, const BRec* qrec) {
+    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, bvel, sb, qrec);
 }
 
 // wave-aggregated append: one atomic per wave; every lane of the wave must call it
@@ -834,14 +854,15 @@ __device__ __forceinline__ long long shard_slot(const unsigned* s_pre, long long
 // same bits), so the per-cell threads start from one load instead of a chain of dependent ones.
 struct TriRec {
     double q0[3], c[3], Rmax, n[3], vdet, im[9], kk;
+    double vj[3];  // velocity of the triangle's first node (the event's relative velocity, :2580-2582)
     long long mj[3];
-    int j0, j1, j2, eleid, pr;
+    int j0, j1, j2, eleid, pr;  // global node ids; eleid: the (local) element, for the self-contact test
     int hoff, hmask, self;  // the pair's hash region and self-contact flag (no parameter load in the search)
 };
 
 __device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam& pp, int nd0, int nd1, int nd2,
                                          int ele, const double q0[3], const double q1[3], const double q2[3],
-                                         TriRec& T) {
+                                         const double vj[3], TriRec& T) {
 #pragma clang fp contract(off)
     const double cx = (q0[0] + q1[0] + q2[0]) / 3.0, cy = (q0[1] + q1[1] + q2[1]) / 3.0,
                  cz = (q0[2] + q1[2] + q2[2]) / 3.0;
@@ -888,6 +909,9 @@ __device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam
     T.j1 = nd1;
     T.j2 = nd2;
     T.eleid = ele;
+    T.vj[0] = vj[0];
+    T.vj[1] = vj[1];
+    T.vj[2] = vj[2];
     T.pr = pr;
     T.hoff = pp.hash_off;
     T.hmask = pp.hash_size - 1;
@@ -895,28 +919,21 @@ __device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam
 }
 
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
-// side of the range box along any axis -> candidate record
-// (multi-GPU divided search: only the triangles j with (j / 64) % own_n == own_r -- runs of 64
-// consecutive ids, so a wave of the live list mostly belongs to one rank, and the contact zone's
-// triangles still spread over every rank)
+// side of the range box along any axis -> candidate record (multi-GPU: a rank's lists hold the
+// triangles of its own elements only)
 __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s, const int* tri_cnt,
                                                 const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                 const int* tri_ele, const PairParam* par,
                                                 const unsigned long long* bbox, unsigned int* ccnt, TriRec* cand,
-                                                long long cshard_cap, int own_r, int own_n) {
+                                                long long cshard_cap) {
     const int n = *tri_cnt;
     __shared__ unsigned s_app[2];
     for (int q0 = bid * blockDim.x; q0 < n; q0 += nb * blockDim.x) {  // block-uniform trip count
         const int q = q0 + (int)threadIdx.x;
-        // every load of an owned triangle unconditional (lanes past the end re-read the last
-        // entry), so the chain is three round trips -- live entry; its element, pair and nodes;
-        // flag, pair box, positions and pair parameters -- instead of one per test. A triangle
-        // another rank owns (divided search) loads nothing past its live entry: it re-reads the
-        // wave's first entry instead, whose lines the wave fetches anyway, so each rank moves about
-        // 1/N of the triangle data.
-        const int j0 = tri_live[q < n ? q : n - 1];
-        const bool mine = own_n <= 1 || (j0 >> 6) % own_n == own_r;
-        const int j = mine ? j0 : __shfl(j0, 0);
+        // every load unconditional (lanes past the end re-read the last entry), so the chain is
+        // three round trips -- live entry; its element, pair and nodes; flag, pair box, positions and
+        // pair parameters -- instead of one per test
+        const int j = tri_live[q < n ? q : n - 1];
         const int ele = tri_ele[j], pr = tri_pair[j];
         const int nd0 = tri_nodes[3 * j], nd1 = tri_nodes[3 * j + 1], nd2 = tri_nodes[3 * j + 2];
         const int fl = s.flag[ele];
@@ -926,7 +943,7 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
         pos(s, nd0, p0);
         pos(s, nd1, p1);
         pos(s, nd2, p2);
-        bool keep = q < n && mine && fl == 1 && !r.empty;  // own triangles only
+        bool keep = q < n && fl == 1 && !r.empty;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             keep &= !(p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]);
@@ -936,7 +953,9 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
         const unsigned slot = block_append(&ccnt[shard * kShardStride], keep, s_app);
         if (keep && (long long)slot < cshard_cap) {
             TriRec T;
-            tri_geom(pr, r, pp, nd0, nd1, nd2, ele, p0, p1, p2, T);
+            double vj[3];
+            velo(s, nd0, vj);
+            tri_geom(pr, r, pp, gid(s, nd0), gid(s, nd1), gid(s, nd2), ele, p0, p1, p2, vj, T);
             cand[shard * cshard_cap + slot] = T;
         }
     }
@@ -945,10 +964,9 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
 __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
                                                       const int* tri_pair, const int* tri_nodes, const int* tri_ele,
                                                       const PairParam* par, const unsigned long long* bbox,
-                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap,
-                                                      int own_r, int own_n) {
+                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap) {
     tri_filter_body(blockIdx.x, gridDim.x, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par, bbox, ccnt, cand,
-                    cshard_cap, own_r, own_n);
+                    cshard_cap);
 }
 
 // events of one thread, kept in registers and appended with one atomic per wave (a same-address
@@ -1000,8 +1018,9 @@ __device__ __forceinline__ BEnt ld_bent(const BEnt* e) {
 // i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
                                          int b, int part, int stride, const PairParam* par, const int* boff,
-                                         const BEnt* __restrict__ blist, double d_lim, double myu,
-                                         unsigned int* evn, long long cap, int* ev_nodes, double* ev_f, EvBuf& eb) {
+                                         const BEnt* __restrict__ blist, const BVel* __restrict__ bvel, double d_lim,
+                                         double myu, unsigned int* evn, long long cap, int* ev_nodes, double* ev_f,
+                                         EvBuf& eb) {
 #pragma clang fp contract(off)
     const int pr = rec->pr;
     const int sl0 = boff[b], sl1 = boff[b + 1];
@@ -1011,7 +1030,7 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
     if (self) {
         const int* cn = s.conn + 8 * (long long)rec->eleid;
 #pragma unroll
-        for (int a = 0; a < 8; ++a) own8[a] = cn[a];
+        for (int a = 0; a < 8; ++a) own8[a] = gid(s, cn[a]);
     }
     // the point-independent part of the test, held in registers for the whole bucket
     const double c0 = rec->c[0], c1 = rec->c[1], c2 = rec->c[2], Rmax = rec->Rmax;
@@ -1040,18 +1059,10 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
         if (!(0.0 <= x1 && 0.0 <= x2 && x1 + x2 <= 1.0 && d > 0.0 && d <= d_lim)) continue;
         const int j0 = rec->j0, j1 = rec->j1, j2 = rec->j2;
         const double nx = rec->n[0], ny = rec->n[1], nz = rec->n[2], kk = rec->kk;
-        // velo = d_disp / d_time of the previous step (:628); the IC before step 1
-        double vi[3], vj[3];
-        for (int c = 0; c < 3; ++c) {
-            if (s.velo0) {
-                vi[c] = s.velo0[3 * i + c];
-                vj[c] = s.velo0[3 * j0 + c];
-            } else {
-                vi[c] = (s.u[3 * i + c] - s.u_pre[3 * i + c]) / s.d_time;
-                vj[c] = (s.u[3 * j0 + c] - s.u_pre[3 * j0 + c]) / s.d_time;
-            }
-        }
-        const double vx = vi[0] - vj[0], vy = vi[1] - vj[1], vz = vi[2] - vj[2];
+        // velo = d_disp / d_time of the previous step (:628), the IC before step 1: formed by the
+        // binning (i) and the prefilter (j0)
+        const BVel w = bvel[sl];
+        const double vx = w.v[0] - rec->vj[0], vy = w.v[1] - rec->vj[1], vz = w.v[2] - rec->vj[2];
         const double mag_v = my3norm(vx, vy, vz);
         double vex = 0.0, vey = 0.0, vez = 0.0;
         if (mag_v > 0.0) {
@@ -1062,7 +1073,7 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
         const double F = kk * d;
         double fx = F * nx, fy = F * ny, fz = F * nz;
         // damping: diag_M[i] indexes the dof vector with a node id (:2592)
-        const double Cd = 2 * sqrt(s.mass[(i) / 3] * kk) * par[pr].Cr;
+        const double Cd = 2 * sqrt(w.mq * kk) * par[pr].Cr;
         const double fc_x = -Cd * vx, fc_y = -Cd * vy, fc_z = -Cd * vz;
         const double dot_ve_n = vex * nx + vey * ny + vez * nz;
         const double vsx = vex - dot_ve_n * nx, vsy = vey - dot_ve_n * ny, vsz = vez - dot_ve_n * nz;
@@ -1113,8 +1124,8 @@ __device__ __forceinline__ void ev_flush(const EvBuf& eb, int lane, unsigned int
 __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
                                                 const TriRec* cand, long long cshard_cap,
                                                 const PairParam* par, const int* boff, const BEnt* blist,
-                                                double d_lim, double myu, unsigned int* evs, long long shard_cap,
-                                                int* ev_nodes, double* ev_f) {
+                                                const BVel* bvel, double d_lim, double myu, unsigned int* evs,
+                                                long long shard_cap, int* ev_nodes, double* ev_f) {
     __shared__ unsigned s_cpre[kCandShards + 4];
     const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
@@ -1159,8 +1170,8 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
             dup |= c2 < cell && (half ? hi : lo) == hb;
         }
         if (valid && !dup)
-            tri_cell(s, rec, mj, hoff + (int)hb, 0, 1, par, boff, blist, d_lim, myu, evn, shard_cap, sh_nodes, sh_f,
-                         eb);
+            tri_cell(s, rec, mj, hoff + (int)hb, 0, 1, par, boff, blist, bvel, d_lim, myu, evn, shard_cap, sh_nodes,
+                     sh_f, eb);
         ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
 }
@@ -1188,12 +1199,11 @@ __device__ __forceinline__ long long shard_prefix(int bid, unsigned int* ctl, co
 // poisoned), so the state stays the last good step's and hakai_step reports the overflow.
 __device__ __forceinline__ void count_body(int bid, int nb, unsigned int* ctl, const unsigned int* evs,
                                            long long shard_cap, const int* ev_nodes, int* cnt, int* touched,
-                                           int* tpos, int tsel, int* poison, const int* x1ctl, int t,
-                                           const double* t_rd) {
+                                           int* tpos, int tsel, int* poison, int t, const double* t_rd) {
     __shared__ unsigned s_pre[kEvShards + 4];
     const long long n = 4 * shard_prefix(bid, ctl, evs, shard_cap, s_pre);
     if (bid == 0 && threadIdx.x == 0) {
-        const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
+        const bool over = ctl[kCandOver] != 0 || s_pre[kEvShards + 1];
         if (over && poison[0] == 0) {
             poison[1] = t_rd ? (int)*t_rd + 1 : t;
             poison[0] = 1;
@@ -1217,9 +1227,8 @@ __device__ __forceinline__ void count_body(int bid, int nb, unsigned int* ctl, c
 }
 
 __global__ void k_ct_count(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                           int* cnt, int* touched, int* tpos, int tsel, int* poison,
-                           const int* x1ctl, int t, const double* t_rd) {
-    count_body(blockIdx.x, gridDim.x, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, x1ctl, t, t_rd);
+                           int* cnt, int* touched, int* tpos, int tsel, int* poison, int t, const double* t_rd) {
+    count_body(blockIdx.x, gridDim.x, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, t, t_rd);
 }
 
 __device__ __forceinline__ void alloc_body(int bid, int nb, unsigned int* ctl, int tsel, const int* touched,
@@ -1336,10 +1345,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_prologue1(
 __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl, const unsigned int* evs,
                                                               long long shard_cap, const int* ev_nodes,
                                                               const double* ev_f, int* cnt, int* touched, int* tpos,
-                                                              int tsel, int* poison, const int* x1ctl, int t,
+                                                              int tsel, int* poison, int t,
                                                               const double* t_rd, int* toff, int* tcnt,
                                                               double* terms, double* fext) {
-    count_body(0, 1, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, x1ctl, t, t_rd);
+    count_body(0, 1, ctl, evs, shard_cap, ev_nodes, cnt, touched, tpos, tsel, poison, t, t_rd);
     __syncthreads();
     alloc_body(0, 1, ctl, tsel, touched, cnt, toff, tcnt);
     __syncthreads();
@@ -1352,7 +1361,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl,
 // only the pair boxes
 __global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                      const int* ni_pair, const int* ni_node, const PairParam* par,
-                                                     const unsigned long long* bbox, int* qbucket, BEnt* qrec,
+                                                     const unsigned long long* bbox, int* qbucket, BRec* qrec,
                                                      int* bcnt, int sb, int nbin, const int* tri_cnt,
                                                      const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                      const int* tri_ele, unsigned int* ccnt, TriRec* cand,
@@ -1361,28 +1370,39 @@ __global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, 
         bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
     else
         tri_filter_body(blockIdx.x - nbin, gridDim.x - nbin, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par,
-                        bbox, ccnt, cand, cshard_cap, 0, 1);
+                        bbox, ccnt, cand, cshard_cap);
 }
 
-// ---- divided multi-GPU search: event exchange ------------------------------------------------
+// ---- multi-GPU exchange (hkc::Xrank) --------------------------------------------------------
+// Every exchanged block is an int4 header -- (count, overflow, last deletion step, full) -- and its
+// records. Rank q's block is read through XBlk.p[q]: the RCCL-gathered receive buffer, or the
+// in-process peer's own send buffer (no copy).
+using hkc::kMaxXRanks;
+using hkc::XBlk;
+__device__ __forceinline__ int xhdr(const char* blk, int w) {
+    return __hip_atomic_load(reinterpret_cast<const int*>(blk) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr size_t kXHdr = 16;
+
 struct EvRec {
-    int n[4];     // i, j0, j1, j2
+    int n[4];     // i, j0, j1, j2 (global node ids)
     double f[3];  // force on i (the triangle nodes get -f/3 each)
 };
 
-// this rank's events of the step, shard order -> one compact record list; (count, overflow) for the
-// all-gather. Overflow = events beyond a shard, candidates beyond their buffer, or a truncated mirror
-// block: exchanged with the counts so every rank poisons the same step.
+// this rank's events of the step, shard order -> its block; overflow = events beyond a shard or
+// candidates beyond their buffer (poisons the step on every rank, k_ct_count_g)
 __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long shard_cap, const int* ev_nodes,
-                          const double* ev_f, EvRec* out, int* cnt_out, const int* x1ctl) {
+                          const double* ev_f, char* blk, long long cap) {
     __shared__ unsigned s_pre[kEvShards + 4];
     const long long n = shard_prefix(blockIdx.x, ctl, evs, shard_cap, s_pre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const bool over = ctl[kCandOver] != 0 || (x1ctl && x1ctl[1] != 0) || s_pre[kEvShards + 1];
-        cnt_out[0] = (int)n;
-        cnt_out[1] = over ? 1 : 0;
+        const bool over = ctl[kCandOver] != 0 || s_pre[kEvShards + 1];
+        int* h = reinterpret_cast<int*>(blk);
+        h[0] = (int)n;
+        h[1] = over ? 1 : 0;
     }
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+    EvRec* out = reinterpret_cast<EvRec*>(blk + kXHdr);
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n && e < cap;
          e += (long long)gridDim.x * blockDim.x) {
         const long long sl = shard_slot(s_pre, shard_cap, e);
         EvRec r;
@@ -1392,27 +1412,18 @@ __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long 
     }
 }
 
-constexpr int kMaxDivRanks = 64;  // divided search: ranks whose event offsets a block holds in LDS
-
-// every rank's (count, overflow) word pair, wherever it lives: the RCCL-gathered array, or the
-// in-process peers' own device words (read directly, no host round trip)
-struct CntPtrs {
-    const int* p[kMaxDivRanks];
-};
-
-// rank prefix of the gathered counts in LDS; block 0 publishes the total. A count beyond the
-// gathered rows (stride; the step is poisoned then, k_ct_count_g) is clamped to them, so no read
-// leaves its rank's rows.
-__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const CntPtrs& cp, int nr, long long* s_off,
-                                                 long long stride) {
+// rank prefix of the blocks' record counts in LDS (each clamped to the block capacity); block 0
+// publishes the event total
+__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const XBlk& xb, int nr, long long* s_off,
+                                                 long long cap, bool publish) {
     if (threadIdx.x == 0) {
         long long run = 0;
         for (int q = 0; q < nr; ++q) {
             s_off[q] = run;
-            run += min((long long)__hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), stride);
+            run += min((long long)xhdr(xb.p[q], 0), cap);
         }
         s_off[nr] = run;
-        if (blockIdx.x == 0) {
+        if (publish && blockIdx.x == 0) {
             ctl[kEv] = (unsigned)run;
             atomicMax(&ctl[kEvMax], (unsigned)run);
         }
@@ -1421,36 +1432,49 @@ __device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const CntPtr
     return s_off[nr];
 }
 
-__device__ __forceinline__ const EvRec* rank_ev(const EvRec* ev, long long stride, const long long* s_off, int nr,
-                                                long long E) {
+__device__ __forceinline__ int rank_of_rec(const long long* s_off, int nr, long long E) {
     int q = 0;
     while (q + 1 < nr && s_off[q + 1] <= E) ++q;
-    return ev + q * stride + (E - s_off[q]);
+    return q;
 }
 
-// (block 0 also poisons step pstep when any rank's buffers overflowed: every rank sees the same
-// words, so every rank poisons the same step)
-__global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long stride, CntPtrs cp, int nr, int* cnt,
-                             int* touched, int* tpos, int tsel, int* poison, int pstep) {
-    __shared__ long long s_off[kMaxDivRanks + 1];
-    __shared__ unsigned s_app[2];
+__device__ __forceinline__ const EvRec* rank_ev(const XBlk& xb, const long long* s_off, int nr, long long E) {
+    const int q = rank_of_rec(s_off, nr, E);
+    return reinterpret_cast<const EvRec*>(xb.p[q] + kXHdr) + (E - s_off[q]);
+}
+
+// any rank's block over its capacity or flagged: poison step pstep on every rank (all read the same
+// headers); xctl records which exchange (bit) for the retry
+__device__ __forceinline__ void x_overflow_check(const XBlk& xb, int nr, long long cap, int* poison, int pstep,
+                                                 int* xctl, int bit) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        bool over = false;
-        for (int q = 0; q < nr; ++q)
-            over |= __hip_atomic_load(cp.p[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-                    __hip_atomic_load(cp.p[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > stride;
-        if (over && poison[0] == 0) {
-            poison[1] = pstep;
-            poison[0] = 1;
+        bool local = false, over = false;  // a rank's own buffers overflowed / the exchange block
+        for (int q = 0; q < nr; ++q) {
+            local |= xhdr(xb.p[q], 1) != 0;
+            over |= (long long)xhdr(xb.p[q], 0) > cap;
+        }
+        if (over) atomicOr(xctl, bit);
+        if (over || local) {
+            if (poison[0] == 0) {
+                poison[1] = pstep;
+                poison[0] = 1;
+            }
         }
     }
-    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off, stride);
+}
+
+__global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, int* cnt, int* touched, int* tpos,
+                             int tsel, int* poison, int pstep, int* xctl) {
+    __shared__ long long s_off[kMaxXRanks + 1];
+    __shared__ unsigned s_app[2];
+    x_overflow_check(xb, nr, cap, poison, pstep, xctl, 4);
+    const long long n = 4 * rank_prefix(ctl, xb, nr, s_off, cap, true);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
         bool first = false;
         if (e < n) {
-            node = rank_ev(ev, stride, s_off, nr, e >> 2)->n[e & 3];
+            node = rank_ev(xb, s_off, nr, e >> 2)->n[e & 3];
             first = atomicAdd(&cnt[node], 1) == 0;
         }
         const unsigned q = block_append(&ctl[kTouched + tsel], first, s_app);
@@ -1461,14 +1485,14 @@ __global__ void k_ct_count_g(unsigned int* ctl, const EvRec* ev, long long strid
     }
 }
 
-__global__ void k_ct_scatter_g(const EvRec* ev, long long stride, CntPtrs cp, int nr, unsigned int* ctl,
-                               const int* toff, const int* tpos, int* cnt, double* terms) {
+__global__ void k_ct_scatter_g(XBlk xb, long long cap, int nr, unsigned int* ctl, const int* toff, const int* tpos,
+                               int* cnt, double* terms) {
 #pragma clang fp contract(off)
-    __shared__ long long s_off[kMaxDivRanks + 1];
-    const long long n = 4 * rank_prefix(ctl, cp, nr, s_off, stride);
+    __shared__ long long s_off[kMaxXRanks + 1];
+    const long long n = 4 * rank_prefix(ctl, xb, nr, s_off, cap, false);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const EvRec* r = rank_ev(ev, stride, s_off, nr, e >> 2);
+        const EvRec* r = rank_ev(xb, s_off, nr, e >> 2);
         const int role = (int)(e & 3);
         const int node = r->n[role];
         const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
@@ -1485,232 +1509,150 @@ __global__ void k_ct_scatter_g(const EvRec* ev, long long stride, CntPtrs cp, in
     }
 }
 
-// in-process group: every peer's packed events (count read on the device) into rank q's stride
-// slot of dst, one row of workgroups per peer; 40-B records as five 8-B words
-struct PeerEv {
-    const EvRec* src[kMaxDivRanks];
-    const int* cnt[kMaxDivRanks];
-};
-
-__global__ void k_ev_gather_peers(PeerEv pe, long long stride, EvRec* dst) {
-    const int q = (int)blockIdx.y;
-    const long long n = min((long long)__hip_atomic_load(pe.cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), stride);
-    const unsigned long long* a = reinterpret_cast<const unsigned long long*>(pe.src[q]);
-    unsigned long long* b = reinterpret_cast<unsigned long long*>(dst + q * stride);
-    static_assert(sizeof(EvRec) == 40, "EvRec: five 8-B words");
-    for (long long w = blockIdx.x * (long long)blockDim.x + threadIdx.x; w < 5 * n; w += (long long)gridDim.x * blockDim.x)
-        b[w] = a[w];
-}
-
-// ---- multi-GPU mirror (see hkc::Mirror) -----------------------------------------------------
-// Block of one rank (bytes; regions 8-byte aligned). Every block: header int[4] = (last deletion
-// step, entries in the deletion list, -, -), X0 u, the deletion list (global element, step) of the
-// previous step, X1 slots (u, u_pre). Blocks of step 0 (after a state reset) add X0 u_pre and
-// velo0, the deletion step of every contact element, and X1 velo0.
-using hkc::MirLayout;
-
-struct X1Map {
-    const int *el2x_ptr, *el2x, *x1_chunk;
-    int* chunk_flag;
-    int* x1ctl;  // [0] new marks since the last slot scan, [1] overflow bits, [2] max X1 chunks, [3] max deletions
-};
-
-// a deleted element's X1 entries: their chunks travel from now on
-__device__ __forceinline__ void x1_mark(const X1Map& X, int e) {
-    const int a0 = X.el2x_ptr[e], a1 = X.el2x_ptr[e + 1];
-    for (int a = a0; a < a1; ++a) X.chunk_flag[X.x1_chunk[X.el2x[a]]] = 1;
-    if (a1 > a0) X.x1ctl[0] = 1;
-}
-
-// this rank's block (header zeroed before): u of the owned X0 nodes; own contact elements deleted
-// since the last pack go to the deletion list and mark their X1 chunks; with `full` also u_pre,
-// velo0 and every contact element's deletion step.
-__global__ void k_mir_pack(const int* xo, int nxo, const int* eo, int neo, const double* u, const double* upre,
-                           const double* velo0, const int* del_step, const int* del_any, char* blk, MirLayout L,
-                           int full, int* last_del, int elem_off, X1Map X) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int* hdr = reinterpret_cast<int*>(blk);
-    if (i == 0) hdr[0] = *del_any;
-    if (i < nxo) {
-        const long long n = xo[i];
-        double* pu = reinterpret_cast<double*>(blk + L.off_u) + 3 * (long long)i;
-        for (int c = 0; c < 3; ++c) pu[c] = u[3 * n + c];
+// deletions of this rank since the last pack -> its block (global element, step); full: every local
+// deletion step (after a state reset / upload / overflow); the header carries the rank's last
+// deletion step
+__global__ void k_xr_dpack(const int* del_step, const int* del_any, int nEloc, long long E0, int* last_del, char* blk,
+                           long long cap, int full) {
+    int* h = reinterpret_cast<int*>(blk);
+    int* pl = reinterpret_cast<int*>(blk + kXHdr);
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nEloc; e += gridDim.x * blockDim.x) {
+        const int d = del_step[e];
         if (full) {
-            double* pp = reinterpret_cast<double*>(blk + L.off_upre) + 3 * (long long)i;
-            double* pv = reinterpret_cast<double*>(blk + L.off_v0) + 3 * (long long)i;
-            for (int c = 0; c < 3; ++c) {
-                pp[c] = upre[3 * n + c];
-                pv[c] = velo0 ? velo0[3 * n + c] : 0.0;
+            pl[e] = d;
+        } else if (d != last_del[e]) {
+            const int k = atomicAdd(&h[0], 1);
+            if (k < cap) {
+                pl[2 * k] = (int)(E0 + e);
+                pl[2 * k + 1] = d;
             }
         }
+        last_del[e] = d;
     }
-    if (i < neo) {
-        const int d = del_step[eo[i]];
-        if (full) reinterpret_cast<int*>(blk + L.off_del)[i] = d;
-        if (d != 0 && last_del[i] == 0) {
-            x1_mark(X, eo[i] + elem_off);
-            if (!full) {
-                const int k = atomicAdd(&hdr[1], 1);
-                if (k < L.capd) {
-                    int* dl = reinterpret_cast<int*>(blk + L.off_dl) + 2 * (long long)k;
-                    dl[0] = eo[i] + elem_off;
-                    dl[1] = d;
-                } else {
-                    atomicOr(&X.x1ctl[1], 2);
-                }
-            }
-        }
-        last_del[i] = d;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        h[2] = *del_any;
+        h[3] = full;
     }
 }
 
-// all ranks' blocks -> the mirror. Slots are disjoint (one owner per node, one rank per element).
-__global__ void k_mir_unpack(const char* recv, size_t blk, int nranks, int maxx, int maxe, const int* xg,
-                             const int* eg, MirLayout L, int full, double* gu, double* gupre, double* gvelo0,
-                             int* gdel, int* gflag, long long nE, X1Map X) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i < (long long)nranks * maxx) {
-        const int g = xg[i];
-        if (g >= 0) {
-            const int q = (int)(i / maxx), k = (int)(i % maxx);
-            const char* b = recv + (size_t)q * blk;
-            const double* pu = reinterpret_cast<const double*>(b + L.off_u) + 3 * (long long)k;
-            for (int c = 0; c < 3; ++c) gu[3 * (long long)g + c] = pu[c];
-            if (full) {
-                const double* pp = reinterpret_cast<const double*>(b + L.off_upre) + 3 * (long long)k;
-                const double* pv = reinterpret_cast<const double*>(b + L.off_v0) + 3 * (long long)k;
-                for (int c = 0; c < 3; ++c) {
-                    gupre[3 * (long long)g + c] = pp[c];
-                    gvelo0[3 * (long long)g + c] = pv[c];
-                }
+// every rank's deletion block -> the global deletion steps; block 0 also the global last deletion
+// step and the overflow check (a list beyond its capacity poisons the step; it is packed again,
+// full, for the retry)
+__global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del, long long nE_g,
+                             int* poison, int pstep, int* xctl) {
+    const int q = (int)blockIdx.y;
+    const char* b = xb.p[q];
+    const int* pl = reinterpret_cast<const int*>(b + kXHdr);
+    if (xhdr(b, 3)) {
+        const long long e0 = e_off[q], ne = e_off[q + 1] - e0;
+        for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < ne; k += (long long)gridDim.x * blockDim.x)
+            g_del[e0 + k] = pl[k];
+    } else {
+        const long long n = min((long long)xhdr(b, 0), cap);
+        for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+            g_del[pl[2 * k]] = pl[2 * k + 1];
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        int mx = 0;
+        bool over = false;
+        for (int r = 0; r < nr; ++r) {
+            mx = max(mx, xhdr(xb.p[r], 2));
+            over |= !xhdr(xb.p[r], 3) && (long long)xhdr(xb.p[r], 0) > cap;
+        }
+        g_del[nE_g + 1] = mx;
+        if (over) {
+            atomicOr(xctl, 1);
+            if (poison[0] == 0) {
+                poison[1] = pstep;
+                poison[0] = 1;
             }
         }
-    }
-    if (full) {
-        if (i < (long long)nranks * maxe) {
-            const int e = eg[i];
-            if (e >= 0) {
-                const int q = (int)(i / maxe), k = (int)(i % maxe);
-                const int d = reinterpret_cast<const int*>(recv + (size_t)q * blk + L.off_del)[k];
-                if (d != 0 && gdel[e] == 0) x1_mark(X, e);
-                gdel[e] = d;
-                gflag[e] = d == 0 ? 1 : 0;
-            }
-        }
-    } else if (i < (long long)nranks * L.capd) {
-        const int q = (int)(i / L.capd), k = (int)(i % L.capd);
-        const char* b = recv + (size_t)q * blk;
-        if (k < min(reinterpret_cast<const int*>(b)[1], L.capd)) {
-            const int* dl = reinterpret_cast<const int*>(b + L.off_dl) + 2 * (long long)k;
-            const int e = dl[0], d = dl[1];
-            if (gdel[e] == 0) x1_mark(X, e);
-            gdel[e] = d;
-            gflag[e] = 0;
-        }
-    }
-    if (i == 0) {
-        int mx = 0, nd = 0;
-        for (int q = 0; q < nranks; ++q) {
-            const int* h = reinterpret_cast<const int*>(recv + (size_t)q * blk);
-            mx = max(mx, h[0]);
-            nd = max(nd, h[1]);
-        }
-        gdel[nE + 1] = mx;
-        X.x1ctl[3] = nd;
     }
 }
 
-// X1 slots: the marked chunks of ranks q0..q1-1 in ascending chunk order (one block; skipped when
-// nothing was marked since the last all-rank scan). counts[q] = chunks rank q sends; more than capc is an
-// overflow, recorded in x1ctl[1] and reported by contact_check.
-__global__ __launch_bounds__(1024) void k_x1_slots(int q0, int q1, const int* seg_chunk, const int* chunk_flag,
-                                                   int* slot_chunk, int capc, int* counts, int* x1ctl,
-                                                   int record) {
-    if (x1ctl[0] == 0) return;
-    int need = 0;
-    __shared__ int s_w[1024 / 64];
-    for (int q = q0; q < q1; ++q) {  // each thread a contiguous run of the segment: one block scan
-        const int c0 = seg_chunk[q], c1 = seg_chunk[q + 1];
-        const int run = (c1 - c0 + (int)blockDim.x - 1) / (int)blockDim.x;
-        const int b0 = min(c0 + (int)threadIdx.x * run, c1), b1 = min(b0 + run, c1);
-        int f = 0;
-        for (int c = b0; c < b1; ++c) f += chunk_flag[c] != 0;
-        int tot;
-        int slot = block_excl_scan(f, s_w, tot);
-        for (int c = b0; c < b1 && f > 0; ++c)
-            if (chunk_flag[c] != 0) {
-                if (slot < capc) slot_chunk[(long long)q * capc + slot] = c;
-                ++slot;
-                --f;
-            }
-        if (threadIdx.x == 0) {
-            counts[q] = tot;
-            if (tot > capc) x1ctl[1] |= 1;
-        }
-        need = max(need, tot);
-    }
-    __syncthreads();
-    // only the unpack's scan over all ranks clears the flag and records the need (the same on every
-    // rank): a pack-time scan of the own segment leaves the other segments' tables to it, which
-    // matters when a capacity change moved the table stride
-    if (threadIdx.x == 0 && record) {
-        x1ctl[0] = 0;
-        x1ctl[2] = need;
-    }
+// pair boxes of all ranks: min of the min words, max of the max words (exact, order-free). RCCL
+// all-reduces with MIN: the max words travel complemented (k_xr_boxflip before and after).
+__global__ void k_xr_boxflip(unsigned long long* bb, int n) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n && ((q % 12) / 3) % 2 == 1) bb[q] = ~bb[q];
 }
-
-struct X1Slots {
-    const int *counts, *slot_chunk, *chunk_first, *chunk_end;
-    int capc;
+struct XBox {
+    const unsigned long long* p[kMaxXRanks];
 };
-
-__device__ __forceinline__ int x1_entry(const X1Slots& S, int q, long long i, int& slot) {
-    slot = (int)(i >> 6);
-    if (slot >= min(S.counts[q], S.capc)) return -1;
-    const int c = S.slot_chunk[(long long)q * S.capc + slot];
-    const int j = S.chunk_first[c] + (int)(i & 63);
-    return j < S.chunk_end[c] ? j : -1;
+__global__ void k_xr_boxcomb(XBox xb, int nr, int n, unsigned long long* out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const bool mx = ((q % 12) / 3) % 2 == 1;
+    unsigned long long v = xb.p[0][q];
+    for (int r = 1; r < nr; ++r) {
+        const unsigned long long w = xb.p[r][q];
+        v = mx ? umax64(v, w) : umin64(v, w);
+    }
+    out[q] = v;
 }
 
-// this rank's X1 slots: u and u_pre (and velo0 at s = 0) of every node of its marked chunks
-__global__ void k_x1_pack(int rank, X1Slots S, const int* x1_loc, const double* u, const double* upre,
-                          const double* velo0, char* blk, size_t off_x1, size_t off_x1v0, int full) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    int slot;
-    const int j = x1_entry(S, rank, i, slot);
-    if (j < 0) return;
-    const long long n = x1_loc[j];
-    const long long o = 64LL * slot + (i & 63);
-    double* p = reinterpret_cast<double*>(blk + off_x1) + 6 * o;
-    for (int c = 0; c < 3; ++c) {
-        p[c] = u[3 * n + c];
-        p[3 + c] = upre[3 * n + c];
-    }
-    if (full) {
-        double* v = reinterpret_cast<double*>(blk + off_x1v0) + 3 * o;
-        for (int c = 0; c < 3; ++c) v[c] = velo0 ? velo0[3 * n + c] : 0.0;
+// A2: this rank's live i-nodes inside their pair's range box -> compact records in its block
+__global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                               const int* ni_pair, const int* ni_node, const PairParam* par,
+                                               const unsigned long long* bbox, char* blk, long long cap, int sb) {
+#pragma clang fp contract(off)
+    __shared__ unsigned s_app[2];
+    const Seg sg = segs[blockIdx.x / sb];
+    if (sg.side != 0) return;  // block-uniform
+    const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
+    unsigned int* cnt = reinterpret_cast<unsigned int*>(blk);
+    BRec* out = reinterpret_cast<BRec*>(blk + kXHdr);
+    for (int q0 = (blockIdx.x % sb) * kB; q0 < n; q0 += sb * kB) {  // block-uniform trip count
+        const int q = q0 + (int)threadIdx.x;
+        bool in = false;
+        int nd = 0, pr = 0;
+        double p[3] = {0.0, 0.0, 0.0};
+        Range r;
+        r.empty = true;
+        if (q < n) {
+            const int k = ni_live[base + q];
+            pr = ni_pair[k];
+            r = pair_range(bbox + 12 * pr);
+            nd = ni_node[k];
+            pos(s, nd, p);
+            in = !(r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] ||
+                   p[1] > r.mx[1] || p[2] > r.mx[2]);  // the candidate test of :2514-2519
+        }
+        const unsigned slot = block_append(cnt, in, s_app);
+        if (in && (long long)slot < cap) {
+            BRec e;
+            bin_rec(s, r, par[pr], pr, nd, p, e);
+            out[slot] = e;
+        }
     }
 }
 
-__global__ void k_x1_unpack(const char* recv, size_t blk, int nranks, X1Slots S, const int* x1_gid, size_t off_x1,
-                            size_t off_x1v0, int full, double* gu, double* gupre, double* gvelo0) {
-    const long long per = 64LL * S.capc;
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= per * nranks) return;
-    const int q = (int)(i / per);
-    int slot;
-    const int j = x1_entry(S, q, i % per, slot);
-    if (j < 0) return;
-    const long long g = x1_gid[j];
-    const long long o = 64LL * slot + (i & 63);
-    const double* p = reinterpret_cast<const double*>(recv + (size_t)q * blk + off_x1) + 6 * o;
-    for (int c = 0; c < 3; ++c) {
-        gu[3 * g + c] = p[c];
-        gupre[3 * g + c] = p[3 + c];
+// A3: bucket of every gathered record (ranks in order) and the bucket counts; xctl bit 2 and the
+// poison when a rank binned more than its block holds
+__global__ void k_xr_bcount(XBlk xb, int nr, long long cap, const PairParam* par, int* bq, int* bcnt, int* poison,
+                            int pstep, int* xctl) {
+    x_overflow_check(xb, nr, cap, poison, pstep, xctl, 2);
+    const int q = (int)blockIdx.y;
+    const long long n = min((long long)xhdr(xb.p[q], 0), cap);
+    const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+        const BEnt& e = rec[k].e;
+        const PairParam& pp = par[e.pad];
+        const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
+        bq[q * cap + k] = b;
+        atomicAdd(&bcnt[b], 1);
     }
-    if (full) {
-        const double* v = reinterpret_cast<const double*>(recv + (size_t)q * blk + off_x1v0) + 3 * o;
-        for (int c = 0; c < 3; ++c) gvelo0[3 * g + c] = v[c];
+}
+
+__global__ void k_xr_fill(XBlk xb, long long cap, const int* bq, const int* boff, int* bcnt, BEnt* blist, BVel* bvel) {
+    const int q = (int)blockIdx.y;
+    const long long n = min((long long)xhdr(xb.p[q], 0), cap);
+    const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+        const int b = bq[q * cap + k];
+        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
+        blist[slot] = rec[k].e;
+        bvel[slot] = rec[k].w;
     }
 }
 
@@ -1866,124 +1808,162 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_el_tri_ptr); dfree(C->d_el_tri); dfree(C->d_el_ni_ptr); dfree(C->d_el_ni); dfree(C->d_el_nj_ptr);
     dfree(C->d_el_nj); dfree(C->d_dlist);
     dfree(C->d_ni_live); dfree(C->d_nj_live); dfree(C->d_tri_live);
-    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_qbucket); dfree(C->d_qrec);
+    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_bvel); dfree(C->d_qbucket); dfree(C->d_qrec);
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt);
     if (C->d_tmp) (void)hipFree(C->d_tmp);
-    if (Mirror* M = C->mir) {
-        (void)comm_gather_register(c, nullptr, nullptr);
-        dfree(M->d_xo); dfree(M->d_eo); dfree(M->d_xg); dfree(M->d_eg); dfree(M->d_g2l);
-        dfree(M->g_coord); dfree(M->g_mass); dfree(M->g_conn); dfree(M->g_u[0]); dfree(M->g_u[1]);
-        dfree(M->g_flag); dfree(M->g_del); dfree(M->g_fext); dfree(M->d_velo0_loc);
-        dfree(M->d_send[0]); dfree(M->d_send[1]); dfree(M->d_recv);
-        dfree(M->d_seg_chunk); dfree(M->d_chunk_first); dfree(M->d_chunk_end); dfree(M->d_x1_gid); dfree(M->d_x1_loc);
-        dfree(M->d_x1_chunk); dfree(M->d_el2x_ptr); dfree(M->d_el2x); dfree(M->d_chunk_flag); dfree(M->d_slot_chunk);
-        dfree(M->d_counts); dfree(M->d_x1ctl); dfree(M->d_last_del);
-        for (void* p : M->d_ev_send)
-            if (p) (void)hipFree(p);
-        dfree(M->d_evcnt); dfree(M->d_evcnt_all); dfree(M->d_ev_recv);
-        if (M->h_evcnt) (void)hipHostFree(M->h_evcnt);
-        if (M->ev_evpacked) (void)hipEventDestroy(M->ev_evpacked);
-        if (M->h_need) (void)hipHostFree(M->h_need);
-        for (auto& e : M->ev_need)
+    if (Xrank* X = C->xr) {
+        (void)hipDeviceSynchronize();  // in-process peers may still read this rank's blocks
+        dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->g_fext); dfree(X->d_last_del);
+        for (int x = 0; x < Xrank::kNx; ++x) {
+            dfree(X->d_send[x][0]);
+            dfree(X->d_send[x][1]);
+            dfree(X->d_recv[x]);
+            for (auto& e : X->ev_sent[x])
+                if (e) (void)hipEventDestroy(e);
+        }
+        dfree(X->d_box[0]); dfree(X->d_box[1]); dfree(X->d_boxg); dfree(X->d_bq); dfree(X->d_xctl);
+        for (auto& e : X->ev_box)
             if (e) (void)hipEventDestroy(e);
-        for (auto& e : M->ev_ag)
+        for (auto& e : X->ev_cnt)
             if (e) (void)hipEventDestroy(e);
-        delete M;
+        if (X->h_cnt) (void)hipHostFree(X->h_cnt);
+        delete X;
     }
     delete C;
     c->contact = nullptr;
     dfree(c->d_fext);
 }
 
-static X1Map x1map(Mirror* M) { return X1Map{M->d_el2x_ptr, M->d_el2x, M->d_x1_chunk, M->d_chunk_flag, M->d_x1ctl}; }
-static X1Slots x1slots(Mirror* M, const MirLayout& L) {
-    return X1Slots{M->d_counts, M->d_slot_chunk, M->d_chunk_first, M->d_chunk_end, L.capc};
+// ---- multi-GPU exchange (Xrank) ------------------------------------------------------------------
+static size_t xr_rec_bytes(int x) { return x == 0 ? 8 : (x == 1 ? sizeof(BRec) : sizeof(EvRec)); }
+// block bytes of exchange x at the current capacity (deletions: also room for a full block)
+static size_t xr_blk(const Xrank* X, int x, bool full = false) {
+    size_t b = kXHdr + xr_rec_bytes(x) * (size_t)X->cap[x];
+    if (x == 0 && full) b = kXHdr + 4 * (size_t)X->maxEloc;
+    return (b + 15) / 16 * 16;
+}
+static size_t xr_alloc_blk(const Xrank* X, int x) {
+    return x == 0 ? std::max(xr_blk(X, 0, false), xr_blk(X, 0, true)) : xr_blk(X, x);
 }
 
-// block layout for the capacities (bytes, 8-byte aligned regions)
-static MirLayout mir_layout(const Mirror* M, int capc, int capd) {
-    MirLayout L;
-    L.capc = capc;
-    L.capd = capd;
-    L.off_u = 16;
-    L.off_dl = L.off_u + 24 * (size_t)M->maxx;
-    L.off_x1 = L.off_dl + 8 * (size_t)capd;
-    L.blk_step = L.off_x1 + 48 * 64 * (size_t)capc;
-    L.off_upre = L.blk_step;
-    L.off_v0 = L.off_upre + 24 * (size_t)M->maxx;
-    L.off_del = L.off_v0 + 24 * (size_t)M->maxx;
-    L.off_x1v0 = L.off_del + (4 * (size_t)M->maxe + 7) / 8 * 8;
-    L.blk_full = L.off_x1v0 + 24 * 64 * (size_t)capc;
-    return L;
+// send (both parities) and receive buffers for the current capacities; bucket-record and
+// bucket-list arrays for the binned records of all ranks
+static int xr_buffers(hakai_ctx* c) {
+    Contact* C = c->contact;
+    Xrank* X = C->xr;
+    bool sync = false;
+    for (int x = 0; x < Xrank::kNx; ++x)
+        sync |= X->send_bytes[x] < xr_alloc_blk(X, x) || (comm_is_rccl(c) && X->recv_bytes[x] < (size_t)X->nranks * xr_alloc_blk(X, x));
+    sync |= X->bq_len < (long long)X->nranks * X->cap[1] || C->blist_cap < (long long)X->nranks * X->cap[1];
+    if (!sync) return 0;
+    HIPCHK(hipDeviceSynchronize());  // (in-process peers read the send blocks)
+    for (int x = 0; x < Xrank::kNx; ++x) {
+        const size_t b = xr_alloc_blk(X, x);
+        if (X->send_bytes[x] < b) {
+            for (int p = 0; p < 2; ++p) {
+                dfree(X->d_send[x][p]);
+                HIPCHK(dalloc(&X->d_send[x][p], b));
+                HIPCHK(hipMemset(X->d_send[x][p], 0, b));
+            }
+            X->send_bytes[x] = b;
+        }
+        if (comm_is_rccl(c) && X->recv_bytes[x] < (size_t)X->nranks * b) {
+            dfree(X->d_recv[x]);
+            HIPCHK(dalloc(&X->d_recv[x], (size_t)X->nranks * b));
+            X->recv_bytes[x] = (size_t)X->nranks * b;
+        }
+    }
+    const long long nb = (long long)X->nranks * X->cap[1];
+    if (X->bq_len < nb) {
+        dfree(X->d_bq);
+        HIPCHK(dalloc(&X->d_bq, (size_t)nb));
+        X->bq_len = nb;
+    }
+    if (C->blist_cap < nb) {
+        dfree(C->d_blist);
+        dfree(C->d_bvel);
+        HIPCHK(dalloc(&C->d_blist, (size_t)nb));
+        HIPCHK(dalloc(&C->d_bvel, (size_t)nb));
+        C->blist_cap = nb;
+    }
+    // the "current step" block pointers (counts, overflow growth) may name freed blocks: point them
+    // at this rank's own (valid, possibly empty) blocks until the next exchange sets them
+    for (int x = 0; x < Xrank::kNx; ++x)
+        for (int q = 0; q < X->nranks; ++q) X->xb_last[x].p[q] = X->d_send[x][0];
+    return 0;
 }
 
-// buffers for the layout of parity par: its send block, the receive blocks, the slot table. A
-// grown slot table is rebuilt by the next scan (marked stale).
-static int mir_buffers(hakai_ctx* c, int par) {
-    Mirror* M = c->contact->mir;
-    const MirLayout& L = M->lay[par];
-    if (M->send_bytes[par] < L.blk_full) {
-        dfree(M->d_send[par]);
-        HIPCHK(dalloc(&M->d_send[par], L.blk_full));
-        M->send_bytes[par] = L.blk_full;
-        if (int rc = comm_gather_register(c, M->d_send[0], M->d_send[1])) return rc;
+// the blocks of exchange x, parity par, of every rank: gathered over RCCL into the receive buffer,
+// or read in place from the in-process peers (after a stream wait on their "sent" event)
+static int xr_gather(hakai_ctx* c, int x, int par, size_t blk, XBlk& xb) {
+    Xrank* X = c->contact->xr;
+    if (X->nranks > kMaxXRanks) return fail(HAKAI_ERR_COMM, "multi-GPU contact: more than %d ranks", kMaxXRanks);
+    if (comm_is_rccl(c)) {
+        if (int rc = comm_allgather_raw(c, X->d_send[x][par], X->d_recv[x], blk)) return rc;
+        for (int q = 0; q < X->nranks; ++q) xb.p[q] = X->d_recv[x] + (size_t)q * blk;
+        return 0;
     }
-    if (M->recv_bytes < (size_t)M->nranks * L.blk_full) {
-        dfree(M->d_recv);
-        HIPCHK(dalloc(&M->d_recv, (size_t)M->nranks * L.blk_full));
-        M->recv_bytes = (size_t)M->nranks * L.blk_full;
-    }
-    if (M->slot_cap < L.capc) {
-        dfree(M->d_slot_chunk);
-        HIPCHK(dalloc(&M->d_slot_chunk, (size_t)M->nranks * L.capc));
-        M->slot_cap = L.capc;
+    for (int q = 0; q < X->nranks; ++q) {
+        hakai_ctx* pc = comm_peer_ctx(c, q);
+        Xrank* P = pc && pc->contact ? pc->contact->xr : nullptr;
+        // the peer packed this step's block: deletions at the end of the previous step (seq), bins in
+        // this step's A2 (same seq and step), events in this step's A3 (same A3 count; a peer may have
+        // ended the step already)
+        const bool same = P && P->cap[x] == X->cap[x] &&
+                          (x == 0 ? P->seq == X->seq
+                                  : x == 1 ? P->seq == X->seq && P->t_a == X->t_a : P->phase_a == X->phase_a);
+        if (!same)
+            return fail(HAKAI_ERR_STATE, "multi-GPU contact: rank %d is not at the same step (step an in-process group "
+                        "with hakai_step_group; hakai_set_contact_global, reset and upload on every rank)", q);
+        if (q != X->rank) HIPCHK(hipStreamWaitEvent(c->stream, P->ev_sent[x][par], 0));
+        xb.p[q] = P->d_send[x][par];
     }
     return 0;
 }
 
-// multi-GPU: pack this rank's mirror block for step M->seq (full = with u_pre, velo0, all deletion
-// steps) in the layout of that step
-static int mir_pack(hakai_ctx* c, bool full) {
-    Contact* C = c->contact;
-    Mirror* M = C->mir;
-    const int par = (int)(M->seq & 1);
-    const MirLayout& L = M->lay[par];
-    const int n = std::max(std::max(M->nxo, M->neo), 1);
-    const double* velo0 = C->use_velo0 ? M->d_velo0_loc : nullptr;
-    HIPCHK(hipMemsetAsync(M->d_send[par], 0, 16, c->stream));  // header: the deletion-list counter
-    hipLaunchKernelGGL(k_mir_pack, dim3((n + kB - 1) / kB), dim3(kB), 0, c->stream, M->d_xo, M->nxo, M->d_eo, M->neo,
-                       c->d_u[c->cur], c->d_u[1 - c->cur], velo0, c->d_del_step, c->d_del_step + c->nEp + 1,
-                       M->d_send[par], L, full ? 1 : 0, M->d_last_del, (int)c->elem_offset, x1map(M));
-    if (M->nchunk > 0)  // also with capc = 0: the counts are what the overflow check reads
-        hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, c->stream, M->rank, M->rank + 1, M->d_seg_chunk,
-                           M->d_chunk_flag, M->d_slot_chunk, L.capc, M->d_counts, M->d_x1ctl, 0);
-    if (M->nchunk > 0 && L.capc > 0) {
-        const long long nt = 64LL * L.capc;
-        hipLaunchKernelGGL(k_x1_pack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, c->stream, M->rank,
-                           x1slots(M, L), M->d_x1_loc, c->d_u[c->cur], c->d_u[1 - c->cur], velo0, M->d_send[par],
-                           L.off_x1, L.off_x1v0, full ? 1 : 0);
-    }
+// this rank's deletions since the last pack (or, full, every local deletion step) -> the deletion
+// block of step X->seq
+static int xr_dpack(hakai_ctx* c, bool full) {
+    Xrank* X = c->contact->xr;
+    const int par = (int)(X->seq & 1);
+    HIPCHK(hipMemsetAsync(X->d_send[0][par], 0, kXHdr, c->stream));
+    const int n = (int)std::max<long long>(X->nEloc, 1);
+    hipLaunchKernelGGL(k_xr_dpack, dim3((unsigned)std::min((n + kB - 1) / kB, 1024)), dim3(kB), 0, c->stream,
+                       c->d_del_step, c->d_del_step + c->nEp + 1, (int)X->nEloc, X->E0, X->d_last_del,
+                       X->d_send[0][par], X->cap[0], full ? 1 : 0);
     HIPCHK(hipGetLastError());
-    return comm_gather_mark(c, par);
+    HIPCHK(hipEventRecord(X->ev_sent[0][par], c->stream));
+    X->full_del = full;
+    return 0;
 }
 
-// forget all deletions (state reset / upload): the next block is a full one
-static int mir_reset(hakai_ctx* c) {
-    Contact* C = c->contact;
-    Mirror* M = C->mir;
-    hipStream_t s = c->stream;
-    HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)C->nE + 2) * sizeof(int), s));
-    HIPCHK(hipMemsetAsync(M->d_last_del, 0, std::max(M->neo, 1) * sizeof(int), s));
-    HIPCHK(hipMemsetAsync(M->d_chunk_flag, 0, std::max(M->nchunk, 1) * sizeof(int), s));
-    HIPCHK(hipMemsetAsync(M->d_counts, 0, M->nranks * sizeof(int), s));
-    const int ctl[4] = {1, 0, 0, 0};  // slots stale
-    HIPCHK(hipMemcpyAsync(M->d_x1ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-    M->seq = 0;
-    M->lay[1] = M->lay[0];
-    return 0;
+// capacities from the counts gathered two steps ago (the same numbers on every rank, so every rank
+// sizes its collectives alike): a count past half a capacity doubles it (at least 4x the count), up
+// to the largest possible. Exchange x in [x0, x1): the deletion block grows before it is packed
+// (end of a step), the bin and event blocks at the start of the step that packs them -- never
+// while an in-process peer may still read the block of the step before.
+static int xr_grow(hakai_ctx* c, int x0, int x1) {
+    Xrank* X = c->contact->xr;
+    if (X->cnt_seq < 2) return 0;
+    const long long sl = (X->cnt_seq - 2) & 3;
+    HIPCHK(hipEventSynchronize(X->ev_cnt[sl]));
+    const int* h = X->h_cnt + (size_t)sl * Xrank::kNx * X->nranks;
+    for (int x = x0; x < x1; ++x) {
+        long long mx = 0;
+        for (int q = 0; q < X->nranks; ++q) mx = std::max<long long>(mx, h[x * X->nranks + q]);
+        if (2 * mx > X->cap[x]) X->cap[x] = std::min(X->cap_max[x], std::max(2 * X->cap[x], 4 * mx));
+    }
+    return xr_buffers(c);
+}
+
+__global__ void k_xr_counts(XBlk d, XBlk b, XBlk e, int nr, int* out) {
+    const int q = threadIdx.x;
+    if (q >= nr) return;
+    out[q] = xhdr(d.p[q], 3) ? 0 : xhdr(d.p[q], 0);
+    out[nr + q] = xhdr(b.p[q], 0);
+    out[2 * nr + q] = xhdr(e.p[q], 0);
 }
 
 int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
@@ -1991,103 +1971,83 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
     if (!C) return 0;
     C->use_velo0 = true;
     C->force_rebuild = true;
-    if (Mirror* M = C->mir) {
-        if (velo0_host)
-            HIPCHK(hipMemcpyAsync(M->d_velo0_loc, velo0_host, 3 * (size_t)c->nN * sizeof(double),
-                                  hipMemcpyHostToDevice, c->stream));
-        if (int rc = mir_reset(c)) return rc;
-        return mir_pack(c, true);
-    }
     if (velo0_host)
         HIPCHK(hipMemcpyAsync(C->d_velo0, velo0_host, 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice,
                               c->stream));
+    if (Xrank* X = C->xr) {  // every deletion step travels with the next block
+        HIPCHK(hipMemsetAsync(X->g_del, 0, ((size_t)X->nE_g + 2) * sizeof(int), c->stream));
+        HIPCHK(hipMemsetAsync(X->d_xctl, 0, 4 * sizeof(int), c->stream));
+        X->seq = 0;
+        X->cnt_seq = 0;
+        return xr_dpack(c, true);
+    }
     return 0;
 }
 
+// multi-GPU, after the element kernel of a step: capacities for the next step, then this step's
+// deletions into the next step's deletion block
 int contact_post_step(hakai_ctx* c) {
     Contact* C = c->contact;
-    if (!C || !C->mir) return 0;
-    Mirror* M = C->mir;
-    const long long s = M->seq++;  // the step just done consumed block s; pack block s+1
-    MirLayout L = M->lay[s & 1];
-    if (s >= 1) {  // grow from the needs of the unpack of step s-1 (the same numbers on every rank)
-        HIPCHK(hipEventSynchronize(M->ev_need[(s - 1) & 3]));
-        const int need_c = M->h_need[2 * ((s - 1) & 3)], need_d = M->h_need[2 * ((s - 1) & 3) + 1];
-        int capc = L.capc, capd = L.capd;
-        if (2 * need_c >= capc && need_c > 0) capc = std::min(M->maxseg, std::max(2 * capc, 4 * need_c + 64));
-        if (4 * need_d >= capd && need_d > 0) capd = std::max(2 * capd, 8 * need_d);
-        if (capc != L.capc || capd != L.capd) {
-            L = mir_layout(M, capc, capd);
-            // slot tables in the new stride (h_need[8] is a pinned constant 1)
-            HIPCHK(hipMemcpyAsync(M->d_x1ctl, M->h_need + 8, sizeof(int), hipMemcpyHostToDevice, c->stream));
-        }
-    }
-    M->lay[M->seq & 1] = L;
-    if (int rc = mir_buffers(c, (int)(M->seq & 1))) return rc;
-    return mir_pack(c, false);
+    if (!C || !C->xr) return 0;
+    Xrank* X = C->xr;
+    ++X->seq;
+    if (int rc = xr_grow(c, 0, 1)) return rc;
+    return xr_dpack(c, false);
 }
 
-// contact force of step t into c->d_fext (before the nodal update, :500-560). Phase A; with
-// divide_ok on a multi-GPU mirror it stops after packing this rank's share of the events, and
-// contact_step_b finishes the step.
-static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
+static int search(hakai_ctx* c, const StepIn& in, bool fused);
+static int bucket_scan(hakai_ctx* c);
+static void tri_search(hakai_ctx* c, const StepIn& in);
+
+static StepIn step_in(hakai_ctx* c, double t, double d_time) {
     Contact* C = c->contact;
-    Mirror* M = C->mir;
-    hipStream_t s = c->stream;
     StepIn in;
+    in.coord = c->d_coord;
+    in.u = c->d_u[c->cur];
+    in.u_pre = c->d_u[1 - c->cur];
+    in.flag = c->d_flag;
+    in.conn = c->d_conn;
+    in.mass = C->xr ? C->xr->g_mass : c->d_mass;
+    in.l2g = C->xr ? C->xr->d_l2g : nullptr;
+    in.del_step = C->xr ? C->xr->g_del : c->d_del_step;
+    in.velo0 = C->use_velo0 ? C->d_velo0 : nullptr;
+    in.d_time = d_time;
+    in.t = (int)t;
+    return in;
+}
+
+// Start of a step's contact work (:500-560): multi-GPU deletions of the previous step, step
+// prologue, live-list update, pair boxes (a rank's partial boxes). One GPU: the whole search too.
+static int step_start(hakai_ctx* c, double t, double d_time) {
+    Contact* C = c->contact;
+    Xrank* X = C->xr;
+    hipStream_t s = c->stream;
+    StepIn in = step_in(c, t, d_time);
     int* del_step = c->d_del_step;
     const int* del_any = c->d_del_step + c->nEp + 1;
     double* fext = c->d_fext;
-    if (M) {  // all-gather the ranks' blocks of this step into the global mirror
-        const int par = (int)(M->seq & 1);
-        const bool full = M->seq == 0;
-        const MirLayout& Ly = M->lay[par];
-        const size_t blk = full ? Ly.blk_full : Ly.blk_step;
-        if (int rc = comm_allgather(c, par, M->d_recv, blk)) return rc;
-        const long long nslot =
-            std::max(1LL, (long long)M->nranks * std::max(std::max(M->maxx, full ? M->maxe : Ly.capd), 1));
-        hipLaunchKernelGGL(k_mir_unpack, dim3((unsigned)((nslot + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
-                           M->nranks, M->maxx, M->maxe, M->d_xg, M->d_eg, Ly, full ? 1 : 0, M->g_u[par],
-                           M->g_u[1 - par], C->d_velo0, M->g_del, M->g_flag, C->nE, x1map(M));
-        if (M->nchunk > 0)
-            hipLaunchKernelGGL(k_x1_slots, dim3(1), dim3(1024), 0, s, 0, M->nranks, M->d_seg_chunk, M->d_chunk_flag,
-                               M->d_slot_chunk, Ly.capc, M->d_counts, M->d_x1ctl, 1);
-        if (M->nchunk > 0 && Ly.capc > 0) {
-            const long long nt = 64LL * Ly.capc * M->nranks;
-            hipLaunchKernelGGL(k_x1_unpack, dim3((unsigned)((nt + kB - 1) / kB)), dim3(kB), 0, s, M->d_recv, blk,
-                               M->nranks, x1slots(M, Ly), M->d_x1_gid, Ly.off_x1, Ly.off_x1v0, full ? 1 : 0,
-                               M->g_u[par], M->g_u[1 - par], C->d_velo0);
-        }
-        HIPCHK(hipMemcpyAsync(M->h_need + 2 * (M->seq & 3), M->d_x1ctl + 2, 2 * sizeof(int), hipMemcpyDeviceToHost,
-                              s));
-        HIPCHK(hipEventRecord(M->ev_need[M->seq & 3], s));
-        in.coord = M->g_coord;
-        in.u = M->g_u[par];
-        in.u_pre = M->g_u[1 - par];
-        in.flag = M->g_flag;
-        in.conn = M->g_conn;
-        in.mass = M->g_mass;
-        del_step = M->g_del;
-        del_any = M->g_del + C->nE + 1;
-        fext = M->g_fext;
-    } else {
-        in.coord = c->d_coord;
-        in.u = c->d_u[c->cur];
-        in.u_pre = c->d_u[1 - c->cur];
-        in.flag = c->d_flag;
-        in.conn = c->d_conn;
-        in.mass = c->d_mass;
+    unsigned long long* bbox = C->d_bbox;
+    if (X) {
+        if (int rc = xr_grow(c, 1, Xrank::kNx)) return rc;
+        X->t_a = in.t;
+        X->par_a = (int)(X->seq & 1);
+        XBlk xb;
+        if (int rc = xr_gather(c, 0, X->par_a, xr_blk(X, 0, X->full_del), xb)) return rc;
+        const unsigned gx = (unsigned)std::min<long long>(std::max<long long>((X->maxEloc + kB - 1) / kB, 1), 256);
+        hipLaunchKernelGGL(k_xr_dunpack, dim3(gx, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks,
+                           X->d_eoff, X->cap[0], X->g_del, X->nE_g, c->d_poison, in.t, X->d_xctl);
+        X->xb_last[0] = xb;
+        del_step = X->g_del;
+        del_any = X->g_del + X->nE_g + 1;
+        fext = X->g_fext;
+        bbox = X->d_box[X->par_a];
     }
-    in.velo0 = C->use_velo0 ? C->d_velo0 : nullptr;
-    in.d_time = d_time;
-    in.del_step = del_step;
-    in.t = (int)t;
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
     const bool rebuild = C->force_rebuild;
     const int tsel = C->tsel = 1 - C->tsel;
     // small decks: reset + deletion scan + surface append in one workgroup (not on full-rebuild
     // steps, whose live-list rebuild sits between the reset and the scan)
-    const bool fused = C->small && C->fuse_small && !M;
+    const bool fused = C->small && C->fuse_small && !X;
     AppendIn A;
     A.el_tri_ptr = C->d_el_tri_ptr; A.el_tri = C->d_el_tri;
     A.el_ni_ptr = C->d_el_ni_ptr; A.el_ni = C->d_el_ni; A.el_nj_ptr = C->d_el_nj_ptr; A.el_nj = C->d_el_nj;
@@ -2096,18 +2056,14 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     A.pair_reg = C->d_pair_reg;
     A.tri_reg = C->tri_reg;
     if (fused && !rebuild) {
-        hipLaunchKernelGGL(k_ct_prologue1, dim3(1), dim3(kSmallThreads), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs,
+        hipLaunchKernelGGL(k_ct_prologue1, dim3(1), dim3(kSmallThreads), 0, s, bbox, C->npairs, C->d_ctl, C->d_evs,
                            C->d_ccnt, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext, del_step,
                            (int)C->nE, C->d_dlist, A, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live,
                            C->ntile > 0 ? 1 : 0);
-        C->force_rebuild = false;
-        C->last_t = in.t;
     } else {
-        hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, C->d_bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
+        hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
                            C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext,
-                           M ? M->d_g2l : nullptr, M ? c->d_fext : nullptr);
-        C->force_rebuild = false;
-        C->last_t = in.t;
+                           X ? X->d_g2l : nullptr, X ? c->d_fext : nullptr);
         if (C->ntile > 0) {
             LiveIn L;
             L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
@@ -2132,15 +2088,31 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
                                c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
         }
     }
-    const bool div = M && M->divide && divide_ok && M->nranks > 1 && M->nranks <= kMaxDivRanks;
-    if (M) M->div_step = div;
+    C->force_rebuild = false;
+    C->last_t = in.t;
+    const Seg* sg = (const Seg*)C->d_seg;
+    if (C->nseg > 0)
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_box), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_nj_live, C->d_ni_node, C->d_nj_node, bbox, C->g_box);
+    HIPCHK(hipGetLastError());
+    if (X) {
+        HIPCHK(hipEventRecord(X->ev_box[X->par_a], s));
+        return 0;
+    }
+    return search(c, in, fused);
+}
+
+// binning, bucket scan and fill, triangle prefilter and search, and (one GPU) the event gather
+// into external_force
+static int search(hakai_ctx* c, const StepIn& in, bool fused) {
+    Contact* C = c->contact;
+    hipStream_t s = c->stream;
+    const int tsel = C->tsel;
     const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
     // small decks: the binning and the triangle prefilter in one launch (both need only the boxes)
     const bool fused_mid = fused && C->nseg > 0 && C->n_tri > 0;
     const Seg* sg = (const Seg*)C->d_seg;
     if (C->nseg > 0) {
-        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_box), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                           C->d_nj_live, C->d_ni_node, C->d_nj_node, C->d_bbox, C->g_box);
         if (fused_mid) {
             const int nbin = C->nseg * C->g_seg;
             hipLaunchKernelGGL(k_ct_binfilter, dim3((unsigned)nbin + gfilt), dim3(kB), 0, s, in, sg, C->d_reg,
@@ -2157,181 +2129,226 @@ static int step_a(hakai_ctx* c, double t, double d_time, bool divide_ok) {
     // the bucket scan and the fill: one workgroup for tables up to kSmallScan, then a workgroup per
     // segment part (fusing the fill into the scan's one workgroup was slower on every reference deck:
     // the fill's scattered atomics and stores want more than one CU)
-    if (C->htot + 1 <= kSmallScan) {
-        hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, s, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
-    } else {
-        size_t tb = C->tmp_bytes;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, s));
-    }
+    if (int rc = bucket_scan(c)) return rc;
     if (C->nseg > 0)
         hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, sg, C->d_reg, C->d_ni_live,
-                           C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->g_seg, C->d_qrec);
+                           C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->d_bvel, C->g_seg, C->d_qrec);
     if (C->n_tri > 0) {
         if (!fused_mid)
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                                C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
-                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, div ? M->rank : 0, div ? M->nranks : 1);
-        hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, s, in, C->d_ctl, C->d_ccnt, (const TriRec*)C->d_cand,
-                           C->cshard_cap,
-                           C->d_par, C->d_boff, C->d_blist, C->d_lim, C->myu, C->d_evs,
-                           C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
+                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap);
+        tri_search(c, in);
     }
     const unsigned ge = (unsigned)C->g_ev;
-    if (div) {  // pack this rank's events; the exchange and the sums are phase B
-        hipLaunchKernelGGL(k_ev_pack, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                           C->d_ev_f, (EvRec*)M->d_ev_send[in.t & 1], M->d_evcnt + 2 * (in.t & 1), M->d_x1ctl);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(M->ev_evpacked, s));
-        M->div_t = in.t;
-        ++M->div_seq;
-        C->use_velo0 = false;
-        return 0;
-    }
     if (fused) {  // small decks: count, alloc, scatter and sum in one workgroup
         hipLaunchKernelGGL(k_ct_gather1, dim3(1), dim3(kSmallThreads), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
                            C->d_ev_nodes, C->d_ev_f, C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison,
-                           nullptr, in.t, c->g_trd, C->d_toff, C->d_tcnt, C->d_terms, fext);
+                           in.t, c->g_trd, C->d_toff, C->d_tcnt, C->d_terms, c->d_fext);
         HIPCHK(hipGetLastError());
         C->use_velo0 = false;
         return 0;
     }
     hipLaunchKernelGGL(k_ct_count, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
-                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison,
-                       M ? M->d_x1ctl : nullptr, in.t, c->g_trd);
+                       C->d_cnt, C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, in.t, c->g_trd);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, fext, M ? M->d_g2l : nullptr, M ? c->d_fext : nullptr);
+                       C->d_terms, c->d_fext, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
 }
 
-int contact_step(hakai_ctx* c, double t, double d_time) { return step_a(c, t, d_time, false); }
-int contact_step_a(hakai_ctx* c, double t, double d_time) { return step_a(c, t, d_time, true); }
-bool contact_divided(const hakai_ctx* c) { return c->contact && c->contact->mir && c->contact->mir->div_step; }
+static int bucket_scan(hakai_ctx* c) {
+    Contact* C = c->contact;
+    if (C->htot + 1 <= kSmallScan) {
+        hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, c->stream, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
+    } else {
+        size_t tb = C->tmp_bytes;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, c->stream));
+    }
+    return 0;
+}
 
-// Phase B of a divided step: every rank's (count, overflow), then its events, all-gathered (RCCL, or
-// device copies from the in-process peers, which all finished phase A); an overflow anywhere
-// poisons the step on every rank; then the same count / scatter / double-double sums as one GPU.
+static void tri_search(hakai_ctx* c, const StepIn& in) {
+    Contact* C = c->contact;
+    hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, c->stream, in, C->d_ctl, C->d_ccnt,
+                       (const TriRec*)C->d_cand, C->cshard_cap, C->d_par, C->d_boff, C->d_blist, C->d_bvel, C->d_lim,
+                       C->myu, C->d_evs, C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
+}
+
+// A2 (multi-GPU): the pair boxes of every rank combined, then this rank's live i-nodes inside
+// their range boxes binned into its block
+static int xr_a2(hakai_ctx* c, double d_time) {
+    Contact* C = c->contact;
+    Xrank* X = C->xr;
+    hipStream_t s = c->stream;
+    const int par = X->par_a, nw = 12 * C->npairs;
+    const unsigned gw = (unsigned)((nw + kB - 1) / kB);
+    if (comm_is_rccl(c)) {
+        hipLaunchKernelGGL(k_xr_boxflip, dim3(gw), dim3(kB), 0, s, X->d_box[par], nw);
+        if (int rc = comm_allreduce_min_u64(c, X->d_box[par], X->d_boxg, (size_t)nw)) return rc;
+        hipLaunchKernelGGL(k_xr_boxflip, dim3(gw), dim3(kB), 0, s, X->d_boxg, nw);
+    } else {
+        XBox xb{};
+        for (int q = 0; q < X->nranks; ++q) {
+            hakai_ctx* pc = comm_peer_ctx(c, q);
+            Xrank* P = pc && pc->contact ? pc->contact->xr : nullptr;
+            if (!P || P->seq != X->seq || P->t_a != X->t_a)
+                return fail(HAKAI_ERR_STATE, "multi-GPU contact: rank %d has not started step %d", q, X->t_a);
+            if (q != X->rank) HIPCHK(hipStreamWaitEvent(s, P->ev_box[par], 0));
+            xb.p[q] = P->d_box[par];
+        }
+        hipLaunchKernelGGL(k_xr_boxcomb, dim3(gw), dim3(kB), 0, s, xb, X->nranks, nw, X->d_boxg);
+    }
+    HIPCHK(hipMemsetAsync(X->d_send[1][par], 0, kXHdr, s));
+    if (C->nseg > 0) {
+        StepIn in = step_in(c, X->t_a, d_time);
+        hipLaunchKernelGGL(k_xr_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, (const Seg*)C->d_seg, C->d_reg,
+                           C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, X->d_boxg, X->d_send[1][par], X->cap[1],
+                           C->g_seg);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(X->ev_sent[1][par], s));
+    return 0;
+}
+
+// A3 (multi-GPU): one hash grid of every rank's binned i-nodes; this rank's own triangles searched
+// against it; its events packed for phase B
+static int xr_a3(hakai_ctx* c, double d_time) {
+    Contact* C = c->contact;
+    Xrank* X = C->xr;
+    hipStream_t s = c->stream;
+    const int par = X->par_a;
+    XBlk xb;
+    if (int rc = xr_gather(c, 1, par, xr_blk(X, 1), xb)) return rc;
+    X->xb_last[1] = xb;
+    const unsigned gb = (unsigned)std::min<long long>(std::max<long long>((X->cap[1] + kB - 1) / kB, 1), 128);
+    hipLaunchKernelGGL(k_xr_bcount, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks, X->cap[1], C->d_par,
+                       X->d_bq, C->d_bcnt, c->d_poison, X->t_a, X->d_xctl);
+    if (int rc = bucket_scan(c)) return rc;
+    hipLaunchKernelGGL(k_xr_fill, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->cap[1], X->d_bq, C->d_boff,
+                       C->d_bcnt, C->d_blist, C->d_bvel);
+    StepIn in = step_in(c, X->t_a, d_time);
+    if (C->n_tri > 0) {
+        const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
+        hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
+                           C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, X->d_boxg, C->d_ccnt,
+                           (TriRec*)C->d_cand, C->cshard_cap);
+        tri_search(c, in);
+    }
+    hipLaunchKernelGGL(k_ev_pack, dim3((unsigned)C->g_ev), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
+                       C->d_ev_nodes, C->d_ev_f, X->d_send[2][par], X->cap[2]);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(X->ev_sent[2][par], s));
+    ++X->phase_a;
+    C->use_velo0 = false;
+    return 0;
+}
+
+int contact_phase(hakai_ctx* c, int part, double t, double d_time) {
+    Contact* C = c->contact;
+    if (!C) return 0;
+    if (part == 1) return step_start(c, t, d_time);
+    if (!C->xr) return 0;
+    return part == 2 ? xr_a2(c, d_time) : xr_a3(c, d_time);
+}
+
+int contact_step(hakai_ctx* c, double t, double d_time) {
+    if (c->contact && c->contact->xr)
+        return fail(HAKAI_ERR_STATE, "contact force probe on a multi-GPU rank: step the group instead");
+    return contact_phase(c, 1, t, d_time);
+}
+
+bool contact_multi(const hakai_ctx* c) { return c->contact && c->contact->xr; }
+
+// Phase B (multi-GPU): every rank's events -- RCCL all-gather, or the in-process peers' blocks read
+// in place -- and the same count / scatter / double-double sums as one GPU, in the global node
+// space; the sums of this rank's nodes go to its external force. Also records the step's gathered
+// counts for the capacities of later steps.
 int contact_step_b(hakai_ctx* c) {
     Contact* C = c->contact;
-    Mirror* M = C ? C->mir : nullptr;
-    if (!M || !M->div_step) return 0;
+    Xrank* X = C ? C->xr : nullptr;
+    if (!X) return 0;
     hipStream_t s = c->stream;
-    const int nr = M->nranks;
-    CntPtrs cp{};
-    const EvRec* ev = nullptr;
-    long long stride = 1;
-    if (comm_is_rccl(c)) {
-        // The counts (8 B per rank) are all-gathered for the kernels, which read them on the device;
-        // the event all-gather moves ag_cap records per rank, a grow-only capacity decided from the
-        // gathered counts of two steps earlier -- the same numbers on every rank, so every rank
-        // sizes the collective alike, and no host round trip stalls the step. A rank with more
-        // events than ag_cap poisons the step on every rank (k_ct_count_g) and the capacity then
-        // grows from that step's counts (contact_after_overflow).
-        if (int rc = comm_allgather_raw(c, M->d_evcnt + 2 * (M->div_t & 1), M->d_evcnt_all, 2 * sizeof(int)))
-            return rc;
-        if (M->ag_seq >= 2) {
-            const long long sl = (M->ag_seq - 2) & 3;
-            HIPCHK(hipEventSynchronize(M->ev_ag[sl]));  // two steps old: long done
-            long long mx = 0;
-            for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, M->h_evcnt[2 * nr * sl + 2 * q]);
-            if (2 * mx > M->ag_cap) M->ag_cap = std::max(2 * M->ag_cap, 4 * mx);
-        }
-        if (M->ag_cap <= 0) M->ag_cap = 4096;  // records (160 KB per rank)
-        const long long sl = M->ag_seq & 3;
-        HIPCHK(hipMemcpyAsync(M->h_evcnt + 2 * nr * sl, M->d_evcnt_all, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipEventRecord(M->ev_ag[sl], s));
-        ++M->ag_seq;
-        // (the send buffers hold ev_cap records, the event buffer's capacity, which contact_event_cap
-        // sets alike on every rank; a rank cannot pack more)
-        M->ag_cap = std::min(M->ag_cap, std::max<long long>(M->ev_cap, 1));
-        stride = M->ag_cap;
-        const size_t need = (size_t)nr * (size_t)stride * sizeof(EvRec);
-        if (need > M->ev_recv_bytes) {
-            HIPCHK(hipStreamSynchronize(s));
-            dfree(M->d_ev_recv);
-            HIPCHK(dalloc(&M->d_ev_recv, need));
-            M->ev_recv_bytes = need;
-        }
-        if (int rc = comm_allgather_raw(c, M->d_ev_send[M->div_t & 1], M->d_ev_recv, (size_t)stride * sizeof(EvRec)))
-            return rc;
-        for (int q = 0; q < nr; ++q) cp.p[q] = M->d_evcnt_all + 2 * q;
-    } else {
-        // in-process group: the peers' counts and events are read on the device after a stream
-        // wait on their phase A (no host round trip); every peer gets a slot of ev_cap records
-        PeerEv pe{};
-        for (int q = 0; q < nr; ++q) {
-            hakai_ctx* pc = comm_peer_ctx(c, q);
-            Mirror* pm = pc && pc->contact ? pc->contact->mir : nullptr;
-            if (!pm || pm->div_seq != M->div_seq || pm->div_t != M->div_t || pm->ev_cap != M->ev_cap)
-                return fail(HAKAI_ERR_STATE, "divided contact: rank %d has not searched step %d (step an in-process "
-                            "group with hakai_step_group; the same contact_event_cap on every rank)", q, M->div_t);
-            if (q != M->rank) HIPCHK(hipStreamWaitEvent(s, pm->ev_evpacked, 0));
-            pe.src[q] = (const EvRec*)pm->d_ev_send[M->div_t & 1];
-            pe.cnt[q] = pm->d_evcnt + 2 * (M->div_t & 1);
-            cp.p[q] = pe.cnt[q];
-        }
-        stride = std::max<long long>(M->ev_cap, 1);
-        const size_t need = (size_t)nr * (size_t)stride * sizeof(EvRec);
-        if (need > M->ev_recv_bytes) {
-            HIPCHK(hipStreamSynchronize(s));
-            dfree(M->d_ev_recv);
-            HIPCHK(dalloc(&M->d_ev_recv, need));
-            M->ev_recv_bytes = need;
-        }
-        hipLaunchKernelGGL(k_ev_gather_peers, dim3(64, (unsigned)nr), dim3(kB), 0, s, pe, stride,
-                           (EvRec*)M->d_ev_recv);
-    }
-    M->ev_stride = stride;
-    ev = (const EvRec*)M->d_ev_recv;
+    const int par = X->par_a, nr = X->nranks;
+    XBlk xb;
+    if (int rc = xr_gather(c, 2, par, xr_blk(X, 2), xb)) return rc;
+    X->xb_last[2] = xb;
     const int tsel = C->tsel;
     const unsigned ge = (unsigned)C->g_ev;
-    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, ev, stride, cp, nr, C->d_cnt,
-                       C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, M->div_t);
+    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, X->cap[2], nr, C->d_cnt,
+                       C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, X->t_a, X->d_xctl);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
-    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, ev, stride, cp, nr, C->d_ctl, C->d_toff, C->d_tpos,
+    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, X->cap[2], nr, C->d_ctl, C->d_toff, C->d_tpos,
                        C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, M->g_fext, M->d_g2l, c->d_fext);
+                       C->d_terms, X->g_fext, X->d_g2l, c->d_fext);
+    // the step's counts, read by xr_grow two steps later
+    const long long sl = X->cnt_seq & 3;
+    hipLaunchKernelGGL(k_xr_counts, dim3(1), dim3(kMaxXRanks), 0, s, X->xb_last[0], X->xb_last[1], xb, nr,
+                       X->d_xctl + 4);
+    HIPCHK(hipMemcpyAsync(X->h_cnt + (size_t)sl * Xrank::kNx * nr, X->d_xctl + 4, Xrank::kNx * nr * sizeof(int),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(X->ev_cnt[sl], s));
+    ++X->cnt_seq;
     HIPCHK(hipGetLastError());
-    M->div_step = false;
     return 0;
 }
 
 // Graph mode (hakai_step): a step may be captured when its contact work is the same launch sequence
-// every step -- no mirror (host-side capacity decisions), no full rebuild, no initial velocity,
-// consecutive step numbers. contact_step's host state then changes only by the tsel flip and
-// last_t, which contact_graph_advance replays for a cached graph's two steps.
+// every step -- one GPU, no full rebuild, no initial velocity, consecutive step numbers.
+// contact_step's host state then changes only by the tsel flip and last_t, which
+// contact_graph_advance replays for a cached graph's two steps.
 bool contact_graph_ok(const hakai_ctx* c, double t) {
     const Contact* C = c->contact;
     if (!C) return true;
-    return !C->mir && !C->force_rebuild && !C->always_rebuild && !C->use_velo0 && (long long)t == C->last_t + 1;
+    return !C->xr && !C->force_rebuild && !C->always_rebuild && !C->use_velo0 && (long long)t == C->last_t + 1;
 }
 
 // hakai_step found a poisoned step: the device state is the last good step's. Rebuild the live
-// lists at the next step; velo of the first step is the initial one only if no step survived. A
-// multi-GPU mirror's block sequence has advanced past the good step: steps are refused until the
-// state is uploaded or reset on every rank.
+// lists at the next step; velo of the first step is the initial one only if no step survived.
+// Multi-GPU: if an exchange capacity overflowed (the same on every rank: they read the same
+// headers), grow it past every count of the failed step and pack every deletion step again, so the
+// step can run again from there (contact_exchange_retry).
 void contact_after_overflow(hakai_ctx* c, long long steps_since_reset) {
     Contact* C = c->contact;
     if (!C) return;
     C->force_rebuild = true;
     C->use_velo0 = steps_since_reset == 0;
     C->last_t = -1;
-    if (Mirror* M = C->mir) {
-        c->poison_halt = true;
-        // RCCL divided search: grow the event all-gather past every count the call saw (the stream
-        // is drained here; the gathered counts are the same on every rank, so is the new capacity)
-        const int nr = M->nranks;
-        for (long long k = std::max(0LL, M->ag_seq - 4); k < M->ag_seq; ++k)
-            for (int q = 0; q < nr; ++q)
-                M->ag_cap = std::max<long long>(M->ag_cap, 2LL * M->h_evcnt[2 * nr * (k & 3) + 2 * q]);
+    if (Xrank* X = C->xr) {
+        int xc[4 + 3 * kMaxXRanks] = {0};
+        const int nr = X->nranks;
+        hipLaunchKernelGGL(k_xr_counts, dim3(1), dim3(kMaxXRanks), 0, c->stream, X->xb_last[0], X->xb_last[1],
+                           X->xb_last[2], nr, X->d_xctl + 4);
+        if (hipMemcpyAsync(xc, X->d_xctl, (4 + Xrank::kNx * nr) * sizeof(int), hipMemcpyDeviceToHost, c->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return;
+        X->retry = false;
+        if (xc[0] & 7) {
+            for (int x = 0; x < Xrank::kNx; ++x) {
+                long long mx = 0;
+                for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, xc[4 + x * nr + q]);
+                if (xc[0] & (1 << x)) X->cap[x] = std::min(X->cap_max[x], std::max(2 * X->cap[x], 4 * mx));
+            }
+            X->retry = true;
+        }
+        (void)hipMemsetAsync(X->d_xctl, 0, sizeof(int), c->stream);
+        if (xr_buffers(c) == 0) (void)xr_dpack(c, true);
     }
+}
+
+bool contact_exchange_retry(hakai_ctx* c) {
+    Contact* C = c->contact;
+    if (!C || !C->xr || !C->xr->retry) return false;
+    C->xr->retry = false;
+    return true;
 }
 
 void contact_graph_advance(hakai_ctx* c, double t_last) {
@@ -2370,33 +2387,19 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, 3 * sizeof(unsigned int), c->stream));  // + shard max, over
         return 0;
     }
-    if (!std::strcmp(key, "contact_mirror_chunks") || !std::strcmp(key, "contact_mirror_deletions")) {
-        // multi-GPU: block capacity for exposed-node chunks / deletion-list entries (both parities;
-        // call on every rank). Capacities also grow on their own between steps.
-        Mirror* M = C->mir;
-        if (!M) return fail(HAKAI_ERR_STATE, "%s without hakai_set_contact_global", key);
-        if (value < 0 || value > (1LL << 24)) return fail(HAKAI_ERR_ARG, "%s out of range", key);
-        HIPCHK(hipStreamSynchronize(c->stream));
-        const bool ch = key[15] == 'c';
-        for (int p = 0; p < 2; ++p) {
-            const int capc = ch ? (int)std::min<long long>(value, M->maxseg) : M->lay[p].capc;
-            const int capd = ch ? M->lay[p].capd : (int)value;
-            M->lay[p] = mir_layout(M, capc, capd);
-            if (int rc = mir_buffers(c, p)) return rc;
-        }
-        // the next block again, in the new layout; every slot table is rebuilt at the next unpack
-        const int one = 1;
-        HIPCHK(hipMemcpy(M->d_x1ctl, &one, sizeof(int), hipMemcpyHostToDevice));
-        if (c->state_ok) {
-            if (int rc = mir_pack(c, M->seq == 0)) return rc;
-            HIPCHK(hipMemcpyAsync(M->d_x1ctl, M->h_need + 8, sizeof(int), hipMemcpyHostToDevice, c->stream));
-        }
-        HIPCHK(hipStreamSynchronize(c->stream));
-        return 0;
-    }
-    if (!std::strcmp(key, "contact_divide")) {  // multi-GPU: divided search (1, default) or replicated (0)
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_divide must be 0 or 1");
-        if (C && C->mir) C->mir->divide = (int)value;
+    if (!std::strcmp(key, "contact_exchange_deletions") || !std::strcmp(key, "contact_exchange_bins") ||
+        !std::strcmp(key, "contact_exchange_events")) {
+        // multi-GPU: records per rank block of an exchange (call on every rank, between steps);
+        // capacities also grow on their own, and a step that overflows one runs again (hakai_step)
+        Xrank* X = C->xr;
+        if (!X) return fail(HAKAI_ERR_STATE, "%s without hakai_set_contact_global", key);
+        const int x = key[17] == 'd' ? 0 : (key[17] == 'b' ? 1 : 2);
+        if (value < 1 || value > (1LL << 28)) return fail(HAKAI_ERR_ARG, "%s out of range", key);
+        HIPCHK(hipDeviceSynchronize());
+        X->cap[x] = std::min<long long>(value, X->cap_max[x]);
+        if (int rc = xr_buffers(c)) return rc;
+        // the next step's deletion block again, in the new layout
+        if (x == 0 && c->state_ok) return xr_dpack(c, true);
         return 0;
     }
     if (!std::strcmp(key, "contact_full_rebuild")) {
@@ -2416,12 +2419,9 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         dfree(C->d_tcnt);
         C->cap = (value + kEvShards - 1) / kEvShards * kEvShards;
         C->tcap = std::min<long long>(C->nN, 4 * C->cap);
-        if (Mirror* M = C->mir) {  // divided search: this rank's events of a step
-            for (auto& p : M->d_ev_send) {
-                if (p) (void)hipFree(p);
-                HIPCHK(hipMalloc(&p, (size_t)C->cap * sizeof(EvRec)));
-            }
-            M->ev_cap = C->cap;
+        if (Xrank* X = C->xr) {  // the event block can hold at most the event buffer
+            X->cap_max[2] = C->cap;
+            X->cap[2] = std::min(X->cap[2], C->cap);
         }
         HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
@@ -2432,7 +2432,7 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
         // the previous step's touched list is gone: clear external_force and its count
         HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), c->stream));
-        if (C->mir) HIPCHK(hipMemsetAsync(C->mir->g_fext, 0, 3 * (size_t)C->nN * sizeof(double), c->stream));
+        if (C->xr) HIPCHK(hipMemsetAsync(C->xr->g_fext, 0, 3 * (size_t)C->nN * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kTouched, 0, 2 * sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvMax, 0, sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvShardMax, 0, sizeof(unsigned int), c->stream));
@@ -2453,17 +2453,13 @@ int contact_check(hakai_ctx* c) {
         return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step (%u in one of %d shards) exceed the "
                     "buffer (%lld); raise hakai_set_tuning(\"contact_candidate_cap\")", mc[0],
                     mc[kCandShardMax - kNcandMax], kCandShards, C->cand_cap);
-    if (Mirror* M = C->mir) {
-        int x1[4];
-        HIPCHK(hipMemcpy(x1, M->d_x1ctl, sizeof(x1), hipMemcpyDeviceToHost));
-        const MirLayout& L = M->lay[M->seq & 1];
-        if (x1[1] & 1)
-            return fail(HAKAI_ERR_STATE, "contact mirror: a rank had more chunks of exposed contact nodes to send "
-                        "than its block holds (now %d); raise hakai_set_tuning(\"contact_mirror_chunks\") on every "
-                        "rank", L.capc);
-        if (x1[1] & 2)
-            return fail(HAKAI_ERR_STATE, "contact mirror: a rank deleted more elements in one step than its block "
-                        "lists (now %d); raise hakai_set_tuning(\"contact_mirror_deletions\") on every rank", L.capd);
+    if (Xrank* X = C->xr) {
+        int xc = 0;
+        HIPCHK(hipMemcpy(&xc, X->d_xctl, sizeof(int), hipMemcpyDeviceToHost));
+        if (xc & 7)
+            return fail(HAKAI_ERR_STATE, "contact exchange: a rank's %s exceeded its block (capacities now %lld / %lld / "
+                        "%lld records; grown for the next step)", (xc & 1) ? "deletions" : (xc & 2) ? "binned contact "
+                        "nodes" : "events", X->cap[0], X->cap[1], X->cap[2]);
     }
     unsigned int ms = 0;
     HIPCHK(hipMemcpy(&ms, C->d_ctl + kEvShardMax, sizeof(unsigned int), hipMemcpyDeviceToHost));
@@ -2472,7 +2468,7 @@ int contact_check(hakai_ctx* c) {
                     "(%lld); raise hakai_set_tuning(\"contact_event_cap\")", mx, ms, kEvShards, C->cap);
     int pz = 0;
     HIPCHK(hipMemcpy(&pz, c->d_poison, sizeof(int), hipMemcpyDeviceToHost));
-    if (pz)  // divided multi-GPU search: another rank's buffers overflowed
+    if (pz)  // multi-GPU search: another rank's buffers overflowed
         return fail(HAKAI_ERR_STATE, "contact: a contact buffer of another rank overflowed; raise "
                     "hakai_set_tuning(\"contact_event_cap\" / \"contact_candidate_cap\") on every rank");
     return 0;
@@ -2489,17 +2485,21 @@ struct HostMesh {
     const std::vector<int>* conn;      // 8nE, 0-based
     const std::vector<int>* mat;       // nE, 0-based
 };
-// multi-GPU: the nodes and elements the contact kernels can ever read
-struct SetupOut {
-    std::vector<char> x0mask;                     // nodes of the initially live entries
-    std::vector<std::pair<int, int>> x1;          // (node, adder element) of the entries a deletion exposes
-    std::vector<char> emask;                      // adders and triangle owners
+// multi-GPU: the entries this rank keeps (owner-computed search, hkc::Xrank) -- the node entries of
+// the nodes it owns (node_owner = rank of the node's lowest incident element) with local node ids,
+// and the triangles of its elements [E0, E1) with local node and element ids; adders stay global.
+struct OwnFilter {
+    int rank = 0, nranks = 1;
+    const std::vector<int>* node_owner = nullptr;  // [nN global]
+    const std::vector<int>* g2l = nullptr;         // [nN global] local node or -1
+    long long E0 = 0, E1 = 0;
+    std::vector<long long> ni_per_rank;            // out: i-node entries each rank owns
 };
 
 // builds c->contact on mesh H (the surfaces, pairs and entry lists of hakai_set_contact_cp);
 // contact_flag is 1 or 2, c->contact was destroyed by the caller
 int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const int64_t* element_instance, int32_t n_cp,
-                  const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems, SetupOut* out) {
+                  const int32_t* cp_instance, const int64_t* cp_elem_off, const int64_t* cp_elems, OwnFilter* own) {
     const int nE = (int)H.nE;
     // instances: contiguous element blocks 1, 2, ... (readInpFile numbers them this way)
     std::vector<Inst> inst;
@@ -2607,8 +2607,10 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     auto keep = [](const Inst& I, const std::vector<char>* filt, int f) {
         return !filt || (*filt)[I.faces[f].ele - I.e0];
     };
+    if (own) own->ni_per_rank.assign((size_t)own->nranks, 0);
     auto node_list = [&](int pr, const Inst& I, const std::vector<char>* filt, bool with_adds, std::vector<int>& vp,
-                         std::vector<int>& vn, std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd) {
+                         std::vector<int>& vn, std::vector<int>& vo, std::vector<int>& va, std::vector<int>& vadd,
+                         bool side_i) {
         // per node: initial (exterior) or the ascending list of elements whose deletion exposes it;
         // bucketed by node id in linear time (adders arrive in ascending element order)
         const int nN = (int)H.nN;
@@ -2638,8 +2640,16 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         long long count = 0;
         for (int n = 0; n < nN; ++n) {
             if (!seen[n]) continue;
+            if (own) {
+                const int q = (*own->node_owner)[n];
+                if (side_i) own->ni_per_rank[q]++;
+                if (q != own->rank) {
+                    count += orig[n];
+                    continue;
+                }
+            }
             vp.push_back(pr);
-            vn.push_back(n);
+            vn.push_back(own ? (*own->g2l)[n] : n);
             vo.push_back(orig[n]);
             if (!orig[n] && with_adds) {
                 int last = -1;
@@ -2664,33 +2674,31 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         const size_t ni0 = ni_node.size(), nj0 = nj_node.size();
         // surface update (:766-804): c_nodes_i grows for every pair whose point instance lost an
         // element; triangles and c_nodes_j grow only when the triangle instance differs
-        const long long c_i = node_list(pr, inst[a], ct[pr].fa, true, ni_pair, ni_node, ni_orig, ni_aptr, ni_add);
-        const long long c_j = node_list(pr, inst[b], ct[pr].fb, !self, nj_pair, nj_node, nj_orig, nj_aptr, nj_add);
+        const long long c_i = node_list(pr, inst[a], ct[pr].fa, true, ni_pair, ni_node, ni_orig, ni_aptr, ni_add, true);
+        const long long c_j =
+            node_list(pr, inst[b], ct[pr].fb, !self, nj_pair, nj_node, nj_orig, nj_aptr, nj_add, false);
         long long c_t = 0;
+        // a triangle (:2140-2145) of element ele, exposed from the start (adder -1) or by the deletion
+        // of adder; multi-GPU: kept by the rank of ele, with local ids
+        auto add_tri = [&](const int* n, int ele, int adder) {
+            const int tv[6] = {n[0], n[1], n[2], n[2], n[3], n[0]};
+            const bool mine = !own || (ele >= own->E0 && ele < own->E1);
+            for (int h = 0; h < 2; ++h) {
+                if (!mine) continue;
+                tri_pair.push_back(pr);
+                for (int q = 0; q < 3; ++q) tri_nodes.push_back(own ? (*own->g2l)[tv[3 * h + q]] : tv[3 * h + q]);
+                tri_ele.push_back(own ? (int)(ele - own->E0) : ele);
+                tri_adder.push_back(adder);
+            }
+        };
         for (int f : inst[b].exterior) {
             if (!keep(inst[b], ct[pr].fb, f)) continue;
-            const int* n = inst[b].faces[f].n;
-            const int tv[6] = {n[0], n[1], n[2], n[2], n[3], n[0]};  // :2140-2145
-            for (int h = 0; h < 2; ++h) {
-                tri_pair.push_back(pr);
-                tri_nodes.insert(tri_nodes.end(), tv + 3 * h, tv + 3 * h + 3);
-                tri_ele.push_back(inst[b].faces[f].ele);
-                tri_adder.push_back(-1);
-                ++c_t;
-            }
+            add_tri(inst[b].faces[f].n, inst[b].faces[f].ele, -1);
+            c_t += 2;
         }
         if (!self)
             for (int j = 0; j < inst[b].nE; ++j)
-                for (int f : inst[b].added[j]) {
-                    const int* n = inst[b].faces[f].n;
-                    const int tv[6] = {n[0], n[1], n[2], n[2], n[3], n[0]};
-                    for (int h = 0; h < 2; ++h) {
-                        tri_pair.push_back(pr);
-                        tri_nodes.insert(tri_nodes.end(), tv + 3 * h, tv + 3 * h + 3);
-                        tri_ele.push_back(inst[b].faces[f].ele);
-                        tri_adder.push_back(inst[b].e0 + j);
-                    }
-                }
+                for (int f : inst[b].added[j]) add_tri(inst[b].faces[f].n, inst[b].faces[f].ele, inst[b].e0 + j);
         // a segment's live node set is a function of (instance, face filter, adders or not): equal
         // keys, equal sets at every step, so one segment's boxes serve both
         if (ni_node.size() > ni0) {
@@ -2807,30 +2815,6 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         }
         invert(taptr, tadd, C->n_tri, el_tri_ptr, el_tri);
     }
-    if (out) {  // every node / element an entry refers to (positions, masses, adders, triangle owners)
-        out->x0mask.assign((size_t)H.nN, 0);
-        out->emask.assign((size_t)H.nE, 0);
-        out->x1.clear();
-        auto nodes_of = [&](const std::vector<int>& node, const std::vector<int>& orig, const std::vector<int>& aptr,
-                            const std::vector<int>& add) {
-            for (size_t k = 0; k < node.size(); ++k) {
-                if (orig[k]) out->x0mask[node[k]] = 1;
-                for (int a = aptr[k]; a < aptr[k + 1]; ++a) out->x1.push_back({node[k], add[a]});
-            }
-        };
-        nodes_of(ni_node, ni_orig, ni_aptr, ni_add);
-        nodes_of(nj_node, nj_orig, nj_aptr, nj_add);
-        for (size_t j = 0; j < tri_adder.size(); ++j)
-            for (int q = 0; q < 3; ++q) {
-                if (tri_adder[j] < 0) out->x0mask[tri_nodes[3 * j + q]] = 1;
-                else out->x1.push_back({tri_nodes[3 * j + q], tri_adder[j]});
-            }
-        for (int e : ni_add) out->emask[e] = 1;
-        for (int e : nj_add) out->emask[e] = 1;
-        for (int e : tri_ele) out->emask[e] = 1;
-        for (int e : tri_adder)
-            if (e >= 0) out->emask[e] = 1;
-    }
     hipStream_t s = c->stream;
     int rc = 0;
 #define UP(dst, v)                                          \
@@ -2860,7 +2844,9 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     }
     HIPCHK(dalloc(&C->d_bcnt, (size_t)C->htot + 1));
     HIPCHK(dalloc(&C->d_boff, (size_t)C->htot + 1));
-    HIPCHK(dalloc(&C->d_blist, (size_t)C->n_ni));
+    C->blist_cap = std::max(C->n_ni, 1);  // (multi-GPU: sized for every rank's records, xr_buffers)
+    HIPCHK(dalloc(&C->d_blist, (size_t)C->blist_cap));
+    HIPCHK(dalloc(&C->d_bvel, (size_t)C->blist_cap));
     HIPCHK(dalloc(&C->d_qbucket, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_qrec, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_tile_cnt, (size_t)C->ntile));
@@ -2889,19 +2875,18 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     HIPCHK(dalloc(&C->d_ccnt, (size_t)kCandShards * kShardStride));
     HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
-    HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)H.nN));
+    HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));
     HIPCHK(hipMemsetAsync(C->d_bcnt, 0, ((size_t)C->htot + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_cnt, 0, ((size_t)H.nN + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_ctl, 0, kCtl * sizeof(unsigned int), s));
     HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), s));
     C->force_rebuild = true;
-    // velocity before the first step: the state's (IC / uploaded) velocity (multi-GPU: gathered
-    // into the mirror with the first block)
-    if (!c->h_velo0.empty() && !out)
+    // velocity before the first step: the state's (IC / uploaded) velocity (local nodes)
+    if (!c->h_velo0.empty())
         HIPCHK(hipMemcpyAsync(C->d_velo0, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double), hipMemcpyHostToDevice, s));
     else
-        HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)H.nN * sizeof(double), s));
+        HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)c->nN * sizeof(double), s));
     C->use_velo0 = c->steps_done == 0 || !c->h_velo0.empty();
     size_t t1 = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, C->d_bcnt, C->d_boff, C->htot + 1, s));
@@ -2911,168 +2896,65 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     return 0;
 }
 
-// Multi-GPU mirror of the global contact model (hkc::Mirror) for a contact set up on the global
-// mesh: block layout, owners, exchange slots, static global arrays; packs block 0 if a state exists.
-int mirror_build(hakai_ctx* c, const SetupOut& so, long long nNode, long long nElement,
-                 const std::vector<double>& gx, const std::vector<int>& gconn, const double* diag_M,
-                 const std::vector<int>& g2l, const int64_t* rank_elem_off) {
+// Multi-GPU (hkc::Xrank) for a contact set up on the global mesh with this rank's entries: the
+// node maps, the global mass and deletion arrays, the exchange blocks; packs the first deletion
+// block if a state exists.
+int xr_build(hakai_ctx* c, const OwnFilter& own, long long nNode, long long nElement, const double* diag_M,
+             const std::vector<int>& g2l, const int64_t* local_node_global, const int64_t* rank_elem_off) {
     hkc::Contact* C = c->contact;
-    auto* M = new hkc::Mirror();
-    C->mir = M;
-    const int nr = hkc::comm_size(c), rank = hkc::comm_rank(c);
-    M->rank = rank;
-    M->nranks = nr;
-    // owner of a node: the rank of its lowest incident element (ranks hold ascending element ranges)
-    std::vector<int> minel((size_t)nNode, INT32_MAX);
-    for (long long e = 0; e < nElement; ++e)
-        for (int i = 0; i < 8; ++i) {
-            int& m = minel[gconn[8 * e + i]];
-            m = std::min(m, (int)e);
-        }
-    auto rank_of = [&](long long e) {
-        return (int)(std::upper_bound(rank_elem_off, rank_elem_off + nr + 1, (int64_t)e) - rank_elem_off) - 1;
-    };
-    std::vector<std::vector<int>> xs((size_t)nr), es((size_t)nr);
-    for (long long n = 0; n < nNode; ++n)
-        if (so.x0mask[n] && minel[n] != INT32_MAX) xs[rank_of(minel[n])].push_back((int)n);
-    for (long long e = 0; e < nElement; ++e)
-        if (so.emask[e]) es[rank_of(e)].push_back((int)e);
-    for (int q = 0; q < nr; ++q) {
-        M->maxx = std::max(M->maxx, (int)xs[q].size());
-        M->maxe = std::max(M->maxe, (int)es[q].size());
-    }
-    std::vector<int> xg((size_t)nr * M->maxx, -1), eg((size_t)nr * M->maxe, -1), xo, eo;
-    for (int q = 0; q < nr; ++q) {
-        std::copy(xs[q].begin(), xs[q].end(), xg.begin() + (size_t)q * M->maxx);
-        std::copy(es[q].begin(), es[q].end(), eg.begin() + (size_t)q * M->maxe);
-    }
-    for (int n : xs[rank]) {
-        if (g2l[n] < 0) return fail(HAKAI_ERR_ARG, "set_contact_global: owned contact node %d is not in the local model", n + 1);
-        xo.push_back(g2l[n]);
-    }
-    for (int e : es[rank]) eo.push_back(e - (int)rank_elem_off[rank]);
-    M->nxo = (int)xo.size();
-    M->neo = (int)eo.size();
-    // X1: per rank q the nodes outside X0 with an adder on q (ascending global id), in chunks of
-    // 64; el2x lists, per adder, the entries it makes travel. Triangle nodes exposed by a deletion
-    // are j-side node entries with the same adder, so the node entries' pairs cover them.
-    std::vector<int> pcnt((size_t)nNode + 1, 0);
-    for (const auto& pa : so.x1)
-        if (!so.x0mask[pa.first]) pcnt[pa.first + 1]++;
-    for (long long n = 0; n < nNode; ++n) pcnt[n + 1] += pcnt[n];
-    std::vector<int> padd((size_t)pcnt[nNode]);
-    {
-        std::vector<int> fill(pcnt.begin(), pcnt.end() - 1);
-        for (const auto& pa : so.x1)
-            if (!so.x0mask[pa.first]) padd[fill[pa.first]++] = pa.second;
-    }
-    std::vector<std::vector<int>> x1n((size_t)nr);                  // per rank: nodes
-    std::vector<std::vector<std::pair<int, int>>> x1a((size_t)nr);  // per rank: (adder, index in x1n[q])
-    for (long long n = 0; n < nNode; ++n) {
-        if (pcnt[n] == pcnt[n + 1]) continue;
-        std::sort(padd.begin() + pcnt[n], padd.begin() + pcnt[n + 1]);
-        int last_q = -1, last_a = -1;
-        for (int k = pcnt[n]; k < pcnt[n + 1]; ++k) {
-            const int a = padd[k];
-            if (a == last_a) continue;
-            last_a = a;
-            const int q = rank_of(a);  // adders ascend, so their ranks do too
-            if (q != last_q) x1n[q].push_back((int)n);
-            last_q = q;
-            x1a[q].push_back({a, (int)x1n[q].size() - 1});
-        }
-    }
-    std::vector<int> seg_chunk(1, 0), chunk_first, chunk_end, x1_gid, x1_loc, x1_chunk;
-    std::vector<int> el2x_ptr((size_t)nElement + 1, 0), el2x;
-    for (int q = 0; q < nr; ++q) {
-        const int e0 = (int)x1_gid.size(), m = (int)x1n[q].size();
-        for (int k = 0; k < m; k += 64) {
-            chunk_first.push_back(e0 + k);
-            chunk_end.push_back(e0 + std::min(m, k + 64));
-        }
-        seg_chunk.push_back((int)chunk_first.size());
-        for (int k = 0; k < m; ++k) {
-            const int n = x1n[q][k];
-            x1_gid.push_back(n);
-            x1_chunk.push_back(seg_chunk[q] + k / 64);
-            if (q == rank && g2l[n] < 0)
-                return fail(HAKAI_ERR_ARG, "set_contact_global: exposed contact node %d is not in the local model", n + 1);
-            x1_loc.push_back(q == rank ? g2l[n] : -1);
-        }
-        for (const auto& ai : x1a[q]) el2x_ptr[ai.first + 1]++;
-    }
-    for (long long e = 0; e < nElement; ++e) el2x_ptr[e + 1] += el2x_ptr[e];
-    el2x.resize((size_t)el2x_ptr[nElement]);
-    {
-        std::vector<int> fill(el2x_ptr.begin(), el2x_ptr.end() - 1);
-        int base = 0;
-        for (int q = 0; q < nr; ++q) {
-            for (const auto& ai : x1a[q]) el2x[fill[ai.first]++] = base + ai.second;
-            base += (int)x1n[q].size();
-        }
-    }
-    M->nx1 = (int)x1_gid.size();
-    M->nchunk = (int)chunk_first.size();
-    for (int q = 0; q < nr; ++q) M->maxseg = std::max(M->maxseg, seg_chunk[q + 1] - seg_chunk[q]);
-    // initial capacities (they grow between steps): 64 chunks of exposed nodes, 4096 deletions
-    M->lay[0] = M->lay[1] = hkc::mir_layout(M, std::min(M->maxseg, 64), 4096);
+    auto* X = new hkc::Xrank();
+    C->xr = X;
+    const int nr = own.nranks;
+    X->rank = own.rank;
+    X->nranks = nr;
+    X->E0 = own.E0;
+    X->nEloc = own.E1 - own.E0;
+    X->nN_g = nNode;
+    X->nE_g = nElement;
+    std::vector<long long> eoff((size_t)nr + 1);
+    for (int q = 0; q <= nr; ++q) eoff[q] = rank_elem_off[q];
+    for (int q = 0; q < nr; ++q) X->maxEloc = std::max<int>(X->maxEloc, (int)(eoff[q + 1] - eoff[q]));
+    long long ci0 = 0, nimax = 1;
+    for (int p = 0; p < C->npairs; ++p) ci0 += C->pair_counts[3 * p];
+    for (long long v : own.ni_per_rank) nimax = std::max(nimax, v);
+    // capacities (records per rank block): deletions up to a rank's elements, binned i-nodes up to
+    // the entries a rank owns, events up to the event buffer; they start small and grow
+    X->cap_max[0] = X->maxEloc;
+    X->cap_max[1] = nimax;
+    X->cap_max[2] = C->cap;
+    X->cap[0] = std::min<long long>(X->cap_max[0], 1024);
+    X->cap[1] = std::min<long long>(X->cap_max[1], std::max<long long>(4096, ci0 / (8 * nr)));
+    X->cap[2] = std::min<long long>(X->cap_max[2], 4096);
+    std::vector<int> l2g((size_t)c->nN);
+    for (long long l = 0; l < c->nN; ++l) l2g[l] = (int)(local_node_global[l] - 1);
     std::vector<double> gmass((size_t)nNode);
     for (long long n = 0; n < nNode; ++n) gmass[n] = diag_M[3 * n];
-    std::vector<int> ones((size_t)nElement, 1);
     hipStream_t s = c->stream;
-    HIPCHK(upload(&M->d_xo, xo, s));
-    HIPCHK(upload(&M->d_eo, eo, s));
-    HIPCHK(upload(&M->d_xg, xg, s));
-    HIPCHK(upload(&M->d_eg, eg, s));
-    HIPCHK(upload(&M->d_g2l, g2l, s));
-    HIPCHK(upload(&M->g_coord, gx, s));
-    HIPCHK(upload(&M->g_mass, gmass, s));
-    HIPCHK(upload(&M->g_conn, gconn, s));
-    HIPCHK(upload(&M->g_flag, ones, s));
+    HIPCHK(upload(&X->d_l2g, l2g, s));
+    HIPCHK(upload(&X->d_g2l, g2l, s));
+    HIPCHK(upload(&X->g_mass, gmass, s));
+    HIPCHK(upload(&X->d_eoff, eoff, s));
+    HIPCHK(dalloc(&X->g_del, (size_t)nElement + 2));
+    HIPCHK(hipMemsetAsync(X->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
+    HIPCHK(dalloc(&X->g_fext, 3 * (size_t)nNode));
+    HIPCHK(hipMemsetAsync(X->g_fext, 0, 3 * (size_t)nNode * sizeof(double), s));
+    HIPCHK(dalloc(&X->d_last_del, (size_t)std::max<long long>(X->nEloc, 1)));
+    HIPCHK(hipMemsetAsync(X->d_last_del, 0, (size_t)std::max<long long>(X->nEloc, 1) * sizeof(int), s));
+    HIPCHK(dalloc(&X->d_xctl, 4 + (size_t)hkc::Xrank::kNx * nr));
+    HIPCHK(hipMemsetAsync(X->d_xctl, 0, (4 + (size_t)hkc::Xrank::kNx * nr) * sizeof(int), s));
     for (int p = 0; p < 2; ++p) {
-        HIPCHK(dalloc(&M->g_u[p], 3 * (size_t)nNode));
-        HIPCHK(hipMemsetAsync(M->g_u[p], 0, 3 * (size_t)nNode * sizeof(double), s));
+        HIPCHK(dalloc(&X->d_box[p], 12 * (size_t)C->npairs));
+        HIPCHK(hipEventCreateWithFlags(&X->ev_box[p], hipEventDisableTiming));
+        for (int x = 0; x < hkc::Xrank::kNx; ++x) HIPCHK(hipEventCreateWithFlags(&X->ev_sent[x][p], hipEventDisableTiming));
     }
-    HIPCHK(hipHostMalloc((void**)&M->h_need, 16 * sizeof(int), hipHostMallocDefault));
-    std::fill(M->h_need, M->h_need + 16, 0);
-    M->h_need[8] = 1;
-    for (auto& e : M->ev_need) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(dalloc(&M->g_del, (size_t)nElement + 2));
-    HIPCHK(hipMemsetAsync(M->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
-    HIPCHK(dalloc(&M->g_fext, 3 * (size_t)nNode));
-    HIPCHK(hipMemsetAsync(M->g_fext, 0, 3 * (size_t)nNode * sizeof(double), s));
-    HIPCHK(upload(&M->d_seg_chunk, seg_chunk, s));
-    HIPCHK(upload(&M->d_chunk_first, chunk_first, s));
-    HIPCHK(upload(&M->d_chunk_end, chunk_end, s));
-    HIPCHK(upload(&M->d_x1_gid, x1_gid, s));
-    HIPCHK(upload(&M->d_x1_loc, x1_loc, s));
-    HIPCHK(upload(&M->d_x1_chunk, x1_chunk, s));
-    HIPCHK(upload(&M->d_el2x_ptr, el2x_ptr, s));
-    HIPCHK(upload(&M->d_el2x, el2x, s));
-    HIPCHK(dalloc(&M->d_chunk_flag, (size_t)std::max(M->nchunk, 1)));
-    HIPCHK(dalloc(&M->d_counts, (size_t)nr));
-    HIPCHK(dalloc(&M->d_x1ctl, 4));
-    HIPCHK(dalloc(&M->d_last_del, (size_t)std::max(M->neo, 1)));
-    HIPCHK(dalloc(&M->d_velo0_loc, 3 * (size_t)c->nN));
-    if (!c->h_velo0.empty())
-        HIPCHK(hipMemcpyAsync(M->d_velo0_loc, c->h_velo0.data(), 3 * (size_t)c->nN * sizeof(double),
-                              hipMemcpyHostToDevice, s));
-    else
-        HIPCHK(hipMemsetAsync(M->d_velo0_loc, 0, 3 * (size_t)c->nN * sizeof(double), s));
-    // divided search: this rank's events of a step (up to the event buffer), the counts
-    M->ev_cap = C->cap;
-    for (auto& p : M->d_ev_send) HIPCHK(hipMalloc(&p, (size_t)M->ev_cap * sizeof(EvRec)));
-    HIPCHK(dalloc(&M->d_evcnt, 4));
-    HIPCHK(dalloc(&M->d_evcnt_all, 2 * (size_t)nr));
-    HIPCHK(hipHostMalloc((void**)&M->h_evcnt, (8 * (size_t)nr + 2) * sizeof(int), hipHostMallocDefault));
-    std::fill(M->h_evcnt, M->h_evcnt + 8 * (size_t)nr + 2, 0);
-    for (auto& e : M->ev_ag) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&M->ev_evpacked, hipEventDisableTiming));
-    for (int p = 0; p < 2; ++p)
-        if (int rc = hkc::mir_buffers(c, p)) return rc;
-    if (int rc = hkc::mir_reset(c)) return rc;
+    HIPCHK(dalloc(&X->d_boxg, 12 * (size_t)C->npairs));
+    HIPCHK(hipHostMalloc((void**)&X->h_cnt, 4 * (size_t)hkc::Xrank::kNx * nr * sizeof(int), hipHostMallocDefault));
+    std::fill(X->h_cnt, X->h_cnt + 4 * (size_t)hkc::Xrank::kNx * nr, 0);
+    for (auto& e : X->ev_cnt) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipStreamSynchronize(s));
+    if (int rc = hkc::xr_buffers(c)) return rc;
     if (c->state_ok)
-        if (int rc = hkc::mir_pack(c, true)) return rc;
+        if (int rc = hkc::contact_state_reset(c, c->h_velo0.empty() ? nullptr : c->h_velo0.data())) return rc;
     HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
@@ -3156,11 +3038,32 @@ int hakai_set_contact_global(hakai_ctx* c, int32_t contact_flag, int64_t nNode, 
             if (gconn[8 * (c->elem_offset + e) + i] != local_node_global[c->h_conn[8 * e + i]] - 1)
                 return fail(HAKAI_ERR_ARG, "set_contact_global: local element %lld differs from global element %lld", e + 1,
                             c->elem_offset + e + 1);
+    if (nr > hkc::kMaxXRanks) return fail(HAKAI_ERR_ARG, "set_contact_global: more than %d ranks", hkc::kMaxXRanks);
+    // owner of a node: the rank of its lowest incident element (ranks hold ascending element ranges)
+    std::vector<int> minel((size_t)nNode, INT32_MAX), owner((size_t)nNode, -1);
+    for (int64_t e = 0; e < nElement; ++e)
+        for (int i = 0; i < 8; ++i) {
+            int& m = minel[gconn[8 * e + i]];
+            m = std::min(m, (int)e);
+        }
+    for (int64_t n = 0; n < nNode; ++n)
+        if (minel[n] != INT32_MAX) {
+            const int q = (int)(std::upper_bound(rank_elem_off, rank_elem_off + nr + 1, (int64_t)minel[n]) - rank_elem_off) - 1;
+            owner[n] = q;
+            if (q == rank && g2l[n] < 0)
+                return fail(HAKAI_ERR_ARG, "set_contact_global: owned node %lld is not in the local model", (long long)n + 1);
+        }
+    OwnFilter own;
+    own.rank = rank;
+    own.nranks = nr;
+    own.node_owner = &owner;
+    own.g2l = &g2l;
+    own.E0 = rank_elem_off[rank];
+    own.E1 = rank_elem_off[rank + 1];
     const HostMesh H{nNode, nElement, &gx, &gconn, &gmat};
-    SetupOut so;
-    int rc = contact_setup(c, H, contact_flag, element_instance, n_cp, cp_instance, cp_elem_off, cp_elems, &so);
+    int rc = contact_setup(c, H, contact_flag, element_instance, n_cp, cp_instance, cp_elem_off, cp_elems, &own);
     if (rc || !c->contact) return rc;
-    rc = mirror_build(c, so, nNode, nElement, gx, gconn, diag_M, g2l, rank_elem_off);
+    rc = xr_build(c, own, nNode, nElement, diag_M, g2l, local_node_global, rank_elem_off);
     if (rc) hkc::contact_destroy(c);
     return rc;
 }
@@ -3220,15 +3123,15 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
     const int64_t v[7] = {ctl[kEv], ctl[kEvMax], ctl[kNcand], ctl[kTouched + C->tsel], 0, 0, 0};
     for (int r = 0; r < C->nreg; ++r) live[C->reg_list_h[r]] += reg[2 * r + 1];
     for (int k = 0; k < cap && k < 7; ++k) stats[k] = k < 4 ? v[k] : live[k == 4 ? 2 : k - 5];
-    if (cap > 7) {  // multi-GPU mirror: exposed-node chunks all ranks sent in the last step, bytes per block
-        long long sent = 0, bytes = 0;
-        if (hkc::Mirror* M = C->mir) {
-            std::vector<int> cnt((size_t)M->nranks);
-            HIPCHK(hipMemcpy(cnt.data(), M->d_counts, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
-            for (int q : cnt) sent += std::min(q, M->lay[M->seq & 1].capc);
-            bytes = (long long)M->lay[M->seq & 1].blk_step;
+    if (cap > 7) {  // multi-GPU: contact-zone i-nodes all ranks binned in the last step, exchange bytes per rank
+        long long binned = 0, bytes = 0;
+        if (hkc::Xrank* X = C->xr) {
+            std::vector<int> cnt((size_t)X->nranks);
+            HIPCHK(hipMemcpy(cnt.data(), X->d_xctl + 4 + X->nranks, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+            for (int q : cnt) binned += q;
+            bytes = (long long)(hkc::xr_blk(X, 0) + hkc::xr_blk(X, 1) + hkc::xr_blk(X, 2));
         }
-        stats[7] = sent;
+        stats[7] = binned;
         if (cap > 8) stats[8] = bytes;
     }
     if (cap > 9) stats[9] = C->htot;  // hash-grid buckets over all pairs (> kSmallScan: device-wide scan)

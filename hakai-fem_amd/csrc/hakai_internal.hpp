@@ -94,7 +94,7 @@ struct hakai_ctx {
                                  // [nEp+1] last step in which any element was deleted
     unsigned long long* d_negjac = nullptr;
     int* d_poison = nullptr;     // [2]: contact buffer overflow in this call (flag, step); see ElemArgs
-    bool poison_halt = false;    // multi-GPU contact overflowed: steps refused until upload/reset
+    long long poison_step = -1;  // the step a contact overflow poisoned in the last failed call
     bool any_plastic = false;
     bool model_ok = false;
     bool state_ok = false;
@@ -167,11 +167,6 @@ bool comm_is_local(const hakai_ctx* c);              // in-process group stepped
 const std::vector<int>* comm_dn_nodes(const hakai_ctx* c);  // nodes shared with rank-1 (or null)
 int comm_rank(const hakai_ctx* c);
 int comm_size(const hakai_ctx* c);
-// All-gather of equal-size device blocks, one per rank, from per-parity send buffers (RCCL
-// ncclAllGather, or device copies between the contexts of an in-process group).
-int comm_gather_register(hakai_ctx* c, void* send0, void* send1);
-int comm_gather_mark(hakai_ctx* c, int par);                             // send[par] packed (c->stream)
-int comm_allgather(hakai_ctx* c, int par, void* recv, size_t bytes);     // ordered on c->stream
 // in-process group: dst + off[q] <- src[q] (bytes[q], 8-byte aligned), all ranks in one launch on
 // c->stream (the caller orders it after the peers' producers)
 constexpr int kMaxLocalGather = 64;
@@ -181,22 +176,29 @@ struct LocalGather {
     long long off[kMaxLocalGather];
 };
 int gather_local(hakai_ctx* c, const LocalGather& g, int n, void* dst);
-int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes);  // RCCL only
+// RCCL only, ordered on c->stream: recv[q*bytes ..] = rank q's send; recv = MIN over ranks (uint64)
+int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes);
+int comm_allreduce_min_u64(hakai_ctx* c, const void* send, void* recv, size_t count);
 bool comm_is_rccl(const hakai_ctx* c);
 hakai_ctx* comm_peer_ctx(hakai_ctx* c, int q);                          // in-process group member q
 // Contact (no-ops without hakai_set_contact).
 void contact_destroy(hakai_ctx* c);
 int contact_state_reset(hakai_ctx* c, const double* velo0_host);
-int contact_step(hakai_ctx* c, double t, double d_time);  // contact force of step t -> d_fext
-// the same in two phases (multi-GPU divided search): A = mirror update + search of this rank's
-// share of the triangles + event pack; B = event all-gather + force sums. An in-process group
-// runs A on every rank before B on any (hakai_step_group).
-int contact_step_a(hakai_ctx* c, double t, double d_time);
+int contact_step(hakai_ctx* c, double t, double d_time);  // one GPU: contact force of step t -> d_fext
+// The contact work of a step in phases (step_once's phase bits kPhaseA1 / A2 / A3): one GPU runs it
+// all in part 1. Multi-GPU (hakai_set_contact_global): part 1 = deletions of the previous step,
+// live lists, this rank's pair boxes; 2 = boxes combined, this rank's contact-zone nodes binned;
+// 3 = every rank's binned nodes hashed, this rank's triangles searched, its events packed;
+// contact_step_b = every rank's events gathered and summed. An in-process group runs each part on
+// every rank before the next part on any (hakai_step_group).
+int contact_phase(hakai_ctx* c, int part, double t, double d_time);
 int contact_step_b(hakai_ctx* c);
-bool contact_divided(const hakai_ctx* c);                 // this step runs the divided search
-int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack the mirror block of the next step
-int contact_check(hakai_ctx* c);                          // event-buffer overflow check (syncs)
+bool contact_multi(const hakai_ctx* c);                   // multi-GPU contact (phase B runs)
+int contact_post_step(hakai_ctx* c);                      // multi-GPU: pack this step's deletions
+int contact_check(hakai_ctx* c);                          // buffer overflow check (syncs)
 void contact_after_overflow(hakai_ctx* c, long long steps_since_reset);  // host state after a poisoned call
+bool contact_exchange_retry(hakai_ctx* c);                // that call overflowed a multi-GPU exchange,
+                                                          // now grown: the step may run again
 void graph_invalidate(hakai_ctx* c);                      // drop captured step graphs (hakai_step)
 bool contact_graph_ok(const hakai_ctx* c, double t);       // step t's contact work can be captured
 void contact_graph_advance(hakai_ctx* c, double t_last);   // host state after a cached graph's steps

@@ -156,7 +156,7 @@ class Solver:
         st = np.zeros(10, np.int64)
         check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 10))
         keys = ("events", "max_events", "candidate_triangles", "touched_nodes", "live_triangles", "live_nodes_i",
-                "live_nodes_j", "mirror_chunks_sent", "mirror_block_bytes", "hash_buckets")
+                "live_nodes_j", "binned_contact_nodes", "exchange_bytes_per_rank", "hash_buckets")
         return {k: int(v) for k, v in zip(keys, st)}
 
     def contact_info(self):
@@ -216,8 +216,9 @@ class Solver:
 
     def set_contact_global(self, glob: Model, local_node_global: np.ndarray, rank_elem_off: np.ndarray,
                            glob_diag_M: np.ndarray | None = None):
-        """Multi-GPU contact (hakai_set_contact_global): this rank mirrors the contact model of the
-        global mesh `glob` (its contact_flag, instances, *Contact Pair surfaces and constants).
+        """Multi-GPU contact (hakai_set_contact_global): this rank sets up the contact model of the
+        global mesh `glob` (its contact_flag, instances, *Contact Pair surfaces and constants) and
+        searches the entries of its own elements and nodes.
         Call after comm_init[_local], set_element_offset and set_interface."""
         if glob_diag_M is None:
             glob_diag_M, _ = glob.lumped_mass()

@@ -157,7 +157,7 @@ def test_charpy_deck_two_ranks_bitexact():
 @pytest.mark.parametrize("name,world", [("car_crash_N2k", 2), ("car_wall_N2k", 3)])
 def test_car_deck_ranks_bitexact(name, world):
     """The v0.0.2 car decks (multi-instance contact, self-contact on car-wall, mass scaling 100)
-    range-partitioned over an in-process group with the divided contact search and the
+    range-partitioned over an in-process group with the owner-computed contact search and the
     reference-order element arithmetic: 20 000 steps bit-identical to one context."""
     z, glob = _deck(name)
     steps = 20000

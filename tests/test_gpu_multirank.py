@@ -75,10 +75,9 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key, divide=1, tune=None):
-    """Range-partitioned contact model on an in-process group, each rank mirroring the global
-    contact model (hakai_set_contact_global); divide=1 (default): each rank searches its share of
-    the triangles and the events are all-gathered."""
+def _run_contact_group(glob, world, n_steps, key, tune=None):
+    """Range-partitioned contact model on an in-process group (hakai_set_contact_global): each rank
+    searches the triangles of its elements against the binned contact nodes of every rank."""
     gdiag, _ = glob.lumped_mass()
     parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
     svs = []
@@ -88,7 +87,6 @@ def _run_contact_group(glob, world, n_steps, key, divide=1, tune=None):
         sv.comm_init_local(r, world, key)
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
-        sv.set_tuning("contact_divide", divide)
         for k, v in (tune or {}).items():
             sv.set_tuning(k, v)
         svs.append(sv)
@@ -116,13 +114,13 @@ def _assert_group_equals_single(glob, parts, g, gdel):
         assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
 
 
-@pytest.mark.parametrize("world,divide", [(2, 1), (3, 1), (4, 1), (2, 0), (3, 0)])
-def test_contact_group_bitexact_with_deletion(world, divide):
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_contact_group_bitexact_with_deletion(world):
     """Multi-GPU contact: contact-driven deletion with the surface update, the
-    impactor and the plate split over ranks; every rank's displacements, stresses and the
-    deletion log equal the single-context run bit for bit -- with the divided search (each rank
-    tests its share of the candidate triangles, events all-gathered, the same order-independent
-    sums) and with the replicated one."""
+    impactor and the plate split over ranks; every rank's displacements, stresses and the deletion
+    log equal the single-context run bit for bit. Each rank keeps the triangles of its own elements
+    and the contact nodes it owns: the live lists and the candidate triangles divide over the ranks,
+    the events are all-gathered and every rank forms the same order-independent sums."""
     from hakai import mesh
     glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
     with Solver(glob) as sv:
@@ -131,16 +129,13 @@ def test_contact_group_bitexact_with_deletion(world, divide):
         gdel = [tuple(x) for x in sv.deleted()]
         gst = sv.contact_stats()
     assert len(gdel) >= 4
-    parts = _run_contact_group(glob, world, glob.n_steps, key=300 + 10 * divide + world, divide=divide)
+    parts = _run_contact_group(glob, world, glob.n_steps, key=300 + world)
     _assert_group_equals_single(glob, parts, g, gdel)
-    for *_, st in parts:  # every rank keeps the whole live lists and sums every rank's events
-        assert st["live_triangles"] == gst["live_triangles"] and st["events"] == gst["events"]
-    cand = [st["candidate_triangles"] for *_, st in parts]
-    gc = gst["candidate_triangles"]
-    if divide:  # the candidate triangles of the last step, split over the ranks
-        assert sum(cand) == gc and (gc < world or max(cand) < gc)
-    else:
-        assert cand == [gc] * world
+    sts = [st for *_, st in parts]
+    assert all(st["events"] == gst["events"] for st in sts)  # every rank sums every event
+    for k in ("live_triangles", "live_nodes_i", "live_nodes_j", "candidate_triangles"):
+        assert sum(st[k] for st in sts) == gst[k], k  # the lists and the search divide
+    assert sum(st["candidate_triangles"] > 0 for st in sts) >= 2
 
 
 @pytest.mark.parametrize("flag,myu,surfaces", [(1, None, False), (2, 0.0, False), (1, None, True)])
@@ -172,46 +167,43 @@ def test_contact_on_communicator_requires_global_model():
             check(sv.L.hakai_set_contact(sv.ctx, 1, ptr(inst, ctypes.c_int64)))
 
 
-def test_contact_group_exposed_node_chunks():
-    """The nodes only a deletion exposes travel in chunks once an adder is deleted: the run with
-    the default block capacity is bit-identical to one context and sends chunks; a block without
-    room for them fails loudly (no silent stale positions) and a raised capacity recovers."""
+@pytest.mark.parametrize("caps", [1, 3])
+def test_contact_group_exchange_capacities_grow(caps):
+    """Every exchange block (deletions, binned contact nodes, events) starting at `caps` records per
+    rank: a step that overflows one is poisoned on every rank, the capacity grows from the counts
+    every rank gathered, and the step runs again -- the run is bit-identical to one context, and
+    the capacities end larger than they started."""
     from hakai import mesh
-    from hakai._abi import HakaiError
-    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    glob = mesh.two_body_model(plate=(16, 16, 8), impactor=(4, 4, 4), v=-3e5, d_time=2e-8, n_steps=300)
     with Solver(glob) as sv:
         sv.step(1, glob.n_steps)
         g = sv.download()
         gdel = [tuple(x) for x in sv.deleted()]
-    parts = _run_contact_group(glob, 2, glob.n_steps, key=610)
-    _assert_group_equals_single(glob, parts, g, gdel)
-    assert all(st["mirror_chunks_sent"] > 0 for *_, st in parts)
-
-    def build(key, chunks):
-        gdiag, _ = glob.lumped_mass()
-        ps = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
-        svs = []
-        for r, (loc, diag, iface, l2g, off) in enumerate(ps):
-            sv = Solver(loc, diag_M=diag)
-            sv.set_element_offset(loc.global_element_offset)
-            sv.comm_init_local(r, 2, key)
-            sv.set_interface(*iface)
-            sv.set_contact_global(glob, l2g, off, gdiag)
-            sv.set_tuning("contact_mirror_chunks", chunks)
-            svs.append(sv)
-        return ps, svs
-
-    _, svs = build(611, 0)
-    with pytest.raises(HakaiError):
-        step_group(svs, 1, glob.n_steps)
-    for sv in svs:
-        sv.close()
-    ps, svs = build(612, 1 << 20)
+    assert len(gdel) > 0
+    tune = {"contact_exchange_deletions": caps, "contact_exchange_bins": caps, "contact_exchange_events": caps}
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, 2, 8080 + caps)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        svs.append(sv)
+    b0 = svs[0].contact_stats()["exchange_bytes_per_rank"]
     step_group(svs, 1, glob.n_steps)
-    for sv, (loc, _, _, l2g, _) in zip(svs, ps):
+    st0 = svs[0].contact_stats()
+    assert st0["exchange_bytes_per_rank"] > b0 and st0["binned_contact_nodes"] > caps
+    dels = []
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
         st = sv.download()
+        dels += [tuple(x) for x in sv.deleted()]
         assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
         sv.close()
+    assert sorted(dels) == gdel
 
 
 @pytest.mark.parametrize("ranks", [2, 3])
@@ -234,7 +226,7 @@ def test_multi_gpu_driver_writes_the_same_vtk(tmp_path, ranks):
 
 def test_contact_group_after_state_upload():
     """hakai_upload_state on every rank (a mid-run state with deleted elements, restricted to each
-    rank's nodes and elements) starts the mirror afresh: the next steps equal a single context
+    rank's nodes and elements) starts the exchange afresh: the next steps equal a single context
     that uploaded the same state, bit for bit."""
     from hakai import mesh
     from hakai.solver import State
@@ -274,42 +266,8 @@ def test_contact_group_after_state_upload():
         sv.close()
 
 
-def test_contact_mirror_capacity_grows_between_steps():
-    """Starting from a one-chunk block, the exposed-node capacity grows between steps from the
-    needs every rank computes identically (no overflow, results bit-identical to one context)."""
-    from hakai import mesh
-    glob = mesh.two_body_model(plate=(16, 16, 8), impactor=(4, 4, 4), v=-3e5, d_time=2e-8, n_steps=300)
-    with Solver(glob) as sv:
-        sv.step(1, glob.n_steps)
-        g = sv.download()
-        gdel = [tuple(x) for x in sv.deleted()]
-    assert len(gdel) > 0
-    gdiag, _ = glob.lumped_mass()
-    parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
-    svs = []
-    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
-        sv = Solver(loc, diag_M=diag)
-        sv.set_element_offset(loc.global_element_offset)
-        sv.comm_init_local(r, 2, 8080)
-        sv.set_interface(*iface)
-        sv.set_contact_global(glob, l2g, off, gdiag)
-        sv.set_tuning("contact_mirror_chunks", 1)
-        svs.append(sv)
-    b0 = svs[0].contact_stats()["mirror_block_bytes"]
-    step_group(svs, 1, glob.n_steps)
-    st0 = svs[0].contact_stats()
-    assert st0["mirror_chunks_sent"] > 1 and st0["mirror_block_bytes"] > b0
-    dels = []
-    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
-        st = sv.download()
-        dels += [tuple(x) for x in sv.deleted()]
-        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
-        sv.close()
-    assert sorted(dels) == gdel
-
-
-def test_contact_group_divided_window_vs_oracle():
-    """A multi-rank run handed to the oracle: a 3-rank divided-search group (reference-order
+def test_contact_group_window_vs_oracle():
+    """A multi-rank run handed to the oracle: a 3-rank contact group (reference-order
     element arithmetic) runs past the first contact deletions; its ranks' states are assembled
     into the global state, the oracle takes over (surfaces updated for the deletions so far) and
     both run the next steps -- every rank's state equals the oracle's bit for bit."""
@@ -371,8 +329,8 @@ def test_contact_group_divided_window_vs_oracle():
     assert sorted(new) == sorted(tuple(int(v) for v in x) for x in o.deletions)
 
 
-def test_divided_contact_overflow_poisons_every_rank():
-    """An event-buffer overflow on any rank in the divided search is seen by every rank in the
+def test_contact_overflow_poisons_every_rank():
+    """An event-buffer overflow on any rank of a contact group is seen by every rank in the
     exchanged counts: the same step is poisoned on all of them (device-side, no host round trip),
     every rank's call fails, and every rank's state is the last good step's."""
     from hakai import mesh
@@ -464,7 +422,7 @@ def test_local_group_owner_assembly_bitexact(world):
 
 
 def test_contact_group_owner_assembly_bitexact():
-    """Contact on a communicator with owner-computed assembly (persistent kernel forced): the mirror's
+    """Contact on a communicator with owner-computed assembly (persistent kernel forced): the
     contact force enters the nodal update and the interface fix beside the owner-computed Q;
     every rank equals one context with the same mode, deletions included."""
     from hakai import mesh

@@ -1,5 +1,5 @@
 """RCCL with more than one rank (hakai_comm_init: grouped ncclSend/ncclRecv interface exchange,
-ncclAllReduce / ncclAllGather at setup, the divided contact search's per-step event all-gather),
+ncclAllReduce / ncclAllGather at setup, the multi-GPU contact search's per-step exchanges),
 one process per rank under torch.distributed.run, against one context bit for bit. On a one-GPU box
 the ranks share the device (HAKAI_RCCL_SHARED_GPU=1: hakai.dist.rank_device makes them separate
 hosts to RCCL, which then connects them with its socket transport over loopback) -- the same RCCL
@@ -51,10 +51,12 @@ def test_rccl_interface_exchange_owner_assembly_bitexact(n):
 
 
 def test_rccl_contact_bitexact():
-    """Two-body impact with contact deletions over 2 RCCL ranks, divided and replicated search."""
+    """Two-body impact with contact deletions over 2 RCCL ranks (owner-computed search), with the
+    default exchange capacities and with one-record blocks that grow (the overflowing steps run
+    again)."""
     out = _torchrun("tools/rccl_contact_check.py", 2)
-    assert "RCCL 2-rank contact (divide=1) vs 1 context bit-exact: True" in out
-    assert "RCCL 2-rank contact (divide=0) vs 1 context bit-exact: True" in out
+    assert "RCCL 2-rank contact (exchange capacities default) vs 1 context bit-exact: True" in out
+    assert "RCCL 2-rank contact (exchange capacities 1) vs 1 context bit-exact: True" in out
 
 
 def test_torchrun_driver_writes_the_same_vtk():

@@ -21,15 +21,12 @@ def main():
     ap.add_argument("--preload", type=int, default=30, help="steps before timing (contact starts at ~10)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--ranks", type=int, default=1,
-                    help=">1: range-partitioned in-process group on this one GPU (multi-GPU contact mirror; "
-                         "measures the per-rank contact cost incl. the all-gather, not scaling)")
-    ap.add_argument("--divide", type=int, default=1,
-                    help="multi-rank contact: 1 = each rank searches its share of the triangles and the events "
-                         "are all-gathered (default), 0 = every rank searches every triangle")
+                    help=">1: range-partitioned in-process group on this one GPU (multi-GPU contact, "
+                         "owner-computed search; measures the per-rank contact cost incl. the exchanges, not scaling)")
     ap.add_argument("--serial", type=int, default=1,
                     help="multi-rank: drain each rank's phase before the next rank's (tuning group_serial), so "
                          "the per-rank kernel timings are not inflated by the ranks sharing this one GPU")
-    ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_divide=0")
+    ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_exchange_bins=4096")
     a = ap.parse_args()
     a.tuning = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in a.tuning.split(",") if kv]
     if a.ranks > 1:
@@ -96,7 +93,6 @@ def group(a):
         sv.comm_init_local(r, a.ranks, 4242)
         sv.set_interface(*iface)
         sv.set_contact_global(m, l2g, off, gdiag)
-        sv.set_tuning("contact_divide", a.divide)
         sv.set_tuning("group_serial", a.serial)
         for k, v in a.tuning:
             sv.set_tuning(k, v)
@@ -116,12 +112,13 @@ def group(a):
         k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
                                                 (K_CONTACT, "contact"), (K_CONTACT_SUM, "contact_sum"),
                                                 (K_EXCHANGE, "exchange"))}
-        per = {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]}
+        # (the contact search is timed per part: three event pairs per step on a rank)
+        per = {n: round(v[0] / (a.steps if n == "contact" else max(v[1], 1)), 4) for n, v in k.items() if v[1]}
         ranks.append({"elements": loc.nElement, "nodes": loc.nNode, "kernel_ms_per_step": per,
                       "contact_total_ms_per_step": round(per.get("contact", 0) + per.get("contact_sum", 0), 4),
                       "contact_stats_last_step": sv.contact_stats()})
     out = {"workload": f"C4 two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group), "
-                       f"contact_divide={a.divide}, group_serial={a.serial}",
+                       f"owner-computed search, group_serial={a.serial}",
            "elements": m.nElement, "steps": a.steps, "preload": a.preload,
            "group_ms_per_step_all_ranks": round(el / a.steps * 1e3, 4), "setup_s": round(t1 - t0, 2),
            "ranks": ranks}

@@ -2,8 +2,10 @@
 """RCCL check of the multi-GPU contact path (hakai_set_contact_global over hakai_comm_init): 2 ranks
 (both on device 0 when only one GPU is visible and HAKAI_RCCL_SHARED_GPU=1: hakai.dist.rank_device
 makes them separate hosts to RCCL, which then runs its socket transport over loopback), a range-partitioned two-body impact with contact
-deletions, the divided contact search (events all-gathered with ncclAllGather, exact sizes) and the
-replicated one, each compared bit for bit with a single-context run. Launch:
+deletions and the owner-computed search (per step: deletions and binned contact-zone nodes
+all-gathered, pair boxes all-reduced, events all-gathered), compared bit for bit with a
+single-context run -- once with small exchange capacities, so blocks grow and steps run again.
+Launch:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \\
       --master-port 29534 tools/rccl_contact_check.py
 Rendezvous and the unique-id broadcast use gloo."""
@@ -35,7 +37,7 @@ def main():
             g1.step(1, glob.n_steps)
             g = g1.download()
             gdel = [tuple(int(v) for v in x) for x in g1.deleted()]
-    for divide in (1, 0):
+    for caps in (None, 1):
         sv = Solver(loc, device=dev, diag_M=diag)
         sv.set_element_offset(loc.global_element_offset)
         uid = comm_unique_id() if rank == 0 else bytes(128)
@@ -44,7 +46,9 @@ def main():
         sv.comm_init(rank, world, bytes(t.tolist()))
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
-        sv.set_tuning("contact_divide", divide)
+        if caps:
+            for k in ("contact_exchange_deletions", "contact_exchange_bins", "contact_exchange_events"):
+                sv.set_tuning(k, caps)
         sv.step(1, glob.n_steps)
         st = sv.download()
         dels = [tuple(int(v) for v in x) for x in sv.deleted()]
@@ -59,7 +63,8 @@ def main():
             for l2, e0, ne, disp, flag, _, _ in objs:
                 same &= np.array_equal(disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2 - 1])
                 same &= np.array_equal(flag, g.element_flag[e0:e0 + ne])
-            print(f"RCCL {world}-rank contact (divide={divide}) vs 1 context bit-exact: {same}; deletions {len(gdel)}; "
+            print(f"RCCL {world}-rank contact (exchange capacities {caps or 'default'}) vs 1 context bit-exact: {same}; "
+                  f"deletions {len(gdel)}; "
                   f"candidates per rank {[o[6] for o in objs]}", flush=True)
             ok &= same
     dist.destroy_process_group()
