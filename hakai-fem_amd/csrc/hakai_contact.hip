@@ -90,7 +90,6 @@ struct Xrank {
     int* d_g2l = nullptr;             // [nN_g] local node id or -1
     double* g_mass = nullptr;         // [nN_g] lumped node mass (diag_M[i] with a node id i, :2592)
     int* g_del = nullptr;             // [nE_g + 2] deletion step; [nE_g + 1] last step with any deletion
-    double* g_fext = nullptr;         // [nN_g][3] contact force in the global node space (sums of phase B)
     int* d_last_del = nullptr;        // [nEloc] local deletion steps at the last pack
     // exchange blocks: int4 header (count, overflow, last deletion step, full) + records
     static constexpr int kNx = 3;     // 0 deletions, 1 binned i-nodes, 2 events
@@ -109,13 +108,15 @@ struct Xrank {
     int* d_bq = nullptr;              // [nranks * cap[1]] bucket of each gathered i-node record
     long long bq_len = 0;
     int* d_xctl = nullptr;            // [0] exchange overflow bits of the current call (1 del, 2 bins, 4 events);
-                                      // [4 ..] the step's gathered counts [kNx][nranks]
-    XBlk xb_last[kNx] = {};           // the blocks of the current step (counts, overflow growth)
+                                      // [4 ..] the step's gathered counts [kNx][nranks], then their
+                                      // maxima since the last overflow growth [kNx][nranks]
     bool retry = false;               // the last poisoned call overflowed an exchange, now grown
-    int* h_cnt = nullptr;             // pinned [4][kNx][nranks] gathered counts, read two steps later
+    int* h_cnt = nullptr;             // pinned, device-mapped [4][kNx][nranks] gathered counts, written by
+    int* d_hcnt = nullptr;            // the kernels that read the blocks (d_hcnt: device view), read two steps later
     hipEvent_t ev_cnt[4] = {nullptr, nullptr, nullptr, nullptr};
     long long seq = 0;                // steps since the last state reset: block parity, count ring
     long long cnt_seq = 0;            // count-ring entries written
+    int sl_a = 0;                     // count-ring slot of the current step
     int t_a = 0;                      // step of the current phase A
     long long phase_a = 0;            // phase-A3 calls (equal on the ranks of a lockstep group)
     int par_a = 0;                    // parity of the blocks of the current step
@@ -324,14 +325,14 @@ __device__ __forceinline__ unsigned ld_ctl(const unsigned int* p) {
 // The per-step kernels below are bodies over (workgroup bid of nb): the __global__ wrappers pass
 // blockIdx.x / gridDim.x, and the fused small-deck kernels (one workgroup, "Small decks") run
 // several bodies back to back with a workgroup barrier between them.
-// (multi-GPU mirror: g2l maps a global touched node to this rank's copy in lfext, -1 if none;
-// null without a mirror)
+// (multi-GPU: the touched nodes are global ids of this rank's nodes, g2l maps them into fext)
 __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* bbox, int npairs, unsigned int* ctl,
                                            unsigned int* evs, unsigned int* ccnt, int force, const int* del_any,
                                            int t, const double* t_rd, const int* touched_prev, int tsel,
-                                           double* fext, const int* g2l = nullptr, double* lfext = nullptr) {
+                                           double* fext, const int* g2l = nullptr, int* zero_hdr = nullptr) {
     if (t_rd) t = (int)*t_rd + 1;  // graph mode: step number from the device counter
     const int i = bid * blockDim.x + threadIdx.x;
+    if (zero_hdr && i < 2) zero_hdr[i] = 0;  // multi-GPU: this step's bin block (count, overflow)
     if (i < kEvShards) evs[i * kShardStride] = 0;
     if (i < kCandShards) ccnt[i * kShardStride] = 0;
     for (int q = i; q < 12 * npairs; q += nb * blockDim.x)
@@ -339,7 +340,7 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
     if (i == 0) {
         ctl[kEv] = 0;
         ctl[kDirty] = force ? 1u : 0u;
-        ctl[kDel] = (!force && *del_any == t - 1) ? 1u : 0u;
+        ctl[kDel] = (!force && del_any && *del_any == t - 1) ? 1u : 0u;
         ctl[kNdel] = 0;
         ctl[kNcand] = 0;
         ctl[kCandOver] = 0;
@@ -348,26 +349,18 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
     }
     const int np = (int)ld_ctl(&ctl[kTouched + 1 - tsel]);
     for (int q = i; q < np; q += nb * blockDim.x) {
-        const int n = touched_prev[q];
-        fext[3 * (long long)n] = 0.0;
-        fext[3 * (long long)n + 1] = 0.0;
-        fext[3 * (long long)n + 2] = 0.0;
-        if (g2l) {
-            const long long l = g2l[n];
-            if (l >= 0) {
-                lfext[3 * l] = 0.0;
-                lfext[3 * l + 1] = 0.0;
-                lfext[3 * l + 2] = 0.0;
-            }
-        }
+        const long long n = g2l ? g2l[touched_prev[q]] : touched_prev[q];  // (multi-GPU: only local nodes)
+        fext[3 * n] = 0.0;
+        fext[3 * n + 1] = 0.0;
+        fext[3 * n + 2] = 0.0;
     }
 }
 
 __global__ void k_ct_reset(unsigned long long* bbox, int npairs, unsigned int* ctl, unsigned int* evs,
                            unsigned int* ccnt, int force, const int* del_any, int t, const double* t_rd,
-                           const int* touched_prev, int tsel, double* fext, const int* g2l, double* lfext) {
+                           const int* touched_prev, int tsel, double* fext, const int* g2l, int* zero_hdr) {
     reset_body(blockIdx.x, gridDim.x, bbox, npairs, ctl, evs, ccnt, force, del_any, t, t_rd, touched_prev, tsel,
-               fext, g2l, lfext);
+               fext, g2l, zero_hdr);
 }
 
 struct StepIn {
@@ -1290,11 +1283,11 @@ __global__ void k_ct_scatter(unsigned int* ctl, const unsigned int* evs, long lo
 // external_force = 0.0 + (sum of the node's terms), summed in double-double and rounded once
 __device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ctl, int tsel, const int* touched,
                                          const int* toff, const int* tcnt, const double* terms, double* fext,
-                                         const int* g2l = nullptr, double* lfext = nullptr) {
+                                         const int* g2l = nullptr) {
 #pragma clang fp contract(off)
     const int nt = (int)ld_ctl(&ctl[kTouched + tsel]);
     for (int q = bid * blockDim.x + threadIdx.x; q < nt; q += nb * blockDim.x) {
-        const long long n = touched[q];
+        const long long n = g2l ? g2l[touched[q]] : touched[q];
         const int a = toff[q], b = a + tcnt[q];
         for (int c = 0; c < 3; ++c) {
             double s = 0.0, e = 0.0;
@@ -1308,17 +1301,12 @@ __device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ct
             }
             fext[3 * n + c] = s + e;
         }
-        if (g2l) {  // multi-GPU mirror: this rank's copy of the node
-            const long long l = g2l[n];
-            if (l >= 0)
-                for (int c = 0; c < 3; ++c) lfext[3 * l + c] = fext[3 * n + c];
-        }
     }
 }
 
 __global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
-                         const double* terms, double* fext, const int* g2l, double* lfext) {
-    sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext, g2l, lfext);
+                         const double* terms, double* fext, const int* g2l) {
+    sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext, g2l);
 }
 
 // ---- small decks: fused single-workgroup phases ------------------------------------------------
@@ -1383,6 +1371,18 @@ __device__ __forceinline__ int xhdr(const char* blk, int w) {
     return __hip_atomic_load(reinterpret_cast<const int*>(blk) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 constexpr size_t kXHdr = 16;
+constexpr int kNxCount = hkc::Xrank::kNx;
+
+// every rank's block header (count, overflow, last deletion step, full) -> LDS, one lane per rank:
+// the loads of all ranks in flight together, not a dependent chain on one thread
+__device__ __forceinline__ void load_hdrs(const XBlk& xb, int nr, int4* s_h) {
+    const int q = (int)threadIdx.x;
+    if (q < nr) {
+        const char* b = xb.p[q];
+        s_h[q] = make_int4(xhdr(b, 0), xhdr(b, 1), xhdr(b, 2), xhdr(b, 3));
+    }
+    __syncthreads();
+}
 
 struct EvRec {
     int n[4];     // i, j0, j1, j2 (global node ids)
@@ -1414,13 +1414,13 @@ __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long 
 
 // rank prefix of the blocks' record counts in LDS (each clamped to the block capacity); block 0
 // publishes the event total
-__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const XBlk& xb, int nr, long long* s_off,
+__device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const int4* s_h, int nr, long long* s_off,
                                                  long long cap, bool publish) {
     if (threadIdx.x == 0) {
         long long run = 0;
         for (int q = 0; q < nr; ++q) {
             s_off[q] = run;
-            run += min((long long)xhdr(xb.p[q], 0), cap);
+            run += min((long long)s_h[q].x, cap);
         }
         s_off[nr] = run;
         if (publish && blockIdx.x == 0) {
@@ -1445,13 +1445,13 @@ __device__ __forceinline__ const EvRec* rank_ev(const XBlk& xb, const long long*
 
 // any rank's block over its capacity or flagged: poison step pstep on every rank (all read the same
 // headers); xctl records which exchange (bit) for the retry
-__device__ __forceinline__ void x_overflow_check(const XBlk& xb, int nr, long long cap, int* poison, int pstep,
+__device__ __forceinline__ void x_overflow_check(const int4* s_h, int nr, long long cap, int* poison, int pstep,
                                                  int* xctl, int bit) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         bool local = false, over = false;  // a rank's own buffers overflowed / the exchange block
         for (int q = 0; q < nr; ++q) {
-            local |= xhdr(xb.p[q], 1) != 0;
-            over |= (long long)xhdr(xb.p[q], 0) > cap;
+            local |= s_h[q].y != 0;
+            over |= (long long)s_h[q].x > cap;
         }
         if (over) atomicOr(xctl, bit);
         if (over || local) {
@@ -1463,19 +1463,36 @@ __device__ __forceinline__ void x_overflow_check(const XBlk& xb, int nr, long lo
     }
 }
 
-__global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, int* cnt, int* touched, int* tpos,
-                             int tsel, int* poison, int pstep, int* xctl) {
+// the gathered record counts of exchange x (a full deletion block counts 0): the step's (read back
+// for the capacities two steps later) and their maxima (the growth after an overflow). Recorded by
+// the kernel that consumes the blocks, so no pointer to a peer's block outlives its step.
+__device__ __forceinline__ void x_counts(const int4* s_h, int nr, int x, int* xctl, int* hc) {
+    const int q = (int)threadIdx.x;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && q < nr) {
+        const int v = (x == 0 && s_h[q].w) ? 0 : s_h[q].x;
+        xctl[4 + x * nr + q] = v;
+        atomicMax(&xctl[4 + (kNxCount + x) * nr + q], v);
+        hc[x * nr + q] = v;  // host-mapped ring slot of the step (no copy launch)
+    }
+}
+
+// every rank's events; only the terms of this rank's nodes (g2l >= 0) are counted and summed
+__global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, const int* g2l, int* cnt, int* touched,
+                             int* tpos, int tsel, int* poison, int pstep, int* xctl, int* hc) {
     __shared__ long long s_off[kMaxXRanks + 1];
     __shared__ unsigned s_app[2];
-    x_overflow_check(xb, nr, cap, poison, pstep, xctl, 4);
-    const long long n = 4 * rank_prefix(ctl, xb, nr, s_off, cap, true);
+    __shared__ int4 s_h[kMaxXRanks];
+    load_hdrs(xb, nr, s_h);
+    x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 4);
+    x_counts(s_h, nr, 2, xctl, hc);
+    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, cap, true);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
         bool first = false;
         if (e < n) {
             node = rank_ev(xb, s_off, nr, e >> 2)->n[e & 3];
-            first = atomicAdd(&cnt[node], 1) == 0;
+            first = g2l[node] >= 0 && atomicAdd(&cnt[node], 1) == 0;
         }
         const unsigned q = block_append(&ctl[kTouched + tsel], first, s_app);
         if (first) {
@@ -1485,16 +1502,19 @@ __global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, 
     }
 }
 
-__global__ void k_ct_scatter_g(XBlk xb, long long cap, int nr, unsigned int* ctl, const int* toff, const int* tpos,
-                               int* cnt, double* terms) {
+__global__ void k_ct_scatter_g(XBlk xb, long long cap, int nr, const int* g2l, unsigned int* ctl, const int* toff,
+                               const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
     __shared__ long long s_off[kMaxXRanks + 1];
-    const long long n = 4 * rank_prefix(ctl, xb, nr, s_off, cap, false);
+    __shared__ int4 s_h[kMaxXRanks];
+    load_hdrs(xb, nr, s_h);
+    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, cap, false);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
         const EvRec* r = rank_ev(xb, s_off, nr, e >> 2);
         const int role = (int)(e & 3);
         const int node = r->n[role];
+        if (g2l[node] < 0) continue;
         const int slot = toff[tpos[node]] + atomicSub(&cnt[node], 1) - 1;  // leaves cnt zeroed
         double* o = terms + 3 * (long long)slot;
         if (role == 0) {  // c_force3[i] += f
@@ -1512,11 +1532,16 @@ __global__ void k_ct_scatter_g(XBlk xb, long long cap, int nr, unsigned int* ctl
 // deletions of this rank since the last pack -> its block (global element, step); full: every local
 // deletion step (after a state reset / upload / overflow); the header carries the rank's last
 // deletion step
+// (count of this block: zeroed by the pack of the other parity, which also zeroes the other
+// block's for the next pack -- every rank has read that one by now; a step without a deletion
+// packs nothing)
 __global__ void k_xr_dpack(const int* del_step, const int* del_any, int nEloc, long long E0, int* last_del, char* blk,
-                           long long cap, int full) {
+                           char* other, long long cap, int full, int t) {
     int* h = reinterpret_cast<int*>(blk);
     int* pl = reinterpret_cast<int*>(blk + kXHdr);
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nEloc; e += gridDim.x * blockDim.x) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<int*>(other)[0] = 0;
+    const bool none = !full && *del_any != t;  // block-uniform
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; !none && e < nEloc; e += gridDim.x * blockDim.x) {
         const int d = del_step[e];
         if (full) {
             pl[e] = d;
@@ -1538,28 +1563,41 @@ __global__ void k_xr_dpack(const int* del_step, const int* del_any, int nEloc, l
 // every rank's deletion block -> the global deletion steps; block 0 also the global last deletion
 // step and the overflow check (a list beyond its capacity poisons the step; it is packed again,
 // full, for the retry)
+// The incremental blocks also hold exactly the elements deleted in the previous step: they go to
+// the deletion list of the live-list update (k_ct_find_del's job on one GPU), and block 0 sets the
+// update flag (after k_ct_reset, which clears the list). A full block comes with a full rebuild
+// of the live lists on every rank (state reset, upload, overflow retry), which needs no list.
 __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del, long long nE_g,
-                             int* poison, int pstep, int* xctl) {
+                             int* poison, int t, int* xctl, int* hc, unsigned int* ctl, int* dlist) {
     const int q = (int)blockIdx.y;
     const char* b = xb.p[q];
     const int* pl = reinterpret_cast<const int*>(b + kXHdr);
-    if (xhdr(b, 3)) {
+    __shared__ int4 s_h[kMaxXRanks];
+    load_hdrs(xb, nr, s_h);
+    x_counts(s_h, nr, 0, xctl, hc);
+    if (s_h[q].w) {
         const long long e0 = e_off[q], ne = e_off[q + 1] - e0;
         for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < ne; k += (long long)gridDim.x * blockDim.x)
             g_del[e0 + k] = pl[k];
     } else {
-        const long long n = min((long long)xhdr(b, 0), cap);
-        for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
-            g_del[pl[2 * k]] = pl[2 * k + 1];
+        const long long n = min((long long)s_h[q].x, cap);
+        for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n;
+             k += (long long)gridDim.x * blockDim.x) {
+            const int e = pl[2 * k], d = pl[2 * k + 1];
+            g_del[e] = d;
+            if (d == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = e;
+        }
     }
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         int mx = 0;
         bool over = false;
         for (int r = 0; r < nr; ++r) {
-            mx = max(mx, xhdr(xb.p[r], 2));
-            over |= !xhdr(xb.p[r], 3) && (long long)xhdr(xb.p[r], 0) > cap;
+            mx = max(mx, s_h[r].z);
+            over |= !s_h[r].w && (long long)s_h[r].x > cap;
         }
         g_del[nE_g + 1] = mx;
+        ctl[kDel] = (ctl[kDirty] == 0 && mx == t - 1) ? 1u : 0u;
+        const int pstep = t;
         if (over) {
             atomicOr(xctl, 1);
             if (poison[0] == 0) {
@@ -1591,12 +1629,36 @@ __global__ void k_xr_boxcomb(XBox xb, int nr, int n, unsigned long long* out) {
     out[q] = v;
 }
 
-// A2: this rank's live i-nodes inside their pair's range box -> compact records in its block
-__global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
-                                               const int* ni_pair, const int* ni_node, const PairParam* par,
-                                               const unsigned long long* bbox, char* blk, long long cap, int sb) {
+// A2: the pair boxes of every rank combined (each workgroup in LDS; workgroup 0 also stores them
+// for the triangle prefilter of A3), then this rank's live i-nodes inside their pair's range box ->
+// compact records in its block. xb: the in-process peers' partial boxes (nxb = nranks), or the
+// RCCL all-reduced one (nxb = 1, max words complemented: flip). npairs > kLdsPairs: k_xr_boxcomb
+// combined them into boxg before (nxb = 0).
+constexpr int kLdsPairs = 64;
+__global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, int nseg, const int* reg,
+                                               const int* ni_live, const int* ni_pair, const int* ni_node,
+                                               const PairParam* par, XBox xb, int nxb, int flip, int npairs,
+                                               unsigned long long* boxg, char* blk, long long cap, int sb) {
 #pragma clang fp contract(off)
     __shared__ unsigned s_app[2];
+    __shared__ alignas(16) unsigned long long s_bb[12 * kLdsPairs];
+    const unsigned long long* bbox = boxg;
+    if (nxb > 0) {
+        for (int q = (int)threadIdx.x; q < 12 * npairs; q += kB) {
+            const bool mx = ((q % 12) / 3) % 2 == 1;
+            unsigned long long v = xb.p[0][q];
+            for (int r = 1; r < nxb; ++r) {
+                const unsigned long long w = xb.p[r][q];
+                v = mx ? umax64(v, w) : umin64(v, w);
+            }
+            if (flip && mx) v = ~v;
+            s_bb[q] = v;
+            if (blockIdx.x == 0) boxg[q] = v;
+        }
+        __syncthreads();
+        bbox = s_bb;
+    }
+    if ((int)blockIdx.x / sb >= nseg) return;  // (nseg = 0: one workgroup, the boxes only)
     const Seg sg = segs[blockIdx.x / sb];
     if (sg.side != 0) return;  // block-uniform
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
@@ -1630,10 +1692,13 @@ __global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, const 
 // A3: bucket of every gathered record (ranks in order) and the bucket counts; xctl bit 2 and the
 // poison when a rank binned more than its block holds
 __global__ void k_xr_bcount(XBlk xb, int nr, long long cap, const PairParam* par, int* bq, int* bcnt, int* poison,
-                            int pstep, int* xctl) {
-    x_overflow_check(xb, nr, cap, poison, pstep, xctl, 2);
+                            int pstep, int* xctl, int* hc) {
+    __shared__ int4 s_h[kMaxXRanks];
+    load_hdrs(xb, nr, s_h);
+    x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 2);
+    x_counts(s_h, nr, 1, xctl, hc);
     const int q = (int)blockIdx.y;
-    const long long n = min((long long)xhdr(xb.p[q], 0), cap);
+    const long long n = min((long long)s_h[q].x, cap);
     const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
         const BEnt& e = rec[k].e;
@@ -1815,7 +1880,7 @@ void contact_destroy(hakai_ctx* c) {
     if (C->d_tmp) (void)hipFree(C->d_tmp);
     if (Xrank* X = C->xr) {
         (void)hipDeviceSynchronize();  // in-process peers may still read this rank's blocks
-        dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->g_fext); dfree(X->d_last_del);
+        dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->d_last_del);
         for (int x = 0; x < Xrank::kNx; ++x) {
             dfree(X->d_send[x][0]);
             dfree(X->d_send[x][1]);
@@ -1888,10 +1953,6 @@ static int xr_buffers(hakai_ctx* c) {
         HIPCHK(dalloc(&C->d_bvel, (size_t)nb));
         C->blist_cap = nb;
     }
-    // the "current step" block pointers (counts, overflow growth) may name freed blocks: point them
-    // at this rank's own (valid, possibly empty) blocks until the next exchange sets them
-    for (int x = 0; x < Xrank::kNx; ++x)
-        for (int q = 0; q < X->nranks; ++q) X->xb_last[x].p[q] = X->d_send[x][0];
     return 0;
 }
 
@@ -1928,11 +1989,11 @@ static int xr_gather(hakai_ctx* c, int x, int par, size_t blk, XBlk& xb) {
 static int xr_dpack(hakai_ctx* c, bool full) {
     Xrank* X = c->contact->xr;
     const int par = (int)(X->seq & 1);
-    HIPCHK(hipMemsetAsync(X->d_send[0][par], 0, kXHdr, c->stream));
+    if (full) HIPCHK(hipMemsetAsync(X->d_send[0][par], 0, kXHdr, c->stream));
     const int n = (int)std::max<long long>(X->nEloc, 1);
     hipLaunchKernelGGL(k_xr_dpack, dim3((unsigned)std::min((n + kB - 1) / kB, 1024)), dim3(kB), 0, c->stream,
                        c->d_del_step, c->d_del_step + c->nEp + 1, (int)X->nEloc, X->E0, X->d_last_del,
-                       X->d_send[0][par], X->cap[0], full ? 1 : 0);
+                       X->d_send[0][par], X->d_send[0][1 - par], X->cap[0], full ? 1 : 0, X->t_a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(X->ev_sent[0][par], c->stream));
     X->full_del = full;
@@ -1958,14 +2019,6 @@ static int xr_grow(hakai_ctx* c, int x0, int x1) {
     return xr_buffers(c);
 }
 
-__global__ void k_xr_counts(XBlk d, XBlk b, XBlk e, int nr, int* out) {
-    const int q = threadIdx.x;
-    if (q >= nr) return;
-    out[q] = xhdr(d.p[q], 3) ? 0 : xhdr(d.p[q], 0);
-    out[nr + q] = xhdr(b.p[q], 0);
-    out[2 * nr + q] = xhdr(e.p[q], 0);
-}
-
 int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
     Contact* C = c->contact;
     if (!C) return 0;
@@ -1976,7 +2029,7 @@ int contact_state_reset(hakai_ctx* c, const double* velo0_host) {
                               c->stream));
     if (Xrank* X = C->xr) {  // every deletion step travels with the next block
         HIPCHK(hipMemsetAsync(X->g_del, 0, ((size_t)X->nE_g + 2) * sizeof(int), c->stream));
-        HIPCHK(hipMemsetAsync(X->d_xctl, 0, 4 * sizeof(int), c->stream));
+        HIPCHK(hipMemsetAsync(X->d_xctl, 0, (4 + 2 * (size_t)Xrank::kNx * X->nranks) * sizeof(int), c->stream));
         X->seq = 0;
         X->cnt_seq = 0;
         return xr_dpack(c, true);
@@ -2027,19 +2080,15 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
     const int* del_any = c->d_del_step + c->nEp + 1;
     double* fext = c->d_fext;
     unsigned long long* bbox = C->d_bbox;
+    XBlk xb{};
     if (X) {
         if (int rc = xr_grow(c, 1, Xrank::kNx)) return rc;
         X->t_a = in.t;
         X->par_a = (int)(X->seq & 1);
-        XBlk xb;
+        X->sl_a = (int)(X->cnt_seq & 3);
         if (int rc = xr_gather(c, 0, X->par_a, xr_blk(X, 0, X->full_del), xb)) return rc;
-        const unsigned gx = (unsigned)std::min<long long>(std::max<long long>((X->maxEloc + kB - 1) / kB, 1), 256);
-        hipLaunchKernelGGL(k_xr_dunpack, dim3(gx, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks,
-                           X->d_eoff, X->cap[0], X->g_del, X->nE_g, c->d_poison, in.t, X->d_xctl);
-        X->xb_last[0] = xb;
         del_step = X->g_del;
         del_any = X->g_del + X->nE_g + 1;
-        fext = X->g_fext;
         bbox = X->d_box[X->par_a];
     }
     if ((long long)in.t != C->last_t + 1 || C->always_rebuild) C->force_rebuild = true;
@@ -2062,8 +2111,14 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                            C->ntile > 0 ? 1 : 0);
     } else {
         hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
-                           C->force_rebuild ? 1 : 0, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext,
-                           X ? X->d_g2l : nullptr, X ? c->d_fext : nullptr);
+                           C->force_rebuild ? 1 : 0, X ? nullptr : del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel,
+                           fext, X ? X->d_g2l : nullptr, X ? (int*)X->d_send[1][X->par_a] : nullptr);
+        if (X) {  // the deletions of every rank (after the reset: they fill its deletion list)
+            const unsigned gx = (unsigned)std::min<long long>(std::max<long long>((X->maxEloc + kB - 1) / kB, 1), 256);
+            hipLaunchKernelGGL(k_xr_dunpack, dim3(gx, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks,
+                               X->d_eoff, X->cap[0], X->g_del, X->nE_g, c->d_poison, in.t, X->d_xctl,
+                               X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks, C->d_ctl, C->d_dlist);
+        }
         if (C->ntile > 0) {
             LiveIn L;
             L.ni_orig = C->d_ni_orig; L.ni_aptr = C->d_ni_aptr; L.ni_add = C->d_ni_add;
@@ -2081,9 +2136,10 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                 hipLaunchKernelGGL(k_ct_live_write, dim3(gt), dim3(kB), 0, s, C->d_ctl, L, tl, C->ntile, C->d_tile_off,
                                    C->d_reg_first, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
             }
-            // incremental update (steps after a deletion)
-            hipLaunchKernelGGL(k_ct_find_del, dim3(C->g_del), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
-                               c->g_trd, C->d_dlist);
+            // incremental update (steps after a deletion; multi-GPU: k_xr_dunpack listed them)
+            if (!X)
+                hipLaunchKernelGGL(k_ct_find_del, dim3(C->g_del), dim3(kB), 0, s, C->d_ctl, del_step, (int)C->nE, in.t,
+                                   c->g_trd, C->d_dlist);
             hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
                                c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
         }
@@ -2156,7 +2212,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
     hipLaunchKernelGGL(k_ct_scatter, dim3(ge), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards, C->d_ev_nodes,
                        C->d_ev_f, C->d_toff, C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, c->d_fext, nullptr, nullptr);
+                       C->d_terms, c->d_fext, nullptr);
     HIPCHK(hipGetLastError());
     C->use_velo0 = false;
     return 0;
@@ -2188,12 +2244,15 @@ static int xr_a2(hakai_ctx* c, double d_time) {
     hipStream_t s = c->stream;
     const int par = X->par_a, nw = 12 * C->npairs;
     const unsigned gw = (unsigned)((nw + kB - 1) / kB);
-    if (comm_is_rccl(c)) {
+    XBox xb{};
+    int nxb = 0, flip = 0;
+    if (comm_is_rccl(c)) {  // min words as they are, max words complemented: one MIN all-reduce, in place
         hipLaunchKernelGGL(k_xr_boxflip, dim3(gw), dim3(kB), 0, s, X->d_box[par], nw);
-        if (int rc = comm_allreduce_min_u64(c, X->d_box[par], X->d_boxg, (size_t)nw)) return rc;
-        hipLaunchKernelGGL(k_xr_boxflip, dim3(gw), dim3(kB), 0, s, X->d_boxg, nw);
+        if (int rc = comm_allreduce_min_u64(c, X->d_box[par], X->d_box[par], (size_t)nw)) return rc;
+        xb.p[0] = X->d_box[par];
+        nxb = 1;
+        flip = 1;
     } else {
-        XBox xb{};
         for (int q = 0; q < X->nranks; ++q) {
             hakai_ctx* pc = comm_peer_ctx(c, q);
             Xrank* P = pc && pc->contact ? pc->contact->xr : nullptr;
@@ -2202,14 +2261,19 @@ static int xr_a2(hakai_ctx* c, double d_time) {
             if (q != X->rank) HIPCHK(hipStreamWaitEvent(s, P->ev_box[par], 0));
             xb.p[q] = P->d_box[par];
         }
-        hipLaunchKernelGGL(k_xr_boxcomb, dim3(gw), dim3(kB), 0, s, xb, X->nranks, nw, X->d_boxg);
+        nxb = X->nranks;
     }
-    HIPCHK(hipMemsetAsync(X->d_send[1][par], 0, kXHdr, s));
-    if (C->nseg > 0) {
+    if (C->npairs > kLdsPairs) {  // combined in global memory first
+        if (flip) hipLaunchKernelGGL(k_xr_boxflip, dim3(gw), dim3(kB), 0, s, X->d_box[par], nw);
+        hipLaunchKernelGGL(k_xr_boxcomb, dim3(gw), dim3(kB), 0, s, xb, nxb, nw, X->d_boxg);
+        nxb = 0;
+        flip = 0;
+    }
+    {  // (bin block header zeroed by this step's k_ct_reset)
         StepIn in = step_in(c, X->t_a, d_time);
-        hipLaunchKernelGGL(k_xr_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, (const Seg*)C->d_seg, C->d_reg,
-                           C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, X->d_boxg, X->d_send[1][par], X->cap[1],
-                           C->g_seg);
+        hipLaunchKernelGGL(k_xr_bin, dim3((unsigned)std::max(1, C->nseg * C->g_seg)), dim3(kB), 0, s, in,
+                           (const Seg*)C->d_seg, C->nseg, C->d_reg, C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par,
+                           xb, nxb, flip, C->npairs, X->d_boxg, X->d_send[1][par], X->cap[1], C->g_seg);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(X->ev_sent[1][par], s));
@@ -2225,10 +2289,10 @@ static int xr_a3(hakai_ctx* c, double d_time) {
     const int par = X->par_a;
     XBlk xb;
     if (int rc = xr_gather(c, 1, par, xr_blk(X, 1), xb)) return rc;
-    X->xb_last[1] = xb;
     const unsigned gb = (unsigned)std::min<long long>(std::max<long long>((X->cap[1] + kB - 1) / kB, 1), 128);
     hipLaunchKernelGGL(k_xr_bcount, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks, X->cap[1], C->d_par,
-                       X->d_bq, C->d_bcnt, c->d_poison, X->t_a, X->d_xctl);
+                       X->d_bq, C->d_bcnt, c->d_poison, X->t_a, X->d_xctl,
+                       X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks);
     if (int rc = bucket_scan(c)) return rc;
     hipLaunchKernelGGL(k_xr_fill, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->cap[1], X->d_bq, C->d_boff,
                        C->d_bcnt, C->d_blist, C->d_bvel);
@@ -2277,24 +2341,20 @@ int contact_step_b(hakai_ctx* c) {
     const int par = X->par_a, nr = X->nranks;
     XBlk xb;
     if (int rc = xr_gather(c, 2, par, xr_blk(X, 2), xb)) return rc;
-    X->xb_last[2] = xb;
     const int tsel = C->tsel;
     const unsigned ge = (unsigned)C->g_ev;
-    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, X->cap[2], nr, C->d_cnt,
-                       C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, X->t_a, X->d_xctl);
+    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, X->cap[2], nr, X->d_g2l, C->d_cnt,
+                       C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, X->t_a, X->d_xctl,
+                       X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * nr);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
-    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, X->cap[2], nr, C->d_ctl, C->d_toff, C->d_tpos,
-                       C->d_cnt, C->d_terms);
+    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, X->cap[2], nr, X->d_g2l, C->d_ctl, C->d_toff,
+                       C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
-                       C->d_terms, X->g_fext, X->d_g2l, c->d_fext);
-    // the step's counts, read by xr_grow two steps later
-    const long long sl = X->cnt_seq & 3;
-    hipLaunchKernelGGL(k_xr_counts, dim3(1), dim3(kMaxXRanks), 0, s, X->xb_last[0], X->xb_last[1], xb, nr,
-                       X->d_xctl + 4);
-    HIPCHK(hipMemcpyAsync(X->h_cnt + (size_t)sl * Xrank::kNx * nr, X->d_xctl + 4, Xrank::kNx * nr * sizeof(int),
-                          hipMemcpyDeviceToHost, s));
-    HIPCHK(hipEventRecord(X->ev_cnt[sl], s));
+                       C->d_terms, c->d_fext, X->d_g2l);
+    // the step's counts (k_xr_dunpack, k_xr_bcount, k_ct_count_g wrote them into the host-mapped
+    // ring slot), read by xr_grow two steps later
+    HIPCHK(hipEventRecord(X->ev_cnt[X->sl_a], s));
     ++X->cnt_seq;
     HIPCHK(hipGetLastError());
     return 0;
@@ -2322,24 +2382,22 @@ void contact_after_overflow(hakai_ctx* c, long long steps_since_reset) {
     C->use_velo0 = steps_since_reset == 0;
     C->last_t = -1;
     if (Xrank* X = C->xr) {
-        int xc[4 + 3 * kMaxXRanks] = {0};
+        int xc[4 + 2 * Xrank::kNx * kMaxXRanks] = {0};
         const int nr = X->nranks;
-        hipLaunchKernelGGL(k_xr_counts, dim3(1), dim3(kMaxXRanks), 0, c->stream, X->xb_last[0], X->xb_last[1],
-                           X->xb_last[2], nr, X->d_xctl + 4);
-        if (hipMemcpyAsync(xc, X->d_xctl, (4 + Xrank::kNx * nr) * sizeof(int), hipMemcpyDeviceToHost, c->stream) !=
-                hipSuccess ||
+        const size_t n = 4 + 2 * (size_t)Xrank::kNx * nr;
+        if (hipMemcpyAsync(xc, X->d_xctl, n * sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
             return;
         X->retry = false;
-        if (xc[0] & 7) {
+        if (xc[0] & 7) {  // past the largest count of the call (its steps after the poisoned one included)
             for (int x = 0; x < Xrank::kNx; ++x) {
                 long long mx = 0;
-                for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, xc[4 + x * nr + q]);
+                for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, xc[4 + (Xrank::kNx + x) * nr + q]);
                 if (xc[0] & (1 << x)) X->cap[x] = std::min(X->cap_max[x], std::max(2 * X->cap[x], 4 * mx));
             }
             X->retry = true;
         }
-        (void)hipMemsetAsync(X->d_xctl, 0, sizeof(int), c->stream);
+        (void)hipMemsetAsync(X->d_xctl, 0, n * sizeof(int), c->stream);
         if (xr_buffers(c) == 0) (void)xr_dpack(c, true);
     }
 }
@@ -2398,8 +2456,12 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipDeviceSynchronize());
         X->cap[x] = std::min<long long>(value, X->cap_max[x]);
         if (int rc = xr_buffers(c)) return rc;
-        // the next step's deletion block again, in the new layout
-        if (x == 0 && c->state_ok) return xr_dpack(c, true);
+        // the next step's deletion block again, in the new layout (a full block: every rank
+        // rebuilds its live lists)
+        if (x == 0 && c->state_ok) {
+            C->force_rebuild = true;
+            return xr_dpack(c, true);
+        }
         return 0;
     }
     if (!std::strcmp(key, "contact_full_rebuild")) {
@@ -2432,7 +2494,6 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(dalloc(&C->d_tcnt, (size_t)C->tcap));
         // the previous step's touched list is gone: clear external_force and its count
         HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), c->stream));
-        if (C->xr) HIPCHK(hipMemsetAsync(C->xr->g_fext, 0, 3 * (size_t)C->nN * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kTouched, 0, 2 * sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvMax, 0, sizeof(unsigned int), c->stream));
         HIPCHK(hipMemsetAsync(C->d_ctl + kEvShardMax, 0, sizeof(unsigned int), c->stream));
@@ -2936,20 +2997,20 @@ int xr_build(hakai_ctx* c, const OwnFilter& own, long long nNode, long long nEle
     HIPCHK(upload(&X->d_eoff, eoff, s));
     HIPCHK(dalloc(&X->g_del, (size_t)nElement + 2));
     HIPCHK(hipMemsetAsync(X->g_del, 0, ((size_t)nElement + 2) * sizeof(int), s));
-    HIPCHK(dalloc(&X->g_fext, 3 * (size_t)nNode));
-    HIPCHK(hipMemsetAsync(X->g_fext, 0, 3 * (size_t)nNode * sizeof(double), s));
     HIPCHK(dalloc(&X->d_last_del, (size_t)std::max<long long>(X->nEloc, 1)));
     HIPCHK(hipMemsetAsync(X->d_last_del, 0, (size_t)std::max<long long>(X->nEloc, 1) * sizeof(int), s));
-    HIPCHK(dalloc(&X->d_xctl, 4 + (size_t)hkc::Xrank::kNx * nr));
-    HIPCHK(hipMemsetAsync(X->d_xctl, 0, (4 + (size_t)hkc::Xrank::kNx * nr) * sizeof(int), s));
+    HIPCHK(dalloc(&X->d_xctl, 4 + 2 * (size_t)hkc::Xrank::kNx * nr));
+    HIPCHK(hipMemsetAsync(X->d_xctl, 0, (4 + 2 * (size_t)hkc::Xrank::kNx * nr) * sizeof(int), s));
     for (int p = 0; p < 2; ++p) {
         HIPCHK(dalloc(&X->d_box[p], 12 * (size_t)C->npairs));
         HIPCHK(hipEventCreateWithFlags(&X->ev_box[p], hipEventDisableTiming));
         for (int x = 0; x < hkc::Xrank::kNx; ++x) HIPCHK(hipEventCreateWithFlags(&X->ev_sent[x][p], hipEventDisableTiming));
     }
     HIPCHK(dalloc(&X->d_boxg, 12 * (size_t)C->npairs));
-    HIPCHK(hipHostMalloc((void**)&X->h_cnt, 4 * (size_t)hkc::Xrank::kNx * nr * sizeof(int), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&X->h_cnt, 4 * (size_t)hkc::Xrank::kNx * nr * sizeof(int),
+                         hipHostMallocMapped | hipHostMallocCoherent));
     std::fill(X->h_cnt, X->h_cnt + 4 * (size_t)hkc::Xrank::kNx * nr, 0);
+    HIPCHK(hipHostGetDevicePointer((void**)&X->d_hcnt, X->h_cnt, 0));
     for (auto& e : X->ev_cnt) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipStreamSynchronize(s));
     if (int rc = hkc::xr_buffers(c)) return rc;

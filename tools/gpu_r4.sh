@@ -10,6 +10,8 @@
 #              sockets: HAKAI_RCCL_SHARED_GPU=1)           -> gpurun_out/r4_rehearse2.json
 #   prof       rocprofv3 kernel trace of a short bench     -> gpurun_out/r4_prof/
 #   drift      fused-kernel drift on the reference decks  -> gpurun_out/r4_deck_drift.jsonl
+#   c4ranks    C4 contact per rank: one context, 2 and 4 in-process ranks -> gpurun_out/r4_c4_ranks.jsonl
+#   c4prof     rocprofv3 kernel trace of the C4 contact run, one context and 2 ranks -> gpurun_out/r4_c4prof_{1,2}/
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r4_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -34,6 +36,15 @@ for st in "$@"; do
     prof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_prof \
               -o r4 -- python bench.py --steps 50 --warmup 5 --cpu-baseline 0 || exit $? ;;
     drift) run 600 gpurun_out/r4_deck_drift.jsonl python tools/deck_drift.py || exit $? ;;
+    c4ranks) : > gpurun_out/r4_c4_ranks.jsonl
+        for r in 1 2 4; do
+            run 600 gpurun_out/r4_c4_ranks_$r.log python tools/bench_contact.py --ranks $r --steps 40 || exit $?
+            grep '^{' gpurun_out/r4_c4_ranks_$r.log >> gpurun_out/r4_c4_ranks.jsonl
+        done ;;
+    c4prof) for r in ${C4PROF_RANKS:-1 2}; do
+            run 600 gpurun_out/r4_c4prof_$r.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_c4prof_$r -o c4 \
+                -- python tools/bench_contact.py --ranks $r --steps 40 || exit $?
+        done ;;
     tests:*) run 1200 gpurun_out/r4_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
                  --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
