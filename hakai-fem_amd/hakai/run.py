@@ -5,8 +5,8 @@ main() with ARGS[1], :3729-3735) with the mesh split over ranks.
         -m hakai.run deck.inp out_dir            # one process per GPU, RCCL over xGMI
 
 Every rank reads the deck, computes the global lumped mass (v2/HAKAI_j.jl:183-218) and takes a
-contiguous global element range (hakai.dist.range_partition); contact decks mirror the global
-contact model on every rank (hakai_set_contact_global). Each step is bit-identical to the
+contiguous global element range (hakai.dist.range_partition); contact decks pass the global
+contact model to every rank, which keeps its own share of it (hakai_set_contact_global). Each step is bit-identical to the
 single-GPU run. At the output cadence (floor(time_num/100) steps, :471-480, :932-942) the ranks send
 their state to rank 0, which uploads it into an output context holding the whole mesh, takes the
 node averages there (cal_node_stress_strain, :3408-3486) and writes out_dir/file%03d.vtk (:3517-3717)

@@ -160,8 +160,8 @@ int hakai_lumped_mass(int64_t nNode, const double* coordmat, int64_t nElement, c
                       double mass_scaling, double* diag_M, double* elementVolume);
 
 /* ---- profiling: per-kernel device time measured with HIP events on the context's stream ---- */
-/* HAKAI_K_CONTACT: the contact step (multi-GPU divided search: the search part); HAKAI_K_CONTACT_SUM:
- * the divided search's event all-gather and force sums (multi-GPU contact only). */
+/* HAKAI_K_CONTACT: the contact step (multi-GPU contact: phases A1-A3, the search); HAKAI_K_CONTACT_SUM:
+ * multi-GPU contact phase B (the gathered events' force sums of the rank's nodes). */
 enum { HAKAI_K_ELEMENT = 0, HAKAI_K_NODAL = 1, HAKAI_K_BC = 2, HAKAI_K_EXCHANGE = 3, HAKAI_K_CONTACT = 4,
        HAKAI_K_CONTACT_SUM = 5, HAKAI_K_COUNT = 6 };
 int hakai_profile_enable(hakai_ctx* ctx, int on);  /* all kernels on / off; resets the totals */
@@ -188,9 +188,11 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
- *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild",
- *   "contact_mirror_chunks", "contact_mirror_deletions": contact buffers and rebuild policy;
- *   "contact_divide"    multi-GPU contact: 1 (default) divided search, 0 replicated search;
+ *   "contact_event_cap", "contact_candidate_cap", "contact_full_rebuild": contact buffers and
+ *                       rebuild policy;
+ *   "contact_exchange_deletions", "contact_exchange_bins", "contact_exchange_events": multi-GPU
+ *                       contact, records per rank block of each per-step exchange (they also grow
+ *                       on their own; call on every rank between steps);
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0). */
@@ -215,15 +217,16 @@ int hakai_set_contact_cp(hakai_ctx* ctx, int32_t contact_flag, const int64_t* el
  * GLOBAL model (the arrays of hakai_upload_model / hakai_set_contact_cp for the whole mesh, and
  * its global diag_M), local_node_global[l] = global 1-based id of this rank's local node l, and
  * rank_elem_off[0..nranks] = the ranks' contiguous global element ranges (0-based, rank r holds
- * [rank_elem_off[r], rank_elem_off[r+1])). Every rank then mirrors the global contact model and
- * all-gathers, each step, the displacements of the contact nodes and the deletion steps of the
- * contact elements; the contact force is bit-identical to one GPU. hakai_set_contact[_cp] on a
- * rank with a communicator returns HAKAI_ERR_STATE. With a mirror, hakai_step, hakai_reset_state,
- * hakai_upload_state, hakai_contact_force and hakai_set_tuning("contact_mirror_chunks" /
- * "contact_mirror_deletions") are collective: every rank calls them in the same order. */
-/* (Divided search, tuning "contact_divide", default 1: rank r searches the candidate triangles
- * j % nranks == r and the ranks' events are all-gathered each step -- the force sums, and so the
- * results, are unchanged; 0 = every rank searches every triangle.) */
+ * [rank_elem_off[r], rank_elem_off[r+1])). Owner-computed search: each rank keeps the triangles
+ * of its elements and the contact nodes it owns (the rank of the node's lowest incident element);
+ * per step the deletions are all-gathered, the pair boxes all-reduced (exact min/max), the own
+ * contact-zone nodes binned and all-gathered, each rank searches its own triangles, and the events
+ * are all-gathered; each rank sums the forces of its own nodes. The contact force is
+ * bit-identical to one GPU. hakai_set_contact[_cp] on a rank with a communicator returns
+ * HAKAI_ERR_STATE. hakai_step, hakai_reset_state, hakai_upload_state and
+ * hakai_set_tuning("contact_exchange_*") are collective: every rank calls them in the same order.
+ * An exchange capacity overflow grows the capacity and the step runs again (up to 8 times);
+ * hakai_contact_force is refused on such a rank (step the group instead). */
 int hakai_set_contact_global(hakai_ctx* ctx, int32_t contact_flag, int64_t nNode, const double* coordmat,
                              int64_t nElement, const int64_t* elementmat, const int64_t* element_material,
                              const int64_t* element_instance, const double* diag_M, const int64_t* local_node_global,
@@ -239,8 +242,8 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
  * max events in any step, prefiltered triangles, nodes with contact force, live triangles, live
  * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
  * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
- * [7] chunks of deletion-exposed contact nodes all ranks sent in the last step, [8] bytes of one
- * rank's per-step block (hakai_set_contact_global); [9] hash-grid buckets of all pairs (tables of
+ * [7] contact-zone nodes all ranks binned in the last step, [8] bytes of one rank's per-step
+ * exchange blocks at their capacities (hakai_set_contact_global); [9] hash-grid buckets of all pairs (tables of
  * more than 32 768 entries take the device-wide scan). */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
@@ -258,10 +261,10 @@ int hakai_comm_init(hakai_ctx* ctx, int rank, int nranks, const uint8_t id[128])
  * directly; across devices use hakai_comm_init). */
 int hakai_comm_init_local(hakai_ctx* ctx, int rank, int nranks, int64_t group_key);
 /* Steps an in-process group (the n contexts of hakai_comm_init_local, ctxs[r] = rank r) in lockstep,
- * n_steps steps from t_first: per step every rank's contact search (phase A) runs before any rank's
- * event exchange, force sums, nodal update and element update (phase B), so the divided multi-GPU
- * contact search works in one process. hakai_step on such a rank steps it alone (one step per call,
- * no divided contact). */
+ * n_steps steps from t_first: per step every rank's contact phase A1 (deletions, live lists, boxes),
+ * then every rank's A2 (box combine, binning), A3 (hash grid, triangle search), then every rank's
+ * phase B (event sums), nodal and element update, so the multi-GPU contact search works in one
+ * process. A contact rank of an in-process group cannot step alone (HAKAI_ERR_STATE). */
 int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_steps, double d_time);
 /* Interface description for this rank's local model ("multi-GPU"):
  * shared nodes (local 0-based ids, sorted by global id) with the rank range [lo, hi] of ranks

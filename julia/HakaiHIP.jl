@@ -153,8 +153,8 @@ end
 step!(c::Ctx, t_first, n, d_time) =
     check(ccall((:hakai_step, lib), Cint, (Ptr{Cvoid}, Float64, Int64, Float64), c.p, t_first, n, d_time))
 sync(c::Ctx) = check(ccall((:hakai_sync, lib), Cint, (Ptr{Cvoid},), c.p))
-# an in-process group (rank r = cs[r+1]) in lockstep: every rank's contact search, then every
-# rank's exchange and update, per step (the divided multi-GPU contact search in one process)
+# an in-process group (rank r = cs[r+1]) in lockstep: every rank's contact phases A1, A2, A3, then
+# every rank's event sums, exchange and update, per step (multi-GPU contact in one process)
 function step_group!(cs::Vector{Ctx}, t_first, n, d_time)
     ps = Ptr{Cvoid}[c.p for c in cs]
     check(ccall((:hakai_step_group, lib), Cint, (Ptr{Ptr{Cvoid}}, Int32, Float64, Int64, Float64), ps,
@@ -273,8 +273,9 @@ set_interface(c::Ctx, local_node::Vector{Int64}, rank_lo::Vector{Int32}, rank_hi
 set_element_offset(c::Ctx, offset) =
     check(ccall((:hakai_set_element_offset, lib), Cint, (Ptr{Cvoid}, Int64), c.p, offset))
 
-# multi-GPU contact: every rank mirrors the GLOBAL contact model (arguments as hakai_upload_model /
-# set_contact_cp for the whole mesh) plus its local->global node map and the ranks' element ranges
+# multi-GPU contact: every rank passes the GLOBAL contact model (arguments as hakai_upload_model /
+# set_contact_cp for the whole mesh) plus its local->global node map and the ranks' element ranges;
+# it keeps its own triangles and contact nodes (owner-computed search)
 function set_contact_global(c::Ctx, contact_flag, coordmat, elementmat, element_material,
                             element_instance::Vector{Int64}, diag_M, local_node_global::Vector{Int64},
                             rank_elem_off::Vector{Int64}, CPs)

@@ -12,6 +12,8 @@
 #   drift      fused-kernel drift on the reference decks  -> gpurun_out/r4_deck_drift.jsonl
 #   c4ranks    C4 contact per rank: one context, 2 and 4 in-process ranks -> gpurun_out/r4_c4_ranks.jsonl
 #   c4prof     rocprofv3 kernel trace of the C4 contact run, one context and 2 ranks -> gpurun_out/r4_c4prof_{1,2}/
+#   decks      reference decks end to end, both element modes, graphs -> gpurun_out/r4_decks.jsonl
+#   deckprof   rocprofv3 kernel trace of car-crash-N2k, 3200 steps, stream mode -> gpurun_out/r4_deckprof/
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r4_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -45,6 +47,10 @@ for st in "$@"; do
             run 600 gpurun_out/r4_c4prof_$r.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_c4prof_$r -o c4 \
                 -- python tools/bench_contact.py --ranks $r --steps 40 || exit $?
         done ;;
+    decks) run 900 gpurun_out/r4_decks.jsonl python tools/deck_bench.py --cpu-steps 0 || exit $? ;;
+    deckprof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_deckprof.log rocprofv3 --kernel-trace --stats \
+                  -d gpurun_out/r4_deckprof -o deck -- python tools/deck_bench.py --decks ${DECK:-car_crash_N2k} \
+                  --cpu-steps 0 --modes 1 --max-steps 3200 || exit $? ;;
     tests:*) run 1200 gpurun_out/r4_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
                  --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
