@@ -1569,6 +1569,9 @@ static int step_group_call(hakai_ctx** ctxs, int32_t n, double t_first, int64_t 
         const bool last = it == n_steps - 1;
         for (int ph : phases)
             for (int r = 0; r < n; ++r) {
+                // group_serial 2: the phase is enqueued behind a fixed sleep (≈0.3 ms), so its kernels
+                // run back to back as in a pipelined run, not at the host's enqueue pace
+                if (ctxs[0]->group_serial == 2) HIPCHK(hk::launch_hold(96, ctxs[r]->stream));
                 if (int rc = step_once(ctxs[r], t, d_time, last, ph)) return rc;
                 if (ph == kPhaseRest) ctxs[r]->tdev_next = -1;
                 if (ctxs[0]->group_serial) HIPCHK(hipStreamSynchronize(ctxs[r]->stream));
@@ -1700,7 +1703,7 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
         return 0;
     }
     if (!std::strcmp(key, "group_serial")) {  // timing: hakai_step_group drains each rank's phase
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "group_serial must be 0 or 1");
+        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "group_serial must be 0, 1 or 2");
         c->group_serial = (int)value;
         return 0;
     }

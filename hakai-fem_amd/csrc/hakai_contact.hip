@@ -23,7 +23,6 @@
 //     relative window (order-independent, no atomics on doubles).
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -105,8 +104,6 @@ struct Xrank {
     unsigned long long* d_box[2] = {nullptr, nullptr};
     unsigned long long* d_boxg = nullptr;
     hipEvent_t ev_box[2] = {nullptr, nullptr};
-    int* d_bq = nullptr;              // [nranks * cap[1]] bucket of each gathered i-node record
-    long long bq_len = 0;
     int* d_xctl = nullptr;            // [0] exchange overflow bits of the current call (1 del, 2 bins, 4 events);
                                       // [4 ..] the step's gathered counts [kNx][nranks], then their
                                       // maxima since the last overflow growth [kNx][nranks]
@@ -124,13 +121,13 @@ struct Xrank {
 
 // A hash-bucket entry: the i-node's cell, node id and position (coord + u of this step, the value
 // the triangle test would gather: the same expression, so the same bits), written by the binning
-// and moved into the bucket list by the fill, so the triangle search reads one 64-B record per
-// entry and has no dependent gather of the node's position behind it.
+// straight into the bucket list, so the triangle search reads one 64-B record per entry and has no
+// dependent gather of the node's position behind it. next: the bucket's next entry (-1 = end).
 struct alignas(16) BEnt {
     long long m[3];
     int node, pad;
     double p[3];
-    double pad2;
+    long long next;
 };
 static_assert(sizeof(BEnt) == 64, "BEnt: four 16-B vectors");
 
@@ -187,11 +184,12 @@ struct Contact {
                      // 6 bounds, so fewer, longer blocks: ~4 entries per thread, one unrolled pass)
     // hash grid over i-nodes
     int htot = 0;
-    int *d_bcnt = nullptr, *d_boff = nullptr, *d_qbucket = nullptr;
+    // bucket heads: (search sequence << 32 | first entry); a head of an older sequence is an empty
+    // bucket, so the table is never cleared (chained buckets: no count, scan or fill pass)
+    unsigned long long* d_head = nullptr;  // [htot]
     BEnt* d_blist = nullptr;        // [blist_cap] bucket lists
     BVel* d_bvel = nullptr;         // [blist_cap] beside them
     long long blist_cap = 0;
-    BRec* d_qrec = nullptr;  // [n_ni] by live-list position: the binned i-node (bin -> fill)
     unsigned long long* d_bbox = nullptr;  // [npairs][12] ordered-integer encoded doubles
     // small decks (set at setup; tuning "contact_fuse_small"): fused single-workgroup phases
     bool small = false;
@@ -215,8 +213,6 @@ struct Contact {
     long long cand_cap = 0, cshard_cap = 0;
     unsigned int* d_ccnt = nullptr; // [kCandShards * kShardStride] candidate count of each shard
     double* d_terms = nullptr;      // [4 cap][3]
-    void* d_tmp = nullptr;
-    size_t tmp_bytes = 0;
     // velocity before the first step (initial condition / uploaded), v2/HAKAI_j.jl:233-239
     double* d_velo0 = nullptr;
     bool use_velo0 = true;
@@ -301,7 +297,7 @@ __device__ __forceinline__ Range pair_range(const unsigned long long* bb_) {
 // incremental update (an element was deleted in the previous step), deleted elements found, and
 // the number of nodes with contact force in each of the two ping-pong "touched" lists.
 enum { kEv = 0, kEvMax = 1, kDirty = 2, kDel = 3, kNdel = 4, kTouched = 5 /* [5], [6] */, kNcand = 7, kTerms = 8,
-       kNcandMax = 9, kEvShardMax = 10, kCandShardMax = 11, kCandOver = 12, kCtl = 16 };
+       kNcandMax = 9, kEvShardMax = 10, kCandShardMax = 11, kCandOver = 12, kSeq = 13, kCtl = 16 };
 // Events are appended into kEvShards shards, each with its own counter on its own 128-B line: with
 // one counter, every wave that found an event waited on the same memory-side atomic (measured:
 // 0.13 ms of a 0.30 ms contact step on C4).
@@ -346,6 +342,7 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
         ctl[kCandOver] = 0;
         ctl[kTerms] = 0;
         ctl[kTouched + tsel] = 0;
+        ctl[kSeq] = ctl[kSeq] + 1u;  // this step's bucket-head stamp (never 0: the heads start at 0)
     }
     const int np = (int)ld_ctl(&ctl[kTouched + 1 - tsel]);
     for (int q = i; q < np; q += nb * blockDim.x) {
@@ -660,9 +657,6 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
     }
 }
 
-// cells of the live i-nodes inside the pair's range box (:2333-2346) -> hash bucket counts.
-// sb blocks per i-segment; qbucket[pos] = bucket or -1 (pos = position in ni_live)
-// vb = virtual block (segment vb / sb, part vb % sb); a launch of nseg * sb workgroups has one each
 // the hash record of live i-node nd (local id) of pair pr at position p inside the range box r
 __device__ __forceinline__ void bin_rec(const StepIn& s, const Range& r, const PairParam& pp, int pr, int nd,
                                         const double p[3], BRec& e) {
@@ -672,20 +666,35 @@ __device__ __forceinline__ void bin_rec(const StepIn& s, const Range& r, const P
     e.e.node = g;
     e.e.pad = pr;
     for (int d = 0; d < 3; ++d) e.e.p[d] = p[d];
-    e.e.pad2 = 0.0;
+    e.e.next = -1;
     velo(s, nd, e.w.v);
     e.w.mq = s.mass[g / 3];  // diag_M[i] with the node id i (:2592)
 }
 
+// entry `slot` of the bucket list into bucket b of search sequence seq: pushed onto the bucket's
+// chain (the order of a bucket's entries is the atomics' and irrelevant: every event's force is
+// summed order-independently)
+__device__ __forceinline__ void bucket_push(unsigned long long* head, int b, unsigned seq, int slot, BEnt e, BVel w,
+                                            BEnt* blist, BVel* bvel) {
+    const unsigned long long old = atomicExch(&head[b], ((unsigned long long)seq << 32) | (unsigned)slot);
+    e.next = (unsigned)(old >> 32) == seq ? (long long)(unsigned)old : -1LL;
+    blist[slot] = e;
+    bvel[slot] = w;
+}
+
+// cells of the live i-nodes inside the pair's range box (:2333-2346) -> the hash grid, each binned
+// node at its live-list position in the bucket list. vb = virtual block (segment vb / sb, part
+// vb % sb); a launch of nseg * sb workgroups has one each.
 __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* segs, const int* reg, const int* ni_live,
                                          const int* ni_pair, const int* ni_node, const PairParam* par,
-                                         const unsigned long long* bbox, int* qbucket, BRec* qrec, int* bcnt,
-                                         int sb) {
+                                         const unsigned long long* bbox, const unsigned int* ctl,
+                                         unsigned long long* head, BEnt* blist, BVel* bvel, int sb) {
 #pragma clang fp contract(off)
     const Seg sg = segs[vb / sb];
     if (sg.side != 0) return;
     const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
     const int bd = (int)blockDim.x;
+    const unsigned seq = ctl[kSeq];
     for (int q = (vb % sb) * bd + (int)threadIdx.x; q < n; q += sb * bd) {
         const int k = ni_live[base + q];
         const int pr = ni_pair[k];
@@ -695,84 +704,20 @@ __device__ __forceinline__ void bin_body(int vb, const StepIn& s, const Seg* seg
         double p[3];
         pos(s, nd, p);
         if (r.empty || p[0] < r.mn[0] || p[1] < r.mn[1] || p[2] < r.mn[2] || p[0] > r.mx[0] || p[1] > r.mx[1] ||
-            p[2] > r.mx[2]) {  // the candidate test of :2514-2519, applied before binning
-            qbucket[base + q] = -1;
+            p[2] > r.mx[2])  // the candidate test of :2514-2519, applied before binning
             continue;
-        }
         BRec e;
         bin_rec(s, r, pp, pr, nd, p, e);
-        qrec[base + q] = e;  // coalesced by live position; the fill moves it into the bucket list
         const int b = pp.hash_off + (int)(hash3(e.e.m[0], e.e.m[1], e.e.m[2]) & (unsigned)(pp.hash_size - 1));
-        qbucket[base + q] = b;
-        atomicAdd(&bcnt[b], 1);
+        bucket_push(head, b, seq, base + q, e.e, e.w, blist, bvel);  // coalesced by live position
     }
 }
 
 __global__ __launch_bounds__(kB) void k_ct_bin(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                const int* ni_pair, const int* ni_node, const PairParam* par,
-                                               const unsigned long long* bbox, int* qbucket, BRec* qrec,
-                                               int* bcnt, int sb) {
-    bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
-}
-
-// Exclusive scan of the bucket counts for small bucket tables (n <= kSmallScan): one block of
-// 1024 threads, each scanning a contiguous run. It replaces the two-kernel device-wide scan, whose
-// launches dominate the contact step of small decks ("Launch-bound step loops").
-constexpr int kSmallScan = 32768;
-__device__ __forceinline__ void scan_small_body(const int* in, int* out, int n) {
-    __shared__ int s_w[16];
-    // each thread scans a run of `per` entries (a multiple of 4, so the run is whole 16-B vectors:
-    // a quarter of the load/store instructions of an element-wise loop)
-    const int per = (((n + (int)blockDim.x - 1) / (int)blockDim.x) + 3) & ~3;
-    const int a = (int)threadIdx.x * per, b = min(n, a + per);
-    const int bv = a + ((max(b - a, 0)) & ~3);  // end of the whole vectors
-    int sum = 0;
-    for (int i = a; i < bv; i += 4) {
-        const int4 v = *reinterpret_cast<const int4*>(in + i);
-        sum += v.x + v.y + v.z + v.w;
-    }
-    for (int i = bv; i < b; ++i) sum += in[i];
-    int total;
-    int run = block_excl_scan(sum, s_w, total);
-    for (int i = a; i < bv; i += 4) {
-        const int4 v = *reinterpret_cast<const int4*>(in + i);
-        int4 o;
-        o.x = run;
-        o.y = o.x + v.x;
-        o.z = o.y + v.y;
-        o.w = o.z + v.z;
-        run = o.w + v.w;
-        *reinterpret_cast<int4*>(out + i) = o;
-    }
-    for (int i = bv; i < b; ++i) {
-        const int v = in[i];
-        out[i] = run;
-        run += v;
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_ct_scan_small(const int* in, int* out, int n) { scan_small_body(in, out, n); }
-
-__device__ __forceinline__ void fill_body(int vb, const Seg* segs, const int* reg, const int* ni_live,
-                                          const int* qbucket, const int* boff, int* bcnt, BEnt* blist, BVel* bvel,
-                                          int sb, const BRec* qrec) {
-    const Seg sg = segs[vb / sb];
-    if (sg.side != 0) return;
-    const int base = reg[2 * sg.region], n = reg[2 * sg.region + 1];
-    const int bd = (int)blockDim.x;
-    for (int q = (vb % sb) * bd + (int)threadIdx.x; q < n; q += sb * bd) {
-        const int b = qbucket[base + q];
-        if (b < 0) continue;
-        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-        blist[slot] = qrec[base + q].e;
-        bvel[slot] = qrec[base + q].w;
-    }
-}
-
-__global__ __launch_bounds__(kB) void k_ct_fill(const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* qbucket, const int* boff, int* bcnt, BEnt* blist,
-                                                BVel* bvel, int sb, const BRec* qrec) {
-    fill_body(blockIdx.x, segs, reg, ni_live, qbucket, boff, bcnt, blist, bvel, sb, qrec);
+                                               const unsigned long long* bbox, const unsigned int* ctl,
+                                               unsigned long long* head, BEnt* blist, BVel* bvel, int sb) {
+    bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, ctl, head, blist, bvel, sb);
 }
 
 // wave-aggregated append: one atomic per wave; every lane of the wave must call it
@@ -1003,20 +948,21 @@ __device__ __forceinline__ BEnt ld_bent(const BEnt* e) {
     r.p[0] = __longlong_as_double(ll2(w2.x, w2.y));
     r.p[1] = __longlong_as_double(ll2(w2.z, w2.w));
     r.p[2] = __longlong_as_double(ll2(w3.x, w3.y));
-    r.pad2 = __longlong_as_double(ll2(w3.z, w3.w));
+    r.next = ll2(w3.z, w3.w);
     return r;
 }
 
 // one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
 // i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
-                                         int b, int part, int stride, const PairParam* par, const int* boff,
+                                         int b, unsigned seq, const PairParam* par, const unsigned long long* head,
                                          const BEnt* __restrict__ blist, const BVel* __restrict__ bvel, double d_lim,
                                          double myu, unsigned int* evn, long long cap, int* ev_nodes, double* ev_f,
                                          EvBuf& eb) {
 #pragma clang fp contract(off)
     const int pr = rec->pr;
-    const int sl0 = boff[b], sl1 = boff[b + 1];
+    const unsigned long long h = head[b];
+    const int first = (unsigned)(h >> 32) == seq ? (int)(unsigned)h : -1;  // an older stamp: empty
     // self contact: the triangle's element's own nodes are skipped (:2496-2507); loaded once
     const bool self = rec->self;
     int own8[8];
@@ -1031,8 +977,10 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
     double im[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) im[k] = rec->im[k];
-    for (int sl = sl0 + part; sl < sl1; sl += stride) {
+    int nxt = -1;
+    for (int sl = first; sl >= 0; sl = nxt) {
         const BEnt be = ld_bent(blist + sl);
+        nxt = (int)be.next;
         const int i = be.node;
         // branch-free cell and self tests: no load waits behind a branch
         bool skip = ((int)(llabs(mj[0] - be.m[0]) > 1) | (int)(llabs(mj[1] - be.m[1]) > 1) |
@@ -1116,9 +1064,9 @@ __device__ __forceinline__ void ev_flush(const EvBuf& eb, int lane, unsigned int
 // 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
 __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
                                                 const TriRec* cand, long long cshard_cap,
-                                                const PairParam* par, const int* boff, const BEnt* blist,
-                                                const BVel* bvel, double d_lim, double myu, unsigned int* evs,
-                                                long long shard_cap, int* ev_nodes, double* ev_f) {
+                                                const PairParam* par, const unsigned long long* head,
+                                                const BEnt* blist, const BVel* bvel, double d_lim, double myu,
+                                                unsigned int* evs, long long shard_cap, int* ev_nodes, double* ev_f) {
     __shared__ unsigned s_cpre[kCandShards + 4];
     const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
@@ -1128,6 +1076,7 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
         ctl[kCandOver] = s_cpre[kCandShards + 1];
     }
     const int lane = (int)(threadIdx.x & 63);
+    const unsigned seq = ctl[kSeq];
     const int shard = (int)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kEvShards);
     unsigned int* evn = evs + shard * kShardStride;
     int* sh_nodes = ev_nodes + 4 * (long long)shard * shard_cap;
@@ -1163,7 +1112,7 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
             dup |= c2 < cell && (half ? hi : lo) == hb;
         }
         if (valid && !dup)
-            tri_cell(s, rec, mj, hoff + (int)hb, 0, 1, par, boff, blist, bvel, d_lim, myu, evn, shard_cap, sh_nodes,
+            tri_cell(s, rec, mj, hoff + (int)hb, seq, par, head, blist, bvel, d_lim, myu, evn, shard_cap, sh_nodes,
                      sh_f, eb);
         ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
@@ -1349,13 +1298,14 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl,
 // only the pair boxes
 __global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                      const int* ni_pair, const int* ni_node, const PairParam* par,
-                                                     const unsigned long long* bbox, int* qbucket, BRec* qrec,
-                                                     int* bcnt, int sb, int nbin, const int* tri_cnt,
+                                                     const unsigned long long* bbox, const unsigned int* ctl,
+                                                     unsigned long long* head, BEnt* blist, BVel* bvel,
+                                                     int sb, int nbin, const int* tri_cnt,
                                                      const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                      const int* tri_ele, unsigned int* ccnt, TriRec* cand,
                                                      long long cshard_cap) {
     if ((int)blockIdx.x < nbin)
-        bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, qbucket, qrec, bcnt, sb);
+        bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, ctl, head, blist, bvel, sb);
     else
         tri_filter_body(blockIdx.x - nbin, gridDim.x - nbin, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par,
                         bbox, ccnt, cand, cshard_cap);
@@ -1689,35 +1639,24 @@ __global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, int ns
     }
 }
 
-// A3: bucket of every gathered record (ranks in order) and the bucket counts; xctl bit 2 and the
-// poison when a rank binned more than its block holds
-__global__ void k_xr_bcount(XBlk xb, int nr, long long cap, const PairParam* par, int* bq, int* bcnt, int* poison,
-                            int pstep, int* xctl, int* hc) {
+// A3: every gathered record (rank q's record k at slot q * cap + k of the bucket list) pushed onto
+// its bucket's chain; xctl bit 2 and the poison when a rank binned more than its block holds
+__global__ void k_xr_insert(XBlk xb, int nr, long long cap, const PairParam* par, const unsigned int* ctl,
+                            unsigned long long* head, BEnt* blist, BVel* bvel, int* poison, int pstep, int* xctl,
+                            int* hc) {
     __shared__ int4 s_h[kMaxXRanks];
     load_hdrs(xb, nr, s_h);
     x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 2);
     x_counts(s_h, nr, 1, xctl, hc);
     const int q = (int)blockIdx.y;
     const long long n = min((long long)s_h[q].x, cap);
+    const unsigned seq = ctl[kSeq];
     const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
-        const BEnt& e = rec[k].e;
+        const BEnt e = rec[k].e;
         const PairParam& pp = par[e.pad];
         const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
-        bq[q * cap + k] = b;
-        atomicAdd(&bcnt[b], 1);
-    }
-}
-
-__global__ void k_xr_fill(XBlk xb, long long cap, const int* bq, const int* boff, int* bcnt, BEnt* blist, BVel* bvel) {
-    const int q = (int)blockIdx.y;
-    const long long n = min((long long)xhdr(xb.p[q], 0), cap);
-    const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
-    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
-        const int b = bq[q * cap + k];
-        const int slot = boff[b] + atomicSub(&bcnt[b], 1) - 1;  // leaves bcnt zeroed for the next step
-        blist[slot] = rec[k].e;
-        bvel[slot] = rec[k].w;
+        bucket_push(head, b, seq, (int)(q * cap + k), e, rec[k].w, blist, bvel);
     }
 }
 
@@ -1873,11 +1812,10 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_el_tri_ptr); dfree(C->d_el_tri); dfree(C->d_el_ni_ptr); dfree(C->d_el_ni); dfree(C->d_el_nj_ptr);
     dfree(C->d_el_nj); dfree(C->d_dlist);
     dfree(C->d_ni_live); dfree(C->d_nj_live); dfree(C->d_tri_live);
-    dfree(C->d_bcnt); dfree(C->d_boff); dfree(C->d_blist); dfree(C->d_bvel); dfree(C->d_qbucket); dfree(C->d_qrec);
+    dfree(C->d_head); dfree(C->d_blist); dfree(C->d_bvel);
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt);
-    if (C->d_tmp) (void)hipFree(C->d_tmp);
     if (Xrank* X = C->xr) {
         (void)hipDeviceSynchronize();  // in-process peers may still read this rank's blocks
         dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->d_last_del);
@@ -1888,7 +1826,7 @@ void contact_destroy(hakai_ctx* c) {
             for (auto& e : X->ev_sent[x])
                 if (e) (void)hipEventDestroy(e);
         }
-        dfree(X->d_box[0]); dfree(X->d_box[1]); dfree(X->d_boxg); dfree(X->d_bq); dfree(X->d_xctl);
+        dfree(X->d_box[0]); dfree(X->d_box[1]); dfree(X->d_boxg); dfree(X->d_xctl);
         for (auto& e : X->ev_box)
             if (e) (void)hipEventDestroy(e);
         for (auto& e : X->ev_cnt)
@@ -1921,7 +1859,7 @@ static int xr_buffers(hakai_ctx* c) {
     bool sync = false;
     for (int x = 0; x < Xrank::kNx; ++x)
         sync |= X->send_bytes[x] < xr_alloc_blk(X, x) || (comm_is_rccl(c) && X->recv_bytes[x] < (size_t)X->nranks * xr_alloc_blk(X, x));
-    sync |= X->bq_len < (long long)X->nranks * X->cap[1] || C->blist_cap < (long long)X->nranks * X->cap[1];
+    sync |= C->blist_cap < (long long)X->nranks * X->cap[1];
     if (!sync) return 0;
     HIPCHK(hipDeviceSynchronize());  // (in-process peers read the send blocks)
     for (int x = 0; x < Xrank::kNx; ++x) {
@@ -1941,11 +1879,6 @@ static int xr_buffers(hakai_ctx* c) {
         }
     }
     const long long nb = (long long)X->nranks * X->cap[1];
-    if (X->bq_len < nb) {
-        dfree(X->d_bq);
-        HIPCHK(dalloc(&X->d_bq, (size_t)nb));
-        X->bq_len = nb;
-    }
     if (C->blist_cap < nb) {
         dfree(C->d_blist);
         dfree(C->d_bvel);
@@ -2049,7 +1982,6 @@ int contact_post_step(hakai_ctx* c) {
 }
 
 static int search(hakai_ctx* c, const StepIn& in, bool fused);
-static int bucket_scan(hakai_ctx* c);
 static void tri_search(hakai_ctx* c, const StepIn& in);
 
 static StepIn step_in(hakai_ctx* c, double t, double d_time) {
@@ -2172,23 +2104,16 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
         if (fused_mid) {
             const int nbin = C->nseg * C->g_seg;
             hipLaunchKernelGGL(k_ct_binfilter, dim3((unsigned)nbin + gfilt), dim3(kB), 0, s, in, sg, C->d_reg,
-                               C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_qrec,
-                               C->d_bcnt, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
+                               C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head,
+                               C->d_blist, C->d_bvel, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
                                C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_ccnt, (TriRec*)C->d_cand,
                                C->cshard_cap);
         } else {
             hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
-                               C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_qbucket, C->d_qrec, C->d_bcnt,
-                               C->g_seg);
+                               C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head, C->d_blist,
+                               C->d_bvel, C->g_seg);
         }
     }
-    // the bucket scan and the fill: one workgroup for tables up to kSmallScan, then a workgroup per
-    // segment part (fusing the fill into the scan's one workgroup was slower on every reference deck:
-    // the fill's scattered atomics and stores want more than one CU)
-    if (int rc = bucket_scan(c)) return rc;
-    if (C->nseg > 0)
-        hipLaunchKernelGGL(k_ct_fill, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, sg, C->d_reg, C->d_ni_live,
-                           C->d_qbucket, C->d_boff, C->d_bcnt, C->d_blist, C->d_bvel, C->g_seg, C->d_qrec);
     if (C->n_tri > 0) {
         if (!fused_mid)
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
@@ -2218,21 +2143,10 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
     return 0;
 }
 
-static int bucket_scan(hakai_ctx* c) {
-    Contact* C = c->contact;
-    if (C->htot + 1 <= kSmallScan) {
-        hipLaunchKernelGGL(k_ct_scan_small, dim3(1), dim3(1024), 0, c->stream, C->d_bcnt, C->d_boff, (int)(C->htot + 1));
-    } else {
-        size_t tb = C->tmp_bytes;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(C->d_tmp, tb, C->d_bcnt, C->d_boff, C->htot + 1, c->stream));
-    }
-    return 0;
-}
-
 static void tri_search(hakai_ctx* c, const StepIn& in) {
     Contact* C = c->contact;
     hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, c->stream, in, C->d_ctl, C->d_ccnt,
-                       (const TriRec*)C->d_cand, C->cshard_cap, C->d_par, C->d_boff, C->d_blist, C->d_bvel, C->d_lim,
+                       (const TriRec*)C->d_cand, C->cshard_cap, C->d_par, C->d_head, C->d_blist, C->d_bvel, C->d_lim,
                        C->myu, C->d_evs, C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
 }
 
@@ -2290,12 +2204,9 @@ static int xr_a3(hakai_ctx* c, double d_time) {
     XBlk xb;
     if (int rc = xr_gather(c, 1, par, xr_blk(X, 1), xb)) return rc;
     const unsigned gb = (unsigned)std::min<long long>(std::max<long long>((X->cap[1] + kB - 1) / kB, 1), 128);
-    hipLaunchKernelGGL(k_xr_bcount, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks, X->cap[1], C->d_par,
-                       X->d_bq, C->d_bcnt, c->d_poison, X->t_a, X->d_xctl,
+    hipLaunchKernelGGL(k_xr_insert, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks, X->cap[1], C->d_par,
+                       C->d_ctl, C->d_head, C->d_blist, C->d_bvel, c->d_poison, X->t_a, X->d_xctl,
                        X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks);
-    if (int rc = bucket_scan(c)) return rc;
-    hipLaunchKernelGGL(k_xr_fill, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->cap[1], X->d_bq, C->d_boff,
-                       C->d_bcnt, C->d_blist, C->d_bvel);
     StepIn in = step_in(c, X->t_a, d_time);
     if (C->n_tri > 0) {
         const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
@@ -2801,7 +2712,7 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         }
     // fused small-deck phases: one 1024-thread workgroup scans the deletion steps, the bucket table
     // and the i-node entries a few times at most
-    C->small = C->nE <= (1 << 16) && C->n_ni <= (1 << 16) && C->htot + 1 <= kSmallScan;
+    C->small = C->nE <= (1 << 16) && C->n_ni <= (1 << 16) && C->htot <= (1 << 15);
     {  // event buffer: 8 events per initial contact point (overflow is detected and reported)
         long long ci0 = 0;
         for (int p = 0; p < C->npairs; ++p) ci0 += C->pair_counts[3 * p];
@@ -2903,13 +2814,11 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         hkc::contact_destroy(c);
         return rc;
     }
-    HIPCHK(dalloc(&C->d_bcnt, (size_t)C->htot + 1));
-    HIPCHK(dalloc(&C->d_boff, (size_t)C->htot + 1));
+    HIPCHK(dalloc(&C->d_head, (size_t)C->htot));
+    HIPCHK(hipMemsetAsync(C->d_head, 0, (size_t)C->htot * sizeof(unsigned long long), s));  // stamp 0: empty
     C->blist_cap = std::max(C->n_ni, 1);  // (multi-GPU: sized for every rank's records, xr_buffers)
     HIPCHK(dalloc(&C->d_blist, (size_t)C->blist_cap));
     HIPCHK(dalloc(&C->d_bvel, (size_t)C->blist_cap));
-    HIPCHK(dalloc(&C->d_qbucket, (size_t)C->n_ni));
-    HIPCHK(dalloc(&C->d_qrec, (size_t)C->n_ni));
     HIPCHK(dalloc(&C->d_tile_cnt, (size_t)C->ntile));
     HIPCHK(dalloc(&C->d_tile_off, (size_t)C->ntile + 1));
     HIPCHK(dalloc(&C->d_dlist, (size_t)nE));
@@ -2938,7 +2847,6 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));
-    HIPCHK(hipMemsetAsync(C->d_bcnt, 0, ((size_t)C->htot + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_cnt, 0, ((size_t)H.nN + 1) * sizeof(int), s));
     HIPCHK(hipMemsetAsync(C->d_ctl, 0, kCtl * sizeof(unsigned int), s));
     HIPCHK(hipMemsetAsync(c->d_fext, 0, 3 * (size_t)c->nN * sizeof(double), s));
@@ -2949,10 +2857,6 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     else
         HIPCHK(hipMemsetAsync(C->d_velo0, 0, 3 * (size_t)c->nN * sizeof(double), s));
     C->use_velo0 = c->steps_done == 0 || !c->h_velo0.empty();
-    size_t t1 = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, C->d_bcnt, C->d_boff, C->htot + 1, s));
-    C->tmp_bytes = t1;
-    HIPCHK(hipMalloc(&C->d_tmp, std::max<size_t>(C->tmp_bytes, 1)));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
@@ -3195,7 +3099,7 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
         stats[7] = binned;
         if (cap > 8) stats[8] = bytes;
     }
-    if (cap > 9) stats[9] = C->htot;  // hash-grid buckets over all pairs (> kSmallScan: device-wide scan)
+    if (cap > 9) stats[9] = C->htot;  // hash-grid buckets over all pairs
     return 0;
 }
 

@@ -1338,6 +1338,18 @@ __global__ void k_set_step(double* slot, double t_prev) {
     if (threadIdx.x == 0) *slot = t_prev;
 }
 
+// Timing aid (hakai_step_group with group_serial 2): one wave sleeps a fixed number of s_sleep
+// rounds (no memory access, always exits), so the host can enqueue a whole phase behind it and the
+// phase then runs back to back instead of at the host's enqueue pace.
+__global__ void k_hold(int rounds) {
+    for (int i = 0; i < rounds; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_hold(int rounds, hipStream_t s) {
+    hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, s, rounds);
+    return hipGetLastError();
+}
+
 hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s) {
     hipLaunchKernelGGL(k_set_step, dim3(1), dim3(64), 0, s, slot, t_prev);
     return hipGetLastError();

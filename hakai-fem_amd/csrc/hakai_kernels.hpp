@@ -120,6 +120,7 @@ hipError_t launch_nodal(const NodalArgs& a, hipStream_t s);
 hipError_t launch_bc(const BCArgs& a, hipStream_t s);
 // graph mode: the step counter slot read by the first step of a captured graph
 hipError_t launch_set_step(double* slot, double t_prev, hipStream_t s);
+hipError_t launch_hold(int rounds, hipStream_t s);  // a fixed sleep on the stream (timing aid)
 
 // Q of every dof from fe (for downloads): Q[3n+c] = sum over incidences in element order.
 hipError_t launch_gather_q(const int* inc_ptr, const int* inc, const double* fe, double* Q, long long nN,

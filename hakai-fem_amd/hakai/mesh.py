@@ -30,10 +30,12 @@ def node_id(ix, iy, iz, nx, ny):
 
 
 def hex_bar(nx: int, ny: int, nz: int, h: float = 1.0, perturb: float = 0.0, seed: int = 0,
-            z0: float = 0.0) -> tuple[np.ndarray, np.ndarray]:
+            z0: float = 0.0, x_slabs: bool = False) -> tuple[np.ndarray, np.ndarray]:
     """Structured bar of nx*ny*nz unit hexes. Returns coordmat (nN,3), elementmat (nE,8) 1-based.
 
-    perturb: uniform random node displacement amplitude as a fraction of h (all three axes)."""
+    perturb: uniform random node displacement amplitude as a fraction of h (all three axes).
+    x_slabs: elements numbered z fastest and x slowest (nodes keep their numbering), so contiguous
+    element ranges are x-slabs instead of z-slabs."""
     xs = np.arange(nx + 1, dtype=np.float64) * h
     ys = np.arange(ny + 1, dtype=np.float64) * h
     zs = z0 + np.arange(nz + 1, dtype=np.float64) * h
@@ -42,7 +44,10 @@ def hex_bar(nx: int, ny: int, nz: int, h: float = 1.0, perturb: float = 0.0, see
     if perturb > 0:
         rng = np.random.default_rng(seed)
         coord += rng.uniform(-perturb * h, perturb * h, size=coord.shape)
-    iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    if x_slabs:
+        ix, iy, iz = np.meshgrid(np.arange(nx), np.arange(ny), np.arange(nz), indexing="ij")
+    else:
+        iz, iy, ix = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     ix, iy, iz = ix.ravel(), iy.ravel(), iz.ravel()
     n = lambda a, b, c: node_id(ix + a, iy + b, iz + c, nx, ny)  # noqa: E731
     elem = np.stack([n(0, 0, 0), n(1, 0, 0), n(1, 1, 0), n(0, 1, 0),
@@ -94,16 +99,19 @@ def config_c5(layers: int = 1600, n: int = 100) -> Model:
 
 def two_body_model(plate=(8, 8, 2), impactor=(4, 4, 4), gap=0.1, v=-1e5, material: Material | None = None,
                    perturb=0.0, seed=0, d_time=1e-7, n_steps=1000, contact_flag=1, myu=None, surfaces=False,
-                   name="two_body") -> Model:
+                   name="two_body", x_slabs=False) -> Model:
     """Two instances: a plate (instance 1) clamped on its bottom face and an impactor block
     (instance 2) above it, centred in x/y, `gap` mm away, with initial velocity v along z.
     All-exterior contact (*Contact, no *Contact Pair). myu overrides the reference's friction 0.25
-    (BASELINE C4 runs frictionless: myu=0)."""
+    (BASELINE C4 runs frictionless: myu=0). x_slabs: elements of each body numbered x slowest, so
+    range partitions cut both bodies into x-slabs and spread the contact zone over the ranks."""
     mat = material or steel_ductile()
     px, py, pz = plate
     ix, iy, iz = impactor
-    c1, e1 = hex_bar(px, py, pz, perturb=perturb, seed=seed)
-    c2, e2 = hex_bar(ix, iy, iz, perturb=perturb, seed=seed + 1, z0=pz + gap)
+    if surfaces and x_slabs:
+        raise ValueError("two_body_model: surfaces assume the z-slab element numbering")
+    c1, e1 = hex_bar(px, py, pz, perturb=perturb, seed=seed, x_slabs=x_slabs)
+    c2, e2 = hex_bar(ix, iy, iz, perturb=perturb, seed=seed + 1, z0=pz + gap, x_slabs=x_slabs)
     c2[:, 0] += (px - ix) / 2.0
     c2[:, 1] += (py - iy) / 2.0
     n1 = c1.shape[0]
@@ -123,12 +131,14 @@ def two_body_model(plate=(8, 8, 2), impactor=(4, 4, 4), gap=0.1, v=-1e5, materia
                  contact_params=params, contact_pairs=cps)
 
 
-def config_c4(scale: int = 1) -> Model:
+def config_c4(scale: int = 1, x_slabs: bool = False) -> Model:
     """C4: plate 200x200x50 + impactor 100x100x200 (2 M hex each), gap 0.1 mm, impactor
     v = -1e5 mm/s, elastoplastic steel, all-exterior contact, frictionless (myu = 0).
-    scale > 1 divides every edge count (tests)."""
+    scale > 1 divides every edge count (tests). x_slabs: the same model with its elements numbered
+    x slowest (range partitions then cut x-slabs, each holding part of the contact zone)."""
     return two_body_model((200 // scale, 200 // scale, 50 // scale), (100 // scale, 100 // scale, 200 // scale),
-                          gap=0.1, v=-1e5, myu=0.0, name="C4")
+                          gap=0.1, v=-1e5, myu=0.0, name="C4" + (" (x-slab numbering)" if x_slabs else ""),
+                          x_slabs=x_slabs)
 
 
 def tensile5e_model() -> Model:

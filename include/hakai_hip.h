@@ -195,7 +195,9 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       on their own; call on every rank between steps);
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
- *                       next rank's (uncontended per-rank timings on one GPU; default 0). */
+ *                       next rank's (uncontended per-rank timings on one GPU; default 0); 2: the
+ *                       same, each phase enqueued behind a fixed ≈0.3 ms sleep kernel so it runs
+ *                       back to back on the GPU instead of at the host's enqueue pace. */
 int hakai_set_tuning(hakai_ctx* ctx, const char* key, int64_t value);
 
 /* ---- contact: all-exterior instance-vs-instance penalty contact --------- */

@@ -114,6 +114,26 @@ def _assert_group_equals_single(glob, parts, g, gdel):
         assert np.array_equal(st.element_flag, g.element_flag[e0:e0 + el])
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_contact_group_x_slabs_bitexact(world):
+    """The same with the elements numbered x slowest (mesh x_slabs), so the rank ranges are
+    x-slabs and every rank holds part of both contact surfaces (the z-slab ranges above put each
+    surface on one rank): bit-identical to one context, and the candidate triangles spread over
+    the ranks."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(8, 8, 2), impactor=(4, 4, 3), v=-3e5, d_time=2e-8, n_steps=400, x_slabs=True)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+        gst = sv.contact_stats()
+    parts = _run_contact_group(glob, world, glob.n_steps, key=350 + world)
+    _assert_group_equals_single(glob, parts, g, gdel)
+    sts = [st for *_, st in parts]
+    assert sum(st["candidate_triangles"] for st in sts) == gst["candidate_triangles"]
+    assert sum(1 for st in sts if st["live_triangles"] > 0) == world  # every rank holds surface
+
+
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_contact_group_bitexact_with_deletion(world):
     """Multi-GPU contact: contact-driven deletion with the surface update, the

@@ -24,9 +24,14 @@ def main():
                     help=">1: range-partitioned in-process group on this one GPU (multi-GPU contact, "
                          "owner-computed search; measures the per-rank contact cost incl. the exchanges, not scaling)")
     ap.add_argument("--serial", type=int, default=1,
-                    help="multi-rank: drain each rank's phase before the next rank's (tuning group_serial), so "
-                         "the per-rank kernel timings are not inflated by the ranks sharing this one GPU")
+                    help="multi-rank (tuning group_serial): 1 drains each rank's phase before the next rank's, so "
+                         "the per-rank timings are not inflated by the ranks sharing this one GPU; 2 also "
+                         "enqueues each phase behind a fixed sleep kernel, so it runs back to back as in a "
+                         "pipelined run instead of at the host's enqueue pace")
     ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_exchange_bins=4096")
+    ap.add_argument("--x-slabs", type=int, default=0,
+                    help="1: C4 with its elements numbered x slowest, so the rank ranges are x-slabs that "
+                         "share the contact zone (the default z-slab ranges put it on two ranks)")
     a = ap.parse_args()
     a.tuning = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in a.tuning.split(",") if kv]
     if a.ranks > 1:
@@ -36,7 +41,7 @@ def main():
     from hakai._abi import K_BC, K_CONTACT, K_ELEMENT, K_NODAL
     from hakai.solver import Solver
     t0 = time.time()
-    m = mesh.config_c4(a.scale)
+    m = mesh.config_c4(a.scale, x_slabs=bool(a.x_slabs))
     t1 = time.time()
     sv = Solver(m)
     for k, v in a.tuning:
@@ -60,7 +65,7 @@ def main():
     st = sv.download(element_flag=True)
     n_active = int(st.element_flag.sum())
     out = {
-        "workload": f"C4 two-body impact, scale 1/{a.scale}", "tuning": dict(a.tuning),
+        "workload": f"{m.name} two-body impact, scale 1/{a.scale}", "tuning": dict(a.tuning),
         "elements": m.nElement, "nodes": m.nNode,
         "pairs": pairs, "element_size": sizes, "steps": a.steps, "preload": a.preload,
         "value_M_element_updates_per_s": round(n_active * a.steps / el / 1e6, 3),
@@ -82,7 +87,7 @@ def group(a):
     from hakai import dist, mesh
     from hakai._abi import K_BC, K_CONTACT, K_CONTACT_SUM, K_ELEMENT, K_EXCHANGE, K_NODAL
     from hakai.solver import Solver, step_group
-    m = mesh.config_c4(a.scale)
+    m = mesh.config_c4(a.scale, x_slabs=bool(a.x_slabs))
     gdiag, _ = m.lumped_mass()
     parts = [dist.range_partition(m, r, a.ranks, gdiag) for r in range(a.ranks)]
     svs = []
@@ -117,7 +122,7 @@ def group(a):
         ranks.append({"elements": loc.nElement, "nodes": loc.nNode, "kernel_ms_per_step": per,
                       "contact_total_ms_per_step": round(per.get("contact", 0) + per.get("contact_sum", 0), 4),
                       "contact_stats_last_step": sv.contact_stats()})
-    out = {"workload": f"C4 two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group), "
+    out = {"workload": f"{m.name} two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group), "
                        f"owner-computed search, group_serial={a.serial}",
            "elements": m.nElement, "steps": a.steps, "preload": a.preload,
            "group_ms_per_step_all_ranks": round(el / a.steps * 1e3, 4), "setup_s": round(t1 - t0, 2),

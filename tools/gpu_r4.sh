@@ -11,6 +11,7 @@
 #   prof       rocprofv3 kernel trace of a short bench     -> gpurun_out/r4_prof/
 #   drift      fused-kernel drift on the reference decks  -> gpurun_out/r4_deck_drift.jsonl
 #   c4ranks    C4 contact per rank: one context, 2 and 4 in-process ranks -> gpurun_out/r4_c4_ranks.jsonl
+#   c4xslab    the same with C4's elements numbered x slowest (rank ranges = x-slabs) -> gpurun_out/r4_c4_xslab.jsonl
 #   c4prof     rocprofv3 kernel trace of the C4 contact run, one context and 2 ranks -> gpurun_out/r4_c4prof_{1,2}/
 #   decks      reference decks end to end, both element modes, graphs -> gpurun_out/r4_decks.jsonl
 #   deckprof   rocprofv3 kernel trace of car-crash-N2k, 3200 steps, stream mode -> gpurun_out/r4_deckprof/
@@ -40,12 +41,17 @@ for st in "$@"; do
     drift) run 600 gpurun_out/r4_deck_drift.jsonl python tools/deck_drift.py || exit $? ;;
     c4ranks) : > gpurun_out/r4_c4_ranks.jsonl
         for r in 1 2 4; do
-            run 600 gpurun_out/r4_c4_ranks_$r.log python tools/bench_contact.py --ranks $r --steps 40 || exit $?
+            run 600 gpurun_out/r4_c4_ranks_$r.log python tools/bench_contact.py --ranks $r --steps 40 --serial ${C4SERIAL:-1} || exit $?
             grep '^{' gpurun_out/r4_c4_ranks_$r.log >> gpurun_out/r4_c4_ranks.jsonl
+        done ;;
+    c4xslab) : > gpurun_out/r4_c4_xslab.jsonl
+        for r in 1 2 4; do
+            run 600 gpurun_out/r4_c4_xslab_$r.log python tools/bench_contact.py --ranks $r --steps 40 --x-slabs 1 --serial ${C4SERIAL:-1} || exit $?
+            grep '^{' gpurun_out/r4_c4_xslab_$r.log >> gpurun_out/r4_c4_xslab.jsonl
         done ;;
     c4prof) for r in ${C4PROF_RANKS:-1 2}; do
             run 600 gpurun_out/r4_c4prof_$r.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_c4prof_$r -o c4 \
-                -- python tools/bench_contact.py --ranks $r --steps 40 || exit $?
+                -- python tools/bench_contact.py --ranks $r --steps 40 --x-slabs ${C4PROF_XSLAB:-0} || exit $?
         done ;;
     decks) run 900 gpurun_out/r4_decks.jsonl python tools/deck_bench.py --cpu-steps 0 || exit $? ;;
     deckprof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_deckprof.log rocprofv3 --kernel-trace --stats \
