@@ -211,7 +211,10 @@ struct Contact {
     void* d_cand = nullptr;         // [cand_cap] TriRec of the triangles passing the prefilter, in
                                     // kCandShards shards of cshard_cap records
     long long cand_cap = 0, cshard_cap = 0;
-    unsigned int* d_ccnt = nullptr; // [kCandShards * kShardStride] candidate count of each shard
+    unsigned int* d_ccnt = nullptr; // [kCandShards * kShardStride] candidate count of each shard (word
+                                    // 0) and item count (word kItemWord)
+    uint2* d_item = nullptr;        // [kCandShards][kItemsPerCand * cshard_cap] (candidate slot, cell << 27 |
+                                    // bucket): the cells of a candidate's neighbourhood that its sphere reaches
     double* d_terms = nullptr;      // [4 cap][3]
     // velocity before the first step (initial condition / uploaded), v2/HAKAI_j.jl:233-239
     double* d_velo0 = nullptr;
@@ -306,6 +309,8 @@ constexpr int kShardStride = 32;  // unsigned ints between shard counters
 // Candidate triangles likewise: prefilter block b appends to shard b % kCandShards (one atomic per
 // block on that shard's counter; clustered candidates fall in consecutive blocks, so shards stay even).
 constexpr int kCandShards = 64;
+constexpr int kItemWord = 16;      // a shard's item counter, in its own half of the counter line
+constexpr int kItemsPerCand = 16;  // item capacity per candidate slot (a candidate has <= 27)
 constexpr int kFilterBlocks = 2048;  // prefilter grid cap
 
 // Step prologue: pair boxes to (+inf, -inf), event counter to 0, full rebuild if the host forces
@@ -330,7 +335,7 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
     const int i = bid * blockDim.x + threadIdx.x;
     if (zero_hdr && i < 2) zero_hdr[i] = 0;  // multi-GPU: this step's bin block (count, overflow)
     if (i < kEvShards) evs[i * kShardStride] = 0;
-    if (i < kCandShards) ccnt[i * kShardStride] = 0;
+    if (i < kCandShards) ccnt[i * kShardStride] = ccnt[i * kShardStride + kItemWord] = 0;
     for (int q = i; q < 12 * npairs; q += nb * blockDim.x)
         bbox[q] = ((q % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;  // min slots +inf, max slots -inf
     if (i == 0) {
@@ -557,9 +562,10 @@ struct AppendIn {
 
 // incremental update, part 2: one block per deleted element, one thread per entry its deletion
 // exposes (triangles, then i-node entries, then j-node entries)
+// (lanes lt of lsz per deleted element: a workgroup, or a wave of the one-workgroup k_xr_front)
 __device__ __forceinline__ void append_body(int bid, int nb, unsigned int* ctl, const int* dlist, const AppendIn& A,
                                             const int* del_step, int t, const double* t_rd, int* reg, int* ni_live,
-                                            int* nj_live, int* tri_live) {
+                                            int* nj_live, int* tri_live, int lt, int lsz) {
     if (ld_ctl(&ctl[kDel]) == 0) return;
     if (t_rd) t = (int)*t_rd + 1;
     const int nd = (int)ld_ctl(&ctl[kNdel]);
@@ -568,7 +574,7 @@ __device__ __forceinline__ void append_body(int bid, int nb, unsigned int* ctl, 
         const int t0 = A.el_tri_ptr[e], nt = A.el_tri_ptr[e + 1] - t0;
         const int i0 = A.el_ni_ptr[e], ni = A.el_ni_ptr[e + 1] - i0;
         const int j0 = A.el_nj_ptr[e], nj = A.el_nj_ptr[e + 1] - j0;
-        for (int x = threadIdx.x; x < nt + ni + nj; x += blockDim.x) {
+        for (int x = lt; x < nt + ni + nj; x += lsz) {
             if (x < nt) {  // unique adder per triangle
                 tri_live[atomicAdd(&reg[2 * A.tri_reg + 1], 1)] = A.el_tri[t0 + x];
             } else if (x < nt + ni) {
@@ -588,7 +594,8 @@ __device__ __forceinline__ void append_body(int bid, int nb, unsigned int* ctl, 
 
 __global__ void k_ct_append(unsigned int* ctl, const int* dlist, AppendIn A, const int* del_step, int t,
                             const double* t_rd, int* reg, int* ni_live, int* nj_live, int* tri_live) {
-    append_body(blockIdx.x, gridDim.x, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live);
+    append_body(blockIdx.x, gridDim.x, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live,
+                (int)threadIdx.x, (int)blockDim.x);
 }
 
 // bounding boxes of the live node lists per pair (:2281-2299). Segment = the live node entries of
@@ -606,19 +613,21 @@ struct Seg {
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
-__global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
-                                                const int* nj_live, const int* ni_node, const int* nj_node,
-                                                unsigned long long* bbox, int sb) {
-    const Seg sg = segs[blockIdx.x / sb];
+// segment vb / sb, part vb % sb
+__device__ __forceinline__ void bbox_body(int vb, int sb, const StepIn& s, const Seg* segs, const int* reg,
+                                          const int* ni_live, const int* nj_live, const int* ni_node,
+                                          const int* nj_node, unsigned long long* bbox) {
+    const Seg sg = segs[vb / sb];
     if (sg.dup) return;  // another segment's blocks fill its boxes
-    const int sub = blockIdx.x % sb;
+    const int sub = vb % sb;
     const bool side_i = sg.side == 0;
     const int* node = side_i ? ni_node : nj_node;
     const int* lst = (side_i ? ni_live : nj_live) + reg[2 * sg.region];
     const int cnt = reg[2 * sg.region + 1];
+    const int bd = (int)blockDim.x;
     unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
 #pragma unroll 4
-    for (int q = sub * kB + (int)threadIdx.x; q < cnt; q += sb * kB) {  // iterations overlap their loads
+    for (int q = sub * bd + (int)threadIdx.x; q < cnt; q += sb * bd) {  // iterations overlap their loads
         double p[3];
         pos(s, node[lst[q]], p);
         for (int d = 0; d < 3; ++d) {
@@ -632,7 +641,7 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
             mn[d] = umin64(mn[d], __shfl_xor(mn[d], off));
             mx[d] = umax64(mx[d], __shfl_xor(mx[d], off));
         }
-    __shared__ unsigned long long red[kB / 64][6];
+    __shared__ unsigned long long red[16][6];
     const int w = threadIdx.x / 64;
     if ((threadIdx.x & 63) == 0)
         for (int d = 0; d < 3; ++d) {
@@ -643,7 +652,7 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
     if (threadIdx.x < 6) {
         const int q = threadIdx.x;
         unsigned long long v = red[0][q];
-        for (int ww = 1; ww < kB / 64; ++ww) v = q < 3 ? umin64(v, red[ww][q]) : umax64(v, red[ww][q]);
+        for (int ww = 1; ww < bd / 64; ++ww) v = q < 3 ? umin64(v, red[ww][q]) : umax64(v, red[ww][q]);
         for (int a = -1; a < 2; ++a) {  // own slot, then the duplicates'
             const int off = a < 0 ? 12 * sg.pair + (side_i ? 0 : 6) : sg.alias[a];
             if (off < 0) continue;
@@ -655,6 +664,12 @@ __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
+                                                const int* nj_live, const int* ni_node, const int* nj_node,
+                                                unsigned long long* bbox, int sb) {
+    bbox_body(blockIdx.x, sb, s, segs, reg, ni_live, nj_live, ni_node, nj_node, bbox);
 }
 
 // the hash record of live i-node nd (local id) of pair pr at position p inside the range box r
@@ -746,6 +761,26 @@ __device__ __forceinline__ unsigned block_append(unsigned int* ctr, bool pred, u
     if (threadIdx.x == 0) s_ctl[1] = s_ctl[0] ? atomicAdd(ctr, s_ctl[0]) : 0u;
     __syncthreads();
     return s_ctl[1] + off + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
+}
+
+// The same for a count per thread (every thread of the block calls it): the thread's first slot
+__device__ __forceinline__ unsigned block_append_n(unsigned int* ctr, unsigned cnt, unsigned* s_ctl) {
+    if (threadIdx.x == 0) s_ctl[0] = 0;
+    __syncthreads();
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned x = cnt;  // wave inclusive scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    unsigned woff = 0;
+    const unsigned wtot = __shfl(x, 63);
+    if (lane == 63 && wtot) woff = atomicAdd(&s_ctl[0], wtot);
+    woff = __shfl(woff, 63);
+    __syncthreads();
+    if (threadIdx.x == 0) s_ctl[1] = s_ctl[0] ? atomicAdd(ctr, s_ctl[0]) : 0u;
+    __syncthreads();
+    return s_ctl[1] + woff + x - cnt;
 }
 
 // Prefix of 64 shard counters (each clamped to the shard capacity) in LDS, one lane per shard of
@@ -856,14 +891,43 @@ __device__ __forceinline__ void tri_geom(int pr, const Range& r, const PairParam
     T.self = pp.self ? 1 : 0;
 }
 
+// Which cells dc (0..26: dx fastest, the reference's dz, dy, dx loops) of the 27 around the
+// candidate's first-node cell can hold an i-node within the candidate's sphere (|p - c| < Rmax,
+// :2532-2536)? A node lies in cell m when ceil((p - amn) / ddiv) == m (bin_rec), i.e. p in
+// (amn + (m-1) ddiv, amn + m ddiv] up to the rounding of that expression. Each box is widened by far
+// more than that rounding and the radius by a relative 1e-9, so a cell is dropped only if no node
+// in it can pass the sphere test: the search visits fewer cells and finds the same events. The
+// squared distance is separable, 3 per axis; NaN geometry keeps every cell. Returns a 27-bit mask.
+__device__ __forceinline__ unsigned reach_mask(const TriRec& T, const double amn[3], double ddiv) {
+    double t2[3][3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double m = (double)(T.mj[d] + (k - 1));
+            const double eps = 1e-9 * ddiv + 1e-12 * (fabs(amn[d]) + fabs(m) * ddiv);
+            const double lo = amn[d] + (m - 1.0) * ddiv - eps, hi = amn[d] + m * ddiv + eps;
+            const double t = fmax(fmax(lo - T.c[d], T.c[d] - hi), 0.0);
+            t2[d][k] = t * t;
+        }
+    const double r = T.Rmax * (1.0 + 1e-9) + 1e-9 * ddiv;
+    const double r2 = r * r * (1.0 + 1e-9);
+    unsigned mask = 0;
+#pragma unroll
+    for (int dc = 0; dc < 27; ++dc)
+        if (!(t2[0][dc % 3] + t2[1][(dc / 3) % 3] + t2[2][dc / 9] > r2)) mask |= 1u << dc;
+    return mask;
+}
+
 // triangle prefilter (:2374-2411): active element, a non-empty pair range, and not entirely on one
 // side of the range box along any axis -> candidate record (multi-GPU: a rank's lists hold the
-// triangles of its own elements only)
+// triangles of its own elements only), and one search item per cell of its neighbourhood that its
+// sphere can reach (cell_reaches), appended to the same shard
 __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s, const int* tri_cnt,
                                                 const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                 const int* tri_ele, const PairParam* par,
                                                 const unsigned long long* bbox, unsigned int* ccnt, TriRec* cand,
-                                                long long cshard_cap) {
+                                                long long cshard_cap, uint2* item) {
     const int n = *tri_cnt;
     __shared__ unsigned s_app[2];
     for (int q0 = bid * blockDim.x; q0 < n; q0 += nb * blockDim.x) {  // block-uniform trip count
@@ -889,12 +953,29 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
         }
         const int shard = bid % kCandShards;
         const unsigned slot = block_append(&ccnt[shard * kShardStride], keep, s_app);
-        if (keep && (long long)slot < cshard_cap) {
-            TriRec T;
+        const bool stored = keep && (long long)slot < cshard_cap;
+        TriRec T;
+        unsigned ni = 0;
+        if (stored) {
             double vj[3];
             velo(s, nd0, vj);
             tri_geom(pr, r, pp, gid(s, nd0), gid(s, nd1), gid(s, nd2), ele, p0, p1, p2, vj, T);
             cand[shard * cshard_cap + slot] = T;
+        }
+        const unsigned mask = stored ? reach_mask(T, r.amn, pp.ddiv) : 0u;
+        ni = (unsigned)__popc(mask);
+        unsigned it = block_append_n(&ccnt[shard * kShardStride + kItemWord], ni, s_app);
+        if (ni) {
+            const long long icap = kItemsPerCand * cshard_cap;
+            uint2* out = item + (long long)shard * icap;
+            const unsigned cs = (unsigned)(shard * cshard_cap + slot);
+            for (unsigned mm = mask; mm; mm &= mm - 1) {
+                const int dc = __ffs(mm) - 1;
+                const unsigned b = (unsigned)T.hoff + (hash3(T.mj[0] + (dc % 3 - 1), T.mj[1] + ((dc / 3) % 3 - 1),
+                                                             T.mj[2] + (dc / 9 - 1)) & (unsigned)T.hmask);
+                if ((long long)it < icap) out[it] = make_uint2(cs, ((unsigned)dc << 27) | b);
+                ++it;
+            }
         }
     }
 }
@@ -902,9 +983,10 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
 __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_cnt, const int* tri_live,
                                                       const int* tri_pair, const int* tri_nodes, const int* tri_ele,
                                                       const PairParam* par, const unsigned long long* bbox,
-                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap) {
+                                                      unsigned int* ccnt, TriRec* cand, long long cshard_cap,
+                                                      uint2* item) {
     tri_filter_body(blockIdx.x, gridDim.x, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par, bbox, ccnt, cand,
-                    cshard_cap);
+                    cshard_cap, item);
 }
 
 // events of one thread, kept in registers and appended with one atomic per wave (a same-address
@@ -953,7 +1035,7 @@ __device__ __forceinline__ BEnt ld_bent(const BEnt* e) {
 }
 
 // one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
-// i-nodes of hash bucket b, the bucket of one of the 27 cells around the triangle's first node.
+// i-nodes of cell mj (one of the 27 around the triangle's first node), found in hash bucket b.
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
                                          int b, unsigned seq, const PairParam* par, const unsigned long long* head,
                                          const BEnt* __restrict__ blist, const BVel* __restrict__ bvel, double d_lim,
@@ -982,9 +1064,10 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
         const BEnt be = ld_bent(blist + sl);
         nxt = (int)be.next;
         const int i = be.node;
-        // branch-free cell and self tests: no load waits behind a branch
-        bool skip = ((int)(llabs(mj[0] - be.m[0]) > 1) | (int)(llabs(mj[1] - be.m[1]) > 1) |
-                     (int)(llabs(mj[2] - be.m[2]) > 1)) != 0;
+        // branch-free cell and self tests: no load waits behind a branch. Only the bucket's entries of
+        // this very cell (other cells' entries are found through their own item, if their cell is
+        // searched at all)
+        bool skip = ((int)(mj[0] != be.m[0]) | (int)(mj[1] != be.m[1]) | (int)(mj[2] != be.m[2])) != 0;
         if (self) {
 #pragma unroll
             for (int a = 0; a < 8; ++a) skip |= (i == own8[a]);
@@ -1061,19 +1144,23 @@ __device__ __forceinline__ void ev_flush(const EvBuf& eb, int lane, unsigned int
             ev_write(sh_nodes, sh_f, base + u, eb.i[u], eb.j0, eb.j1, eb.j2, eb.f[u][0], eb.f[u][1], eb.f[u][2]);
 }
 
-// 32 lanes per candidate triangle (27 cells used; the record loads are wave-uniform)
-__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
-                                                const TriRec* cand, long long cshard_cap,
-                                                const PairParam* par, const unsigned long long* head,
-                                                const BEnt* blist, const BVel* bvel, double d_lim, double myu,
-                                                unsigned int* evs, long long shard_cap, int* ev_nodes, double* ev_f) {
-    __shared__ unsigned s_cpre[kCandShards + 4];
-    const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
+// one lane per search item (candidate triangle, cell): the prefilter listed only the cells its
+// sphere reaches, so no lane is idle and no bucket needs deduplicating (each item takes its own
+// cell's entries)
+__device__ __forceinline__ void tri_body(const StepIn& s, unsigned int* ctl, const unsigned int* ccnt,
+                                         const TriRec* cand, long long cshard_cap, const uint2* item,
+                                         const PairParam* par, const unsigned long long* head, const BEnt* blist,
+                                         const BVel* bvel, double d_lim, double myu, unsigned int* evs,
+                                         long long shard_cap, int* ev_nodes, double* ev_f) {
+    __shared__ unsigned s_cpre[kCandShards + 4], s_ipre[kCandShards + 4];
+    (void)shard_scan(ccnt, cshard_cap, s_cpre);
+    const long long icap = kItemsPerCand * cshard_cap;
+    const long long n = shard_scan(ccnt + kItemWord, icap, s_ipre);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
         ctl[kNcand] = s_cpre[kCandShards + 2];
         atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
         atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
-        ctl[kCandOver] = s_cpre[kCandShards + 1];
+        ctl[kCandOver] = s_cpre[kCandShards + 1] | s_ipre[kCandShards + 1];
     }
     const int lane = (int)(threadIdx.x & 63);
     const unsigned seq = ctl[kSeq];
@@ -1086,36 +1173,25 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
         EvBuf eb;
         eb.n = 0;
         eb.j0 = eb.j1 = eb.j2 = 0;
-        // lane c of a triangle's 32 takes cell c (dz, dy, dx in the reference's loop order); a cell
-        // whose bucket a lower cell of the same triangle maps to is skipped, so every bucket is
-        // visited once. Buckets are compared across lanes (readlane), one hash per lane.
-        const int cell = (int)(q & 31);
-        const bool valid = q < n && cell < 27;
-        const TriRec* rec = cand + (valid ? shard_slot(s_cpre, cshard_cap, q >> 5) : 0);
-        long long mj[3] = {0, 0, 0};
-        unsigned hb = 0x80000000u | (unsigned)lane;  // never equal to a real bucket (< 2^31)
-        int hoff = 0;
-        if (valid) {
-            hoff = rec->hoff;
-            mj[0] = rec->mj[0];
-            mj[1] = rec->mj[1];
-            mj[2] = rec->mj[2];
-            hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
-                 (unsigned)rec->hmask;
+        if (q < n) {
+            const uint2 it = item[shard_slot(s_ipre, icap, q)];
+            const TriRec* rec = cand + it.x;
+            const int dc = (int)(it.y >> 27);
+            const long long cell[3] = {rec->mj[0] + (dc % 3 - 1), rec->mj[1] + ((dc / 3) % 3 - 1),
+                                       rec->mj[2] + (dc / 9 - 1)};
+            tri_cell(s, rec, cell, (int)(it.y & ((1u << 27) - 1u)), seq, par, head, blist, bvel, d_lim, myu, evn,
+                     shard_cap, sh_nodes, sh_f, eb);
         }
-        bool dup = false;
-        const int half = lane & 32;
-#pragma unroll
-        for (int c2 = 0; c2 < 26; ++c2) {
-            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)hb, c2);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)hb, 32 + c2);
-            dup |= c2 < cell && (half ? hi : lo) == hb;
-        }
-        if (valid && !dup)
-            tri_cell(s, rec, mj, hoff + (int)hb, seq, par, head, blist, bvel, d_lim, myu, evn, shard_cap, sh_nodes,
-                     sh_f, eb);
         ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
+}
+
+__global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
+                                                const TriRec* cand, long long cshard_cap, const uint2* item,
+                                                const PairParam* par, const unsigned long long* head,
+                                                const BEnt* blist, const BVel* bvel, double d_lim, double myu,
+                                                unsigned int* evs, long long shard_cap, int* ev_nodes, double* ev_f) {
+    tri_body(s, ctl, ccnt, cand, cshard_cap, item, par, head, blist, bvel, d_lim, myu, evs, shard_cap, ev_nodes, ev_f);
 }
 
 // the event shards; block 0 also publishes the totals for the overflow check and the stats
@@ -1253,9 +1329,11 @@ __device__ __forceinline__ void sum_body(int bid, int nb, const unsigned int* ct
     }
 }
 
-__global__ void k_ct_sum(const unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
+__global__ void k_ct_sum(unsigned int* ctl, int tsel, const int* touched, const int* toff, const int* tcnt,
                          const double* terms, double* fext, const int* g2l) {
     sum_body(blockIdx.x, gridDim.x, ctl, tsel, touched, toff, tcnt, terms, fext, g2l);
+    // multi-GPU: the next step's touched list starts empty (its steps run no k_ct_reset)
+    if (g2l && blockIdx.x == 0 && threadIdx.x == 0) ctl[kTouched + 1 - tsel] = 0;
 }
 
 // ---- small decks: fused single-workgroup phases ------------------------------------------------
@@ -1276,7 +1354,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_ct_prologue1(
     __syncthreads();
     find_del_body(0, 1, ctl, del_step, nE, t, t_rd, dlist);
     __syncthreads();
-    append_body(0, 1, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live);
+    append_body(0, 1, ctl, dlist, A, del_step, t, t_rd, reg, ni_live, nj_live, tri_live, (int)threadIdx.x,
+                (int)blockDim.x);
 }
 
 __global__ __launch_bounds__(kSmallThreads) void k_ct_gather1(unsigned int* ctl, const unsigned int* evs,
@@ -1303,12 +1382,12 @@ __global__ __launch_bounds__(kB) void k_ct_binfilter(StepIn s, const Seg* segs, 
                                                      int sb, int nbin, const int* tri_cnt,
                                                      const int* tri_live, const int* tri_pair, const int* tri_nodes,
                                                      const int* tri_ele, unsigned int* ccnt, TriRec* cand,
-                                                     long long cshard_cap) {
+                                                     long long cshard_cap, uint2* item) {
     if ((int)blockIdx.x < nbin)
         bin_body(blockIdx.x, s, segs, reg, ni_live, ni_pair, ni_node, par, bbox, ctl, head, blist, bvel, sb);
     else
         tri_filter_body(blockIdx.x - nbin, gridDim.x - nbin, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par,
-                        bbox, ccnt, cand, cshard_cap);
+                        bbox, ccnt, cand, cshard_cap, item);
 }
 
 // ---- multi-GPU exchange (hkc::Xrank) --------------------------------------------------------
@@ -1427,11 +1506,24 @@ __device__ __forceinline__ void x_counts(const int4* s_h, int nr, int x, int* xc
 }
 
 // every rank's events; only the terms of this rank's nodes (g2l >= 0) are counted and summed
+// (also the reset's share of phase B: the previous step's touched nodes' forces back to 0 -- the
+// nodal update of that step has read them -- and the term counter)
 __global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, const int* g2l, int* cnt, int* touched,
-                             int* tpos, int tsel, int* poison, int pstep, int* xctl, int* hc) {
+                             int* tpos, int tsel, int* poison, int pstep, int* xctl, int* hc, const int* touched_prev,
+                             double* fext) {
     __shared__ long long s_off[kMaxXRanks + 1];
     __shared__ unsigned s_app[2];
     __shared__ int4 s_h[kMaxXRanks];
+    {
+        const int np = (int)ld_ctl(&ctl[kTouched + 1 - tsel]);
+        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
+            const long long l = g2l[touched_prev[q]];
+            fext[3 * l] = 0.0;
+            fext[3 * l + 1] = 0.0;
+            fext[3 * l + 2] = 0.0;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctl[kTerms] = 0;
+    }
     load_hdrs(xb, nr, s_h);
     x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 4);
     x_counts(s_h, nr, 2, xctl, hc);
@@ -1558,6 +1650,70 @@ __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long 
     }
 }
 
+// A1 of a step without a full rebuild (multi-GPU), ONE 1024-thread workgroup: k_ct_reset's share of
+// the phase (event and candidate counters, this step's partial box words and bin block header, the
+// bucket-head sequence), every rank's deletion records into the global deletion steps and the
+// deletion list, and the surface append (a wave per deleted element). A rank's block that is full
+// (a peer out of step) is unpacked too. The previous step's touched forces and the term counter are
+// phase B's (k_ct_count_g), the touched counter the previous k_ct_sum's.
+__global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del,
+                                                   long long nE_g, int* poison, int t, int* xctl, int* hc,
+                                                   unsigned int* ctl, int* dlist, unsigned long long* bbox,
+                                                   int npairs, unsigned int* evs, unsigned int* ccnt, int* zero_hdr,
+                                                   AppendIn A, int* reg, int* ni_live, int* nj_live, int* tri_live,
+                                                   int with_lists) {
+    __shared__ int4 s_h[kMaxXRanks];
+    load_hdrs(xb, nr, s_h);
+    x_counts(s_h, nr, 0, xctl, hc);
+    const int tid = (int)threadIdx.x, bd = (int)blockDim.x;
+    if (tid < kEvShards) evs[tid * kShardStride] = 0;
+    if (tid < kCandShards) ccnt[tid * kShardStride] = ccnt[tid * kShardStride + kItemWord] = 0;
+    for (int q = tid; q < 12 * npairs; q += bd) bbox[q] = ((q % 12) / 3) % 2 == 0 ? ~0ULL : 0ULL;
+    if (tid < 2) zero_hdr[tid] = 0;
+    if (tid == 0) {
+        int mx = 0;
+        bool over = false;
+        for (int r = 0; r < nr; ++r) {
+            mx = max(mx, s_h[r].z);
+            over |= !s_h[r].w && (long long)s_h[r].x > cap;
+        }
+        g_del[nE_g + 1] = mx;
+        ctl[kEv] = 0;
+        ctl[kDirty] = 0;
+        ctl[kNdel] = 0;
+        ctl[kNcand] = 0;
+        ctl[kCandOver] = 0;
+        ctl[kSeq] = ctl[kSeq] + 1u;
+        ctl[kDel] = mx == t - 1 ? 1u : 0u;
+        if (over) {
+            atomicOr(xctl, 1);
+            if (poison[0] == 0) {
+                poison[1] = t;
+                poison[0] = 1;
+            }
+        }
+        __threadfence();  // (the counters before the other waves' atomics and agent-scope loads)
+    }
+    __syncthreads();
+    for (int q = 0; q < nr; ++q) {
+        const int* pl = reinterpret_cast<const int*>(xb.p[q] + kXHdr);
+        if (s_h[q].w) {
+            const long long e0 = e_off[q], ne = e_off[q + 1] - e0;
+            for (long long k = tid; k < ne; k += bd) g_del[e0 + k] = pl[k];
+        } else {
+            const long long n = min((long long)s_h[q].x, cap);
+            for (long long k = tid; k < n; k += bd) {
+                const int e = pl[2 * k], d = pl[2 * k + 1];
+                g_del[e] = d;
+                if (d == t - 1) dlist[atomicAdd(&ctl[kNdel], 1u)] = e;
+            }
+        }
+    }
+    __syncthreads();
+    if (with_lists)
+        append_body(tid >> 6, bd >> 6, ctl, dlist, A, g_del, t, nullptr, reg, ni_live, nj_live, tri_live, tid & 63, 64);
+}
+
 // pair boxes of all ranks: min of the min words, max of the max words (exact, order-free). RCCL
 // all-reduces with MIN: the max words travel complemented (k_xr_boxflip before and after).
 __global__ void k_xr_boxflip(unsigned long long* bb, int n) {
@@ -1651,12 +1807,26 @@ __global__ void k_xr_insert(XBlk xb, int nr, long long cap, const PairParam* par
     const int q = (int)blockIdx.y;
     const long long n = min((long long)s_h[q].x, cap);
     const unsigned seq = ctl[kSeq];
-    const BRec* rec = reinterpret_cast<const BRec*>(xb.p[q] + kXHdr);
+    const uint4* rec = reinterpret_cast<const uint4*>(xb.p[q] + kXHdr);  // 6 x 16 B per record
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
-        const BEnt e = rec[k].e;
-        const PairParam& pp = par[e.pad];
-        const int b = pp.hash_off + (int)(hash3(e.m[0], e.m[1], e.m[2]) & (unsigned)(pp.hash_size - 1));
-        bucket_push(head, b, seq, (int)(q * cap + k), e, rec[k].w, blist, bvel);
+        // the record moves as six 16-B vectors (a by-value BRec became a 96-B private array in LDS)
+        uint4 w[6];
+#pragma unroll
+        for (int v = 0; v < 6; ++v) w[v] = rec[6 * k + v];
+        const PairParam& pp = par[(int)w[1].w];  // BEnt: m[3] = w0.xy w0.zw w1.xy, node w1.z, pad w1.w
+        const int b = pp.hash_off + (int)(hash3(ll2(w[0].x, w[0].y), ll2(w[0].z, w[0].w), ll2(w[1].x, w[1].y)) &
+                                          (unsigned)(pp.hash_size - 1));
+        const int slot = (int)(q * cap + k);
+        const unsigned long long old = atomicExch(&head[b], ((unsigned long long)seq << 32) | (unsigned)slot);
+        const long long nx = (unsigned)(old >> 32) == seq ? (long long)(unsigned)old : -1LL;
+        w[3].z = (unsigned)(unsigned long long)nx;  // BEnt::next, the last 8 B
+        w[3].w = (unsigned)((unsigned long long)nx >> 32);
+        uint4* be = reinterpret_cast<uint4*>(blist + slot);
+        uint4* bv = reinterpret_cast<uint4*>(bvel + slot);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) be[v] = w[v];
+        bv[0] = w[4];
+        bv[1] = w[5];
     }
 }
 
@@ -1815,7 +1985,7 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_head); dfree(C->d_blist); dfree(C->d_bvel);
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
-    dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt);
+    dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt); dfree(C->d_item);
     if (Xrank* X = C->xr) {
         (void)hipDeviceSynchronize();  // in-process peers may still read this rank's blocks
         dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->d_last_del);
@@ -2041,6 +2211,11 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                            C->d_ccnt, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext, del_step,
                            (int)C->nE, C->d_dlist, A, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live,
                            C->ntile > 0 ? 1 : 0);
+    } else if (X && !rebuild) {  // multi-GPU: the reset's share, the deletions and the append in one workgroup
+        hipLaunchKernelGGL(k_xr_front, dim3(1), dim3(1024), 0, s, xb, X->nranks, X->d_eoff, X->cap[0], X->g_del,
+                           X->nE_g, c->d_poison, in.t, X->d_xctl, X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks,
+                           C->d_ctl, C->d_dlist, bbox, C->npairs, C->d_evs, C->d_ccnt, (int*)X->d_send[1][X->par_a], A,
+                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live, C->ntile > 0 ? 1 : 0);
     } else {
         hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
                            C->force_rebuild ? 1 : 0, X ? nullptr : del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel,
@@ -2107,7 +2282,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
                                C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head,
                                C->d_blist, C->d_bvel, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
                                C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_ccnt, (TriRec*)C->d_cand,
-                               C->cshard_cap);
+                               C->cshard_cap, C->d_item);
         } else {
             hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
                                C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head, C->d_blist,
@@ -2118,7 +2293,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
         if (!fused_mid)
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                                C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
-                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap);
+                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, C->d_item);
         tri_search(c, in);
     }
     const unsigned ge = (unsigned)C->g_ev;
@@ -2146,7 +2321,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
 static void tri_search(hakai_ctx* c, const StepIn& in) {
     Contact* C = c->contact;
     hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, c->stream, in, C->d_ctl, C->d_ccnt,
-                       (const TriRec*)C->d_cand, C->cshard_cap, C->d_par, C->d_head, C->d_blist, C->d_bvel, C->d_lim,
+                       (const TriRec*)C->d_cand, C->cshard_cap, C->d_item, C->d_par, C->d_head, C->d_blist, C->d_bvel, C->d_lim,
                        C->myu, C->d_evs, C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
 }
 
@@ -2212,7 +2387,7 @@ static int xr_a3(hakai_ctx* c, double d_time) {
         const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
         hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                            C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, X->d_boxg, C->d_ccnt,
-                           (TriRec*)C->d_cand, C->cshard_cap);
+                           (TriRec*)C->d_cand, C->cshard_cap, C->d_item);
         tri_search(c, in);
     }
     hipLaunchKernelGGL(k_ev_pack, dim3((unsigned)C->g_ev), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
@@ -2256,7 +2431,7 @@ int contact_step_b(hakai_ctx* c) {
     const unsigned ge = (unsigned)C->g_ev;
     hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, X->cap[2], nr, X->d_g2l, C->d_cnt,
                        C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, X->t_a, X->d_xctl,
-                       X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * nr);
+                       X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * nr, C->d_touched[1 - tsel], c->d_fext);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
     hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, X->cap[2], nr, X->d_g2l, C->d_ctl, C->d_toff,
@@ -2351,8 +2526,10 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipStreamSynchronize(c->stream));
         if (C->d_cand) (void)hipFree(C->d_cand);
         C->d_cand = nullptr;
+        dfree(C->d_item);
         size_cand(C, value);
         HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
+        HIPCHK(dalloc(&C->d_item, (size_t)kItemsPerCand * C->cand_cap));
         HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, 3 * sizeof(unsigned int), c->stream));  // + shard max, over
         return 0;
     }
@@ -2731,9 +2908,9 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         C->g_seg = clampi((maxseg + kB - 1) / kB, 1, kSegBlocks);
         C->g_box = clampi((maxseg + 4 * kB - 1) / (4 * kB), 1, 128);  // ~4 entries per thread: one unrolled pass
         C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
-        // >= 64 waves (every event shard); one pass over every live triangle as a candidate (32
-        // lanes each) up to the 4096-block cap -- small self-contact decks keep half their triangles
-        C->g_tri = clampi((32 * ct0 + 127) / 128, 32, 4096);
+        // >= 64 waves (every event shard); one pass over 16 search items (reachable cells) per live
+        // triangle up to the 4096-block cap -- small self-contact decks keep half their triangles
+        C->g_tri = clampi((16 * ct0 + 127) / 128, 32, 4096);
         C->g_node = clampi((2 * ci0 + kB - 1) / kB, 4, 256);
         C->g_del = clampi((C->nE / 4 + kB - 1) / kB, 1, 1024);
         C->g_reset = clampi((std::max<long long>(std::max<long long>(kEvShards, 12LL * C->npairs), 2 * ci0) + kB - 1) / kB,
@@ -2844,6 +3021,8 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     }
     HIPCHK(dalloc(&C->d_ccnt, (size_t)kCandShards * kShardStride));
     HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
+    HIPCHK(dalloc(&C->d_item, (size_t)kItemsPerCand * C->cand_cap));
+    if (C->htot >= (1 << 27)) return fail(HAKAI_ERR_ARG, "contact: %d hash buckets (search items hold 27 bits)", C->htot);
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));

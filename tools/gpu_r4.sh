@@ -56,7 +56,7 @@ for st in "$@"; do
     decks) run 900 gpurun_out/r4_decks.jsonl python tools/deck_bench.py --cpu-steps 0 || exit $? ;;
     deckprof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_deckprof.log rocprofv3 --kernel-trace --stats \
                   -d gpurun_out/r4_deckprof -o deck -- python tools/deck_bench.py --decks ${DECK:-car_crash_N2k} \
-                  --cpu-steps 0 --modes 1 --max-steps 3200 || exit $? ;;
+                  --cpu-steps 0 --modes 1 --max-steps 3200 --tuning graph=0 || exit $? ;;
     tests:*) run 1200 gpurun_out/r4_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
                  --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
