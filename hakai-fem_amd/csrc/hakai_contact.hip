@@ -962,6 +962,7 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
             tri_geom(pr, r, pp, gid(s, nd0), gid(s, nd1), gid(s, nd2), ele, p0, p1, p2, vj, T);
             cand[shard * cshard_cap + slot] = T;
         }
+        if (!item) continue;  // (small decks: no items, k_ct_tri32; block-uniform)
         const unsigned mask = stored ? reach_mask(T, r.amn, pp.ddiv) : 0u;
         ni = (unsigned)__popc(mask);
         unsigned it = block_append_n(&ccnt[shard * kShardStride + kItemWord], ni, s_app);
@@ -1036,6 +1037,7 @@ __device__ __forceinline__ BEnt ld_bent(const BEnt* e) {
 
 // one (candidate triangle, neighbour cell) pair: the rest of the loop body at :2371-2698 for the
 // i-nodes of cell mj (one of the 27 around the triangle's first node), found in hash bucket b.
+template <bool EXACT_CELL>
 __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restrict__ rec, const long long mj[3],
                                          int b, unsigned seq, const PairParam* par, const unsigned long long* head,
                                          const BEnt* __restrict__ blist, const BVel* __restrict__ bvel, double d_lim,
@@ -1064,10 +1066,14 @@ __device__ __forceinline__ void tri_cell(const StepIn& s, const TriRec* __restri
         const BEnt be = ld_bent(blist + sl);
         nxt = (int)be.next;
         const int i = be.node;
-        // branch-free cell and self tests: no load waits behind a branch. Only the bucket's entries of
-        // this very cell (other cells' entries are found through their own item, if their cell is
-        // searched at all)
-        bool skip = ((int)(mj[0] != be.m[0]) | (int)(mj[1] != be.m[1]) | (int)(mj[2] != be.m[2])) != 0;
+        // branch-free cell and self tests: no load waits behind a branch. EXACT_CELL (search items):
+        // only the bucket's entries of this very cell (other cells' entries are found through their
+        // own item, if their cell is searched at all); else (32 lanes per candidate, each bucket
+        // visited once) every entry of the 27-neighbourhood of the first-node cell mj
+        bool skip = EXACT_CELL
+                        ? ((int)(mj[0] != be.m[0]) | (int)(mj[1] != be.m[1]) | (int)(mj[2] != be.m[2])) != 0
+                        : ((int)(llabs(mj[0] - be.m[0]) > 1) | (int)(llabs(mj[1] - be.m[1]) > 1) |
+                           (int)(llabs(mj[2] - be.m[2]) > 1)) != 0;
         if (self) {
 #pragma unroll
             for (int a = 0; a < 8; ++a) skip |= (i == own8[a]);
@@ -1179,8 +1185,8 @@ __device__ __forceinline__ void tri_body(const StepIn& s, unsigned int* ctl, con
             const int dc = (int)(it.y >> 27);
             const long long cell[3] = {rec->mj[0] + (dc % 3 - 1), rec->mj[1] + ((dc / 3) % 3 - 1),
                                        rec->mj[2] + (dc / 9 - 1)};
-            tri_cell(s, rec, cell, (int)(it.y & ((1u << 27) - 1u)), seq, par, head, blist, bvel, d_lim, myu, evn,
-                     shard_cap, sh_nodes, sh_f, eb);
+            tri_cell<true>(s, rec, cell, (int)(it.y & ((1u << 27) - 1u)), seq, par, head, blist, bvel, d_lim, myu,
+                           evn, shard_cap, sh_nodes, sh_f, eb);
         }
         ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
     }
@@ -1192,6 +1198,63 @@ __global__ __launch_bounds__(128) void k_ct_tri(StepIn s, unsigned int* ctl, con
                                                 const BEnt* blist, const BVel* bvel, double d_lim, double myu,
                                                 unsigned int* evs, long long shard_cap, int* ev_nodes, double* ev_f) {
     tri_body(s, ctl, ccnt, cand, cshard_cap, item, par, head, blist, bvel, d_lim, myu, evs, shard_cap, ev_nodes, ev_f);
+}
+
+// Small decks: 32 lanes per candidate triangle (27 cells used), lane c takes cell c (dz, dy, dx in the
+// reference's loop order); a cell whose bucket a lower cell of the same triangle maps to is
+// skipped, so every bucket is visited once (buckets compared across lanes, readlane). No search
+// items: at a few hundred candidates the prefilter's item pass costs more than idle lanes do.
+__global__ __launch_bounds__(128) void k_ct_tri32(StepIn s, unsigned int* ctl, const unsigned int* ccnt,
+                                                  const TriRec* cand, long long cshard_cap, const PairParam* par,
+                                                  const unsigned long long* head, const BEnt* blist, const BVel* bvel,
+                                                  double d_lim, double myu, unsigned int* evs, long long shard_cap,
+                                                  int* ev_nodes, double* ev_f) {
+    __shared__ unsigned s_cpre[kCandShards + 4];
+    const long long n = 32LL * shard_scan(ccnt, cshard_cap, s_cpre);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // totals for the stats, the overflow check and the poison
+        ctl[kNcand] = s_cpre[kCandShards + 2];
+        atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
+        atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
+        ctl[kCandOver] = s_cpre[kCandShards + 1];
+    }
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned seq = ctl[kSeq];
+    const int shard = (int)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) % kEvShards);
+    unsigned int* evn = evs + shard * kShardStride;
+    int* sh_nodes = ev_nodes + 4 * (long long)shard * shard_cap;
+    double* sh_f = ev_f + 3 * (long long)shard * shard_cap;
+    for (long long q0 = blockIdx.x * (long long)blockDim.x; q0 < n; q0 += (long long)gridDim.x * blockDim.x) {
+        const long long q = q0 + threadIdx.x;  // wave-uniform trip count (the append below is wave-wide)
+        EvBuf eb;
+        eb.n = 0;
+        eb.j0 = eb.j1 = eb.j2 = 0;
+        const int cell = (int)(q & 31);
+        const bool valid = q < n && cell < 27;
+        const TriRec* rec = cand + (valid ? shard_slot(s_cpre, cshard_cap, q >> 5) : 0);
+        long long mj[3] = {0, 0, 0};
+        unsigned hb = 0x80000000u | (unsigned)lane;  // never equal to a real bucket (< 2^31)
+        int hoff = 0;
+        if (valid) {
+            hoff = rec->hoff;
+            mj[0] = rec->mj[0];
+            mj[1] = rec->mj[1];
+            mj[2] = rec->mj[2];
+            hb = hash3(mj[0] + (cell % 3 - 1), mj[1] + ((cell / 3) % 3 - 1), mj[2] + (cell / 9 - 1)) &
+                 (unsigned)rec->hmask;
+        }
+        bool dup = false;
+        const int half = lane & 32;
+#pragma unroll
+        for (int c2 = 0; c2 < 26; ++c2) {
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)hb, c2);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)hb, 32 + c2);
+            dup |= c2 < cell && (half ? hi : lo) == hb;
+        }
+        if (valid && !dup)
+            tri_cell<false>(s, rec, mj, hoff + (int)hb, seq, par, head, blist, bvel, d_lim, myu, evn, shard_cap,
+                            sh_nodes, sh_f, eb);
+        ev_flush(eb, lane, evn, shard_cap, sh_nodes, sh_f);
+    }
 }
 
 // the event shards; block 0 also publishes the totals for the overflow check and the stats
@@ -2282,7 +2345,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
                                C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head,
                                C->d_blist, C->d_bvel, C->g_seg, nbin, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
                                C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_ccnt, (TriRec*)C->d_cand,
-                               C->cshard_cap, C->d_item);
+                               C->cshard_cap, C->small ? nullptr : C->d_item);
         } else {
             hipLaunchKernelGGL(k_ct_bin, dim3(C->nseg * C->g_seg), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
                                C->d_ni_pair, C->d_ni_node, C->d_par, C->d_bbox, C->d_ctl, C->d_head, C->d_blist,
@@ -2293,7 +2356,7 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
         if (!fused_mid)
             hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                                C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, C->d_bbox,
-                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, C->d_item);
+                               C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, C->small ? nullptr : C->d_item);
         tri_search(c, in);
     }
     const unsigned ge = (unsigned)C->g_ev;
@@ -2320,6 +2383,12 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
 
 static void tri_search(hakai_ctx* c, const StepIn& in) {
     Contact* C = c->contact;
+    if (C->small) {
+        hipLaunchKernelGGL(k_ct_tri32, dim3(C->g_tri), dim3(128), 0, c->stream, in, C->d_ctl, C->d_ccnt,
+                           (const TriRec*)C->d_cand, C->cshard_cap, C->d_par, C->d_head, C->d_blist, C->d_bvel,
+                           C->d_lim, C->myu, C->d_evs, C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
+        return;
+    }
     hipLaunchKernelGGL(k_ct_tri, dim3(C->g_tri), dim3(128), 0, c->stream, in, C->d_ctl, C->d_ccnt,
                        (const TriRec*)C->d_cand, C->cshard_cap, C->d_item, C->d_par, C->d_head, C->d_blist, C->d_bvel, C->d_lim,
                        C->myu, C->d_evs, C->cap / kEvShards, C->d_ev_nodes, C->d_ev_f);
@@ -2387,7 +2456,7 @@ static int xr_a3(hakai_ctx* c, double d_time) {
         const unsigned gfilt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
         hipLaunchKernelGGL(k_ct_tri_filter, dim3(gfilt), dim3(kB), 0, s, in, C->d_reg + 2 * C->tri_reg + 1,
                            C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, X->d_boxg, C->d_ccnt,
-                           (TriRec*)C->d_cand, C->cshard_cap, C->d_item);
+                           (TriRec*)C->d_cand, C->cshard_cap, C->small ? nullptr : C->d_item);
         tri_search(c, in);
     }
     hipLaunchKernelGGL(k_ev_pack, dim3((unsigned)C->g_ev), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
@@ -2910,7 +2979,7 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
         C->g_ev = clampi((4 * ci0 + kB - 1) / kB, 16, 1024);
         // >= 64 waves (every event shard); one pass over 16 search items (reachable cells) per live
         // triangle up to the 4096-block cap -- small self-contact decks keep half their triangles
-        C->g_tri = clampi((16 * ct0 + 127) / 128, 32, 4096);
+        C->g_tri = clampi(((C->small ? 32 : 16) * ct0 + 127) / 128, 32, 4096);  // (small: 32 lanes per candidate)
         C->g_node = clampi((2 * ci0 + kB - 1) / kB, 4, 256);
         C->g_del = clampi((C->nE / 4 + kB - 1) / kB, 1, 1024);
         C->g_reset = clampi((std::max<long long>(std::max<long long>(kEvShards, 12LL * C->npairs), 2 * ci0) + kB - 1) / kB,
