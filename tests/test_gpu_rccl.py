@@ -50,13 +50,14 @@ def test_rccl_interface_exchange_owner_assembly_bitexact(n):
     assert f"RCCL {n}-rank interface exchange (owner-computed assembly) vs 1 context bit-exact: True" in out
 
 
-def test_rccl_contact_bitexact():
-    """Two-body impact with contact deletions over 2 RCCL ranks (owner-computed search), with the
-    default exchange capacities and with one-record blocks that grow (the overflowing steps run
-    again)."""
-    out = _torchrun("tools/rccl_contact_check.py", 2)
-    assert "RCCL 2-rank contact (exchange capacities default) vs 1 context bit-exact: True" in out
-    assert "RCCL 2-rank contact (exchange capacities 1) vs 1 context bit-exact: True" in out
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_contact_bitexact(world):
+    """Two-body impact with contact deletions over 2 and 3 RCCL ranks (owner-computed search; at 3
+    ranks the middle rank exchanges with both neighbours), with the default exchange capacities
+    and with one-record blocks that grow (the overflowing steps run again)."""
+    out = _torchrun("tools/rccl_contact_check.py", world)
+    assert f"RCCL {world}-rank contact (exchange capacities default) vs 1 context bit-exact: True" in out
+    assert f"RCCL {world}-rank contact (exchange capacities 1) vs 1 context bit-exact: True" in out
 
 
 def test_torchrun_driver_writes_the_same_vtk():
