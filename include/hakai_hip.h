@@ -194,6 +194,9 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       contact, records per rank block of each per-step exchange (they also grow
  *                       on their own; call on every rank between steps);
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
+ *   "contact_filter_memo" -1 (default: on for decks that are not small), 0 or 1: the triangle
+ *                       prefilter skips a triangle it rejected before while the nodes' accumulated
+ *                       motion cannot have brought it to its pair's range box (same candidates);
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0); 2: the
  *                       same, each phase enqueued behind a fixed ≈0.3 ms sleep kernel so it runs
@@ -245,8 +248,9 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
  * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
  * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
  * [7] contact-zone nodes all ranks binned in the last step, [8] bytes of one rank's per-step
- * exchange blocks at their capacities (hakai_set_contact_global); [9] hash-grid buckets of all pairs (tables of
- * more than 32 768 entries take the device-wide scan). */
+ * exchange blocks at their capacities (hakai_set_contact_global); [9] hash-grid buckets of all pairs;
+ * [10] live triangles the prefilter tested in full in the last step (the rest its memo skipped;
+ * multi-GPU: this rank's). */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);

@@ -134,6 +134,33 @@ def test_contact_group_x_slabs_bitexact(world):
     assert sum(1 for st in sts if st["live_triangles"] > 0) == world  # every rank holds surface
 
 
+@pytest.mark.parametrize("world,deck", [(2, "x_slabs"), (3, "deletion")])
+def test_contact_group_filter_memo_bitexact(world, deck):
+    """The prefilter memo on every rank (its clock runs on the all-ranks motion word: a rank's
+    triangles have nodes other ranks own): bit-identical to one context without the memo, the same
+    candidate triangles, fewer triangles tested in full."""
+    from hakai import mesh
+    if deck == "x_slabs":
+        glob = mesh.two_body_model(plate=(8, 8, 2), impactor=(4, 4, 3), v=-3e5, d_time=2e-8, n_steps=400,
+                                   x_slabs=True)
+    else:
+        glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    with Solver(glob) as sv:
+        sv.set_tuning("contact_filter_memo", 0)
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+        gst = sv.contact_stats()
+    parts = _run_contact_group(glob, world, glob.n_steps, key=370 + world, tune={"contact_filter_memo": 1})
+    _assert_group_equals_single(glob, parts, g, gdel)
+    sts = [st for *_, st in parts]
+    assert sum(st["candidate_triangles"] for st in sts) == gst["candidate_triangles"]
+    assert sum(st["tested_triangles"] for st in sts) < sum(st["live_triangles"] for st in sts)
+    # the A3 insert and prefilter in two launches (contact_fuse_binfilter 0) instead of one
+    parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world, tune={"contact_fuse_binfilter": 0})
+    _assert_group_equals_single(glob, parts, g, gdel)
+
+
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_contact_group_bitexact_with_deletion(world):
     """Multi-GPU contact: contact-driven deletion with the surface update, the

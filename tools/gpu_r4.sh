@@ -12,7 +12,8 @@
 #   drift      fused-kernel drift on the reference decks  -> gpurun_out/r4_deck_drift.jsonl
 #   c4ranks    C4 contact per rank: one context, 2 and 4 in-process ranks -> gpurun_out/r4_c4_ranks.jsonl
 #   c4xslab    the same with C4's elements numbered x slowest (rank ranges = x-slabs) -> gpurun_out/r4_c4_xslab.jsonl
-#   c4prof     rocprofv3 kernel trace of the C4 contact run, one context and 2 ranks -> gpurun_out/r4_c4prof_{1,2}/
+#   c4prof     rocprofv3 kernel trace of the C4 contact run, one context and 2 ranks -> gpurun_out/r4_c4prof_{1,2}$C4TAG/
+#              (C4TUNE: extra tuning keys, e.g. contact_filter_memo=0)
 #   decks      reference decks end to end, both element modes, graphs -> gpurun_out/r4_decks.jsonl
 #   deckprof   rocprofv3 kernel trace of car-crash-N2k, 3200 steps, stream mode -> gpurun_out/r4_deckprof/
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r4_tests.log
@@ -40,8 +41,8 @@ for st in "$@"; do
               -o r4 -- python bench.py --steps 50 --warmup 5 --cpu-baseline 0 || exit $? ;;
     drift) run 600 gpurun_out/r4_deck_drift.jsonl python tools/deck_drift.py || exit $? ;;
     c4ranks) : > gpurun_out/r4_c4_ranks.jsonl
-        for r in 1 2 4; do
-            run 600 gpurun_out/r4_c4_ranks_$r.log python tools/bench_contact.py --ranks $r --steps 40 --serial ${C4SERIAL:-1} || exit $?
+        for r in ${C4RANKS:-1 2 4}; do
+            run 600 gpurun_out/r4_c4_ranks_$r.log python tools/bench_contact.py --ranks $r --steps 40 --serial ${C4SERIAL:-1} --tuning "${C4TUNE:-}" || exit $?
             grep '^{' gpurun_out/r4_c4_ranks_$r.log >> gpurun_out/r4_c4_ranks.jsonl
         done ;;
     c4xslab) : > gpurun_out/r4_c4_xslab.jsonl
@@ -50,8 +51,8 @@ for st in "$@"; do
             grep '^{' gpurun_out/r4_c4_xslab_$r.log >> gpurun_out/r4_c4_xslab.jsonl
         done ;;
     c4prof) for r in ${C4PROF_RANKS:-1 2}; do
-            run 600 gpurun_out/r4_c4prof_$r.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_c4prof_$r -o c4 \
-                -- python tools/bench_contact.py --ranks $r --steps 40 --x-slabs ${C4PROF_XSLAB:-0} || exit $?
+            run 600 gpurun_out/r4_c4prof_$r${C4TAG:-}.log rocprofv3 --kernel-trace --stats -d gpurun_out/r4_c4prof_$r${C4TAG:-} -o c4 \
+                -- python tools/bench_contact.py --ranks $r --steps 40 --x-slabs ${C4PROF_XSLAB:-0} --tuning "${C4TUNE:-}" || exit $?
         done ;;
     decks) run 900 gpurun_out/r4_decks.jsonl python tools/deck_bench.py --cpu-steps 0 || exit $? ;;
     deckprof) HAKAI_GRAPH=0 run 600 gpurun_out/r4_deckprof.log rocprofv3 --kernel-trace --stats \
