@@ -194,9 +194,12 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       contact, records per rank block of each per-step exchange (they also grow
  *                       on their own; call on every rank between steps);
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
- *   "contact_filter_memo" -1 (default: on for decks that are not small), 0 or 1: the triangle
+ *   "contact_filter_memo" 0 (default), 1, or -1 (on for decks that are not small): the triangle
  *                       prefilter skips a triangle it rejected before while the nodes' accumulated
- *                       motion cannot have brought it to its pair's range box (same candidates);
+ *                       motion cannot have brought it to its pair's range box (same candidates;
+ *                       measured slower on C4, whose contact-zone triangles dominate the prefilter);
+ *   "contact_fuse_binfilter" 1 (default): the binning (multi-GPU: the bucket insert) and the
+ *                       triangle prefilter run in one launch, side by side;
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0); 2: the
  *                       same, each phase enqueued behind a fixed ≈0.3 ms sleep kernel so it runs
