@@ -632,12 +632,15 @@ __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsig
 
 // segment vb / sb, part vb % sb. MOTION (the prefilter memo is on): j-node (triangle node) segments
 // also raise the box array's motion word to their max of |u - u_pre| per component, as the
-// non-negative double's bits (ordered like the values; a NaN is larger than every number and stays)
+// non-negative double's bits (ordered like the values; a NaN is larger than every number and stays).
+// !MOTION with a motion word (a multi-GPU rank without the memo): the word is set to all ones -- a
+// NaN, so the combined clock of any rank that has the memo on stops every skip (no bound from here)
 template <bool MOTION>
 __device__ __forceinline__ void bbox_body(int vb, int sb, const StepIn& s, const Seg* segs, const int* reg,
                                           const int* ni_live, const int* nj_live, const int* ni_node,
                                           const int* nj_node, unsigned long long* bbox,
                                           unsigned long long* motion) {
+    if (!MOTION && motion && vb == 0 && threadIdx.x == 0) *motion = ~0ULL;
     const Seg sg = segs[vb / sb];
     if (sg.dup) return;  // another segment's blocks fill its boxes
     const int sub = vb % sb;
@@ -2619,9 +2622,9 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
     C->last_t = in.t;
     const Seg* sg = (const Seg*)C->d_seg;
     if (C->nseg > 0)
-        hipLaunchKernelGGL((memo_on(C) || X ? k_ct_bbox<true> : k_ct_bbox<false>), dim3(C->nseg * C->g_box), dim3(kB),
-                           0, s, in, sg, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_ni_node, C->d_nj_node, bbox, C->g_box,
-                           bbox + 12 * C->npairs);  // (multi-GPU: every rank, the word is a max over ranks)
+        hipLaunchKernelGGL((memo_on(C) ? k_ct_bbox<true> : k_ct_bbox<false>), dim3(C->nseg * C->g_box), dim3(kB), 0, s,
+                           in, sg, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_ni_node, C->d_nj_node, bbox, C->g_box,
+                           memo_on(C) || X ? bbox + 12 * C->npairs : nullptr);  // (multi-GPU: a max over ranks)
     HIPCHK(hipGetLastError());
     if (X) {
         HIPCHK(hipEventRecord(X->ev_box[X->par_a], s));

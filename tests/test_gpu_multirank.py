@@ -75,7 +75,7 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key, tune=None):
+def _run_contact_group(glob, world, n_steps, key, tune=None, rank_tune=None):
     """Range-partitioned contact model on an in-process group (hakai_set_contact_global): each rank
     searches the triangles of its elements against the binned contact nodes of every rank."""
     gdiag, _ = glob.lumped_mass()
@@ -87,7 +87,7 @@ def _run_contact_group(glob, world, n_steps, key, tune=None):
         sv.comm_init_local(r, world, key)
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
-        for k, v in (tune or {}).items():
+        for k, v in list((tune or {}).items()) + list(((rank_tune or {}).get(r) or {}).items()):
             sv.set_tuning(k, v)
         svs.append(sv)
     step_group(svs, 1, n_steps)
@@ -159,6 +159,12 @@ def test_contact_group_filter_memo_bitexact(world, deck):
     # the A3 insert and prefilter in two launches (contact_fuse_binfilter 0) instead of one
     parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world, tune={"contact_fuse_binfilter": 0})
     _assert_group_equals_single(glob, parts, g, gdel)
+    # the memo on rank 0 only: the other ranks mark the motion clock unbounded, so rank 0 skips
+    # nothing (and stays exact)
+    parts = _run_contact_group(glob, world, glob.n_steps, key=390 + world, rank_tune={0: {"contact_filter_memo": 1}})
+    _assert_group_equals_single(glob, parts, g, gdel)
+    st0 = parts[0][4]
+    assert st0["tested_triangles"] > 0 or st0["live_triangles"] == 0
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
