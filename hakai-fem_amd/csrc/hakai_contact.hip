@@ -195,6 +195,7 @@ struct Contact {
     bool small = false;
     int fuse_small = 1;
     int fuse_binfilter = 1;  // tuning "contact_fuse_binfilter": binning and prefilter in one launch
+    int front_append = 0;    // tuning "contact_front_append" (multi-GPU): the surface append inside k_xr_front
 
     // events and per-node gather over the touched nodes
     long long cap = 0;
@@ -2578,11 +2579,17 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                            C->d_ccnt, del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel, fext, del_step,
                            (int)C->nE, C->d_dlist, A, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live,
                            C->ntile > 0 ? 1 : 0);
-    } else if (X && !rebuild) {  // multi-GPU: the reset's share, the deletions and the append in one workgroup
+    } else if (X && !rebuild) {
+        // multi-GPU: the reset's share and every rank's deletions in one workgroup; the surface append
+        // after it with a full grid (one workgroup took 35-63 us on C4's deletion steps, against
+        // 15-18 for the grid, and ~4 us more on steps without deletions)
         hipLaunchKernelGGL(k_xr_front, dim3(1), dim3(1024), 0, s, xb, X->nranks, X->d_eoff, X->cap[0], X->g_del,
                            X->nE_g, c->d_poison, in.t, X->d_xctl, X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks,
                            C->d_ctl, C->d_dlist, bbox, C->npairs, C->d_evs, C->d_ccnt, (int*)X->d_send[1][X->par_a], A,
-                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live, C->ntile > 0 ? 1 : 0);
+                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live, C->front_append && C->ntile > 0 ? 1 : 0);
+        if (!C->front_append && C->ntile > 0)
+            hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
+                               c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
     } else {
         hipLaunchKernelGGL(k_ct_reset, dim3(C->g_reset), dim3(kB), 0, s, bbox, C->npairs, C->d_ctl, C->d_evs, C->d_ccnt,
                            C->force_rebuild ? 1 : 0, X ? nullptr : del_any, in.t, c->g_trd, C->d_touched[1 - tsel], tsel,
@@ -2897,6 +2904,12 @@ static void size_cand(Contact* C, long long total) {
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
+    if (!std::strcmp(key, "contact_front_append")) {
+        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_front_append must be 0 or 1");
+        C->front_append = (int)value;
+        graph_invalidate(c);
+        return 0;
+    }
     if (!std::strcmp(key, "contact_fuse_binfilter")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_binfilter must be 0 or 1");
         C->fuse_binfilter = (int)value;

@@ -200,6 +200,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       measured slower on C4, whose contact-zone triangles dominate the prefilter);
  *   "contact_fuse_binfilter" 1 (default): the binning (multi-GPU: the bucket insert) and the
  *                       triangle prefilter run in one launch, side by side;
+ *   "contact_front_append" 0 (default; multi-GPU): a deletion step's surface append runs as its own
+ *                       grid after the one-workgroup front; 1: inside the front;
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0); 2: the
  *                       same, each phase enqueued behind a fixed ≈0.3 ms sleep kernel so it runs

@@ -156,8 +156,10 @@ def test_contact_group_filter_memo_bitexact(world, deck):
     sts = [st for *_, st in parts]
     assert sum(st["candidate_triangles"] for st in sts) == gst["candidate_triangles"]
     assert sum(st["tested_triangles"] for st in sts) < sum(st["live_triangles"] for st in sts)
-    # the A3 insert and prefilter in two launches (contact_fuse_binfilter 0) instead of one
-    parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world, tune={"contact_fuse_binfilter": 0})
+    # the A3 insert and prefilter in two launches (contact_fuse_binfilter 0) instead of one, and the
+    # surface append inside the one-workgroup front (contact_front_append 1) instead of its own grid
+    parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world,
+                               tune={"contact_fuse_binfilter": 0, "contact_front_append": 1})
     _assert_group_equals_single(glob, parts, g, gdel)
     # the memo on rank 0 only: the other ranks mark the motion clock unbounded, so rank 0 skips
     # nothing (and stays exact)
