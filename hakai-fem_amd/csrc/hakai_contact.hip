@@ -195,7 +195,6 @@ struct Contact {
     bool small = false;
     int fuse_small = 1;
     int fuse_binfilter = 1;  // tuning "contact_fuse_binfilter": binning and prefilter in one launch
-    int front_append = 0;    // tuning "contact_front_append" (multi-GPU): the surface append inside k_xr_front
 
     // events and per-node gather over the touched nodes
     long long cap = 0;
@@ -217,12 +216,6 @@ struct Contact {
                                     // 0) and item count (word kItemWord)
     uint2* d_item = nullptr;        // [kCandShards][kItemsPerCand * cshard_cap] (candidate slot, cell << 27 |
                                     // bucket): the cells of a candidate's neighbourhood that its sphere reaches
-    // prefilter memo (TriMemo; large decks, tuning "contact_filter_memo"): per triangle record
-    double2* d_memo = nullptr;      // [n_tri] extreme coordinate, clock at the record
-    uint2* d_memo_meta = nullptr;   // [n_tri] side code, step stamp
-    double* d_memo_clk = nullptr;   // [4] clock by step parity, stamp of the last rebuild
-    int2* d_memo_q = nullptr;       // [kCandShards][memo_qcap] triangles to test in full (j, pair)
-    int memo = 0;                   // -1: on for large decks (not Contact::small); default off (measured)
     double* d_terms = nullptr;      // [4 cap][3]
     // velocity before the first step (initial condition / uploaded), v2/HAKAI_j.jl:233-239
     double* d_velo0 = nullptr;
@@ -319,8 +312,6 @@ constexpr int kShardStride = 32;  // unsigned ints between shard counters
 constexpr int kCandShards = 64;
 constexpr int kItemWord = 1;       // a shard's item counter: with the candidate counter one 64-bit word
 constexpr int kTestWord = 8;       // triangles the shard's prefilter blocks tested in full (stats)
-constexpr int kMemoSpan = 4;       // prefilter memo: live entries per thread in one skip pass
-constexpr int kTestBlocks = 512;   // prefilter memo: grid of the full test over the queue
 constexpr int kItemsPerCand = 16;  // item capacity per candidate slot (a candidate has <= 27)
 constexpr int kFilterBlocks = 2048;  // prefilter grid cap
 
@@ -334,12 +325,10 @@ __device__ __forceinline__ unsigned ld_ctl(const unsigned int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The box array: 12 words per pair (pair_range) and one more, the motion word -- the largest
-// displacement component of a live contact node over the step (the double's bits; multi-GPU:
-// every rank's largest), the clock of the prefilter memo (TriMemo). Min words start at +inf, max
-// words (and the motion word) at 0.
-__host__ __device__ __forceinline__ int box_words(int npairs) { return 12 * npairs + 1; }
-__device__ __forceinline__ bool box_max(int q, int npairs) { return q >= 12 * npairs || ((q % 12) / 3) % 2 == 1; }
+// The box array: 12 words per pair (pair_range), ordered-integer encoded doubles; min words start
+// at +inf, max words at -inf (0).
+__host__ __device__ __forceinline__ int box_words(int npairs) { return 12 * npairs; }
+__device__ __forceinline__ bool box_max(int q) { return ((q % 12) / 3) % 2 == 1; }
 
 // The per-step kernels below are bodies over (workgroup bid of nb): the __global__ wrappers pass
 // blockIdx.x / gridDim.x, and the fused small-deck kernels (one workgroup, "Small decks") run
@@ -355,7 +344,7 @@ __device__ __forceinline__ void reset_body(int bid, int nb, unsigned long long* 
     if (i < kEvShards) evs[i * kShardStride] = 0;
     if (i < kCandShards)
         ccnt[i * kShardStride] = ccnt[i * kShardStride + kTestWord] = ccnt[i * kShardStride + kItemWord] = 0;
-    for (int q = i; q < box_words(npairs); q += nb * blockDim.x) bbox[q] = box_max(q, npairs) ? 0ULL : ~0ULL;
+    for (int q = i; q < box_words(npairs); q += nb * blockDim.x) bbox[q] = box_max(q) ? 0ULL : ~0ULL;
     if (i == 0) {
         ctl[kEv] = 0;
         ctl[kDirty] = force ? 1u : 0u;
@@ -580,7 +569,7 @@ struct AppendIn {
 
 // incremental update, part 2: one block per deleted element, one thread per entry its deletion
 // exposes (triangles, then i-node entries, then j-node entries)
-// (lanes lt of lsz per deleted element: a workgroup, or a wave of the one-workgroup k_xr_front)
+// (lanes lt of lsz per deleted element: a workgroup, or a wave of a one-workgroup kernel)
 __device__ __forceinline__ void append_body(int bid, int nb, unsigned int* ctl, const int* dlist, const AppendIn& A,
                                             const int* del_step, int t, const double* t_rd, int* reg, int* ni_live,
                                             int* nj_live, int* tri_live, int lt, int lsz) {
@@ -631,17 +620,10 @@ struct Seg {
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
-// segment vb / sb, part vb % sb. MOTION (the prefilter memo is on): j-node (triangle node) segments
-// also raise the box array's motion word to their max of |u - u_pre| per component, as the
-// non-negative double's bits (ordered like the values; a NaN is larger than every number and stays).
-// !MOTION with a motion word (a multi-GPU rank without the memo): the word is set to all ones -- a
-// NaN, so the combined clock of any rank that has the memo on stops every skip (no bound from here)
-template <bool MOTION>
+// segment vb / sb, part vb % sb
 __device__ __forceinline__ void bbox_body(int vb, int sb, const StepIn& s, const Seg* segs, const int* reg,
                                           const int* ni_live, const int* nj_live, const int* ni_node,
-                                          const int* nj_node, unsigned long long* bbox,
-                                          unsigned long long* motion) {
-    if (!MOTION && motion && vb == 0 && threadIdx.x == 0) *motion = ~0ULL;
+                                          const int* nj_node, unsigned long long* bbox) {
     const Seg sg = segs[vb / sb];
     if (sg.dup) return;  // another segment's blocks fill its boxes
     const int sub = vb % sb;
@@ -650,43 +632,30 @@ __device__ __forceinline__ void bbox_body(int vb, int sb, const StepIn& s, const
     const int* lst = (side_i ? ni_live : nj_live) + reg[2 * sg.region];
     const int cnt = reg[2 * sg.region + 1];
     const int bd = (int)blockDim.x;
-    const bool mot = MOTION && !side_i;  // (block-uniform)
-    unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL}, dm = 0ULL;
+    unsigned long long mn[3] = {~0ULL, ~0ULL, ~0ULL}, mx[3] = {0ULL, 0ULL, 0ULL};
 #pragma unroll 4
     for (int q = sub * bd + (int)threadIdx.x; q < cnt; q += sb * bd) {  // iterations overlap their loads
-        const int n = node[lst[q]];
         double p[3];
-        pos(s, n, p);
+        pos(s, node[lst[q]], p);
         for (int d = 0; d < 3; ++d) {
             const unsigned long long e = enc(p[d]);
             mn[d] = umin64(mn[d], e);
             mx[d] = umax64(mx[d], e);
-            if (mot)
-                dm = umax64(dm, (unsigned long long)__double_as_longlong(fabs(s.u[3 * n + d] - s.u_pre[3 * n + d])));
         }
     }
-    for (int off = 32; off > 0; off >>= 1) {
+    for (int off = 32; off > 0; off >>= 1)
         for (int d = 0; d < 3; ++d) {
             mn[d] = umin64(mn[d], __shfl_xor(mn[d], off));
             mx[d] = umax64(mx[d], __shfl_xor(mx[d], off));
         }
-        if (mot) dm = umax64(dm, __shfl_xor(dm, off));
-    }
-    __shared__ unsigned long long red[16][7];
+    __shared__ unsigned long long red[16][6];
     const int w = threadIdx.x / 64;
-    if ((threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 0)
         for (int d = 0; d < 3; ++d) {
             red[w][d] = mn[d];
             red[w][3 + d] = mx[d];
         }
-        red[w][6] = dm;
-    }
     __syncthreads();
-    if (threadIdx.x == 6 && mot) {
-        unsigned long long v = red[0][6];
-        for (int ww = 1; ww < bd / 64; ++ww) v = umax64(v, red[ww][6]);
-        if (v != 0ULL) atomicMax(motion, v);
-    }
     if (threadIdx.x < 6) {
         const int q = threadIdx.x;
         unsigned long long v = red[0][q];
@@ -704,11 +673,10 @@ __device__ __forceinline__ void bbox_body(int vb, int sb, const StepIn& s, const
     }
 }
 
-template <bool MOTION>
 __global__ __launch_bounds__(kB) void k_ct_bbox(StepIn s, const Seg* segs, const int* reg, const int* ni_live,
                                                 const int* nj_live, const int* ni_node, const int* nj_node,
-                                                unsigned long long* bbox, int sb, unsigned long long* motion) {
-    bbox_body<MOTION>(blockIdx.x, sb, s, segs, reg, ni_live, nj_live, ni_node, nj_node, bbox, motion);
+                                                unsigned long long* bbox, int sb) {
+    bbox_body(blockIdx.x, sb, s, segs, reg, ni_live, nj_live, ni_node, nj_node, bbox);
 }
 
 // the hash record of live i-node nd (local id) of pair pr at position p inside the range box r
@@ -980,35 +948,15 @@ __device__ __forceinline__ unsigned reach_mask(const TriRec& T, const double amn
     return mask;
 }
 
-// Prefilter memo (large decks): a triangle the prefilter rejected because all three nodes lay
-// below (above) its pair's range box along axis d records that side, its extreme coordinate E (the
-// largest (smallest) of the three along d) and the motion clock S0; a dead element's triangle records
-// that. The clock S advances every step by the box array's motion word -- no live triangle node moved
-// further along any axis since the previous step -- so no node of the triangle moved more than
-// S - S0 since the record, and while E + (S - S0) + tol < mn[d] (E - (S - S0) - tol > mx[d]) for the
-// current range box the full test would reject it again: it is skipped without loading its element,
-// nodes and positions. tol covers the rounding of positions, clock sums and the comparison (relative
-// 1e-10 and half an ulp of S per step since the record). The candidates are exactly the full test's.
-// The clock restarts (and every older record is void) on full-rebuild steps.
-struct TriMemo {
-    const unsigned int* ctl;          // kSeq (step stamp, its parity picks the clock slot), kDirty
-    double* clock;                    // [2] S by step parity; [2] as unsigned: kSeq of the last rebuild
-    double2* rec;                     // per triangle (j): E, S0 (null: memo off)
-    uint2* meta;                      // per triangle: code (2d + side (1: above), 6 dead, else none), kSeq
-    const unsigned long long* motion;  // the box array's motion word
-};
-constexpr unsigned kMemoDead = 6u;
-
 // The full prefilter test (:2374-2411) of live triangle j of pair pr with range box r (act: a real
 // entry; every thread of the block calls it): active element, not entirely on one side of the range
 // box along any axis -> candidate record in the block's shard (multi-GPU: a rank's lists hold the
 // triangles of its own elements only) and one search item per cell of its neighbourhood that its
-// sphere can reach (reach_mask); MEMO: the triangle's new record
-template <bool MEMO>
+// sphere can reach (reach_mask)
 __device__ __forceinline__ void tri_test(int bid, const StepIn& s, int j, int pr, const Range& r, bool act,
                                          const int* tri_nodes, const int* tri_ele, const PairParam* par,
                                          unsigned int* ccnt, TriRec* cand, long long cshard_cap, uint2* item,
-                                         const TriMemo& M, unsigned seq, double S, unsigned long long* s_app) {
+                                         unsigned long long* s_app) {
 #pragma clang fp contract(off)
     // every load issued up front (inactive lanes re-read a real entry)
     const int ele = tri_ele[j];
@@ -1024,32 +972,6 @@ __device__ __forceinline__ void tri_test(int bid, const StepIn& s, int j, int pr
     for (int d = 0; d < 3; ++d) {
         keep &= !(p0[d] < r.mn[d] && p1[d] < r.mn[d] && p2[d] < r.mn[d]);
         keep &= !(p0[d] > r.mx[d] && p1[d] > r.mx[d] && p2[d] > r.mx[d]);
-    }
-    if (MEMO && act) {
-        unsigned code = 7u;
-        double E = 0.0;
-        if (fl != 1) {
-            code = kMemoDead;
-        } else if (!keep) {  // the side with the widest gap
-            double best = 0.0;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                const double hi = fmax(fmax(p0[d], p1[d]), p2[d]), lo = fmin(fmin(p0[d], p1[d]), p2[d]);
-                const double gb = r.mn[d] - hi, ga = lo - r.mx[d];
-                if (gb > best) {
-                    best = gb;
-                    code = 2u * d;
-                    E = hi;
-                }
-                if (ga > best) {
-                    best = ga;
-                    code = 2u * d + 1u;
-                    E = lo;
-                }
-            }
-        }
-        M.meta[j] = make_uint2(code, seq);
-        if (code < kMemoDead) M.rec[j] = make_double2(E, S);
     }
     TriRec T;
     unsigned mask = 0u;
@@ -1104,8 +1026,7 @@ __device__ __forceinline__ void tri_filter_body(int bid, int nb, const StepIn& s
         const bool act = q < n && !r.empty;
         const unsigned long long m = __ballot(act);
         if ((tid & 63) == 0 && m) atomicAdd(tested, (unsigned)__popcll(m));
-        tri_test<false>(bid, s, j, pr, r, act, tri_nodes, tri_ele, par, ccnt, cand, cshard_cap, item, TriMemo{}, 0u,
-                        0.0, s_app);
+        tri_test(bid, s, j, pr, r, act, tri_nodes, tri_ele, par, ccnt, cand, cshard_cap, item, s_app);
     }
 }
 
@@ -1116,109 +1037,6 @@ __global__ __launch_bounds__(kB) void k_ct_tri_filter(StepIn s, const int* tri_c
                                                       uint2* item) {
     tri_filter_body(blockIdx.x, gridDim.x, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par, bbox, ccnt, cand,
                     cshard_cap, item);
-}
-
-// With the memo the prefilter is two launches. k_ct_tri_memo: kMemoSpan live entries per thread
-// (live entry; its pair, code and record; the pair box -- three round trips, no element or node
-// data) -> the triangles its records do not settle, (j, pair) into the to-test queue of the block's
-// shard (word kTestWord of the shard's counter line: one atomic per block iteration); its
-// workgroup 0 advances the clock. k_ct_tri_test: the full test of every queued triangle, spread
-// evenly over its grid (the queue holds about a tenth of the live triangles on C4, clustered
-// around the contact zone; in one launch the zone's blocks would test theirs one after the other).
-__global__ __launch_bounds__(kB) void k_ct_tri_memo(const int* tri_cnt, const int* tri_live, const int* tri_pair,
-                                                    const unsigned long long* bbox, unsigned int* ccnt, int2* queue,
-                                                    long long qcap, TriMemo M) {
-#pragma clang fp contract(off)
-    const int n = *tri_cnt;
-    const int bid = (int)blockIdx.x, nb = (int)gridDim.x, tid = (int)threadIdx.x;
-    __shared__ int2 s_list[kMemoSpan * kB];
-    __shared__ unsigned s_nl, s_base;
-    const unsigned seq = ld_ctl(&M.ctl[kSeq]);
-    const bool fresh = ld_ctl(&M.ctl[kDirty]) != 0u;
-    double S = 0.0;
-    unsigned since_rb = 0u;
-    if (!fresh) {
-        S = M.clock[(seq - 1u) & 1u] + __longlong_as_double((long long)*M.motion);
-        since_rb = seq - reinterpret_cast<const unsigned*>(M.clock + 2)[0];
-    }
-    if (bid == 0 && tid == 0) {
-        M.clock[seq & 1u] = S;
-        if (fresh) reinterpret_cast<unsigned*>(M.clock + 2)[0] = seq;
-    }
-    const int shard = bid % kCandShards;
-    for (int q0 = bid * kMemoSpan * kB; q0 < n; q0 += nb * kMemoSpan * kB) {  // block-uniform trip count
-        if (tid == 0) s_nl = 0u;
-        __syncthreads();
-        // every load of the pass issued before any test (three round trips for the kMemoSpan entries)
-        int jj[kMemoSpan], pp[kMemoSpan];
-        uint2 mt[kMemoSpan];
-        double2 e[kMemoSpan];
-#pragma unroll
-        for (int k = 0; k < kMemoSpan; ++k) {
-            const int q = q0 + k * kB + tid;
-            jj[k] = tri_live[q < n ? q : n - 1];
-        }
-#pragma unroll
-        for (int k = 0; k < kMemoSpan; ++k) {
-            pp[k] = tri_pair[jj[k]];
-            mt[k] = make_uint2(~0u, 0u);
-            e[k] = make_double2(0.0, 0.0);
-            if (!fresh) {
-                mt[k] = M.meta[jj[k]];
-                e[k] = M.rec[jj[k]];  // (with the code; unused unless a side record)
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kMemoSpan; ++k) {
-            const Range r = pair_range(bbox + 12 * pp[k]);
-            bool skip = false;
-            if (mt[k].x <= kMemoDead && seq - mt[k].y <= since_rb) {  // a record of this clock epoch
-                const unsigned d = mt[k].x >> 1;
-                const double mv = S - e[k].y;
-                const double tol = mv + 1e-10 * (1.0 + fabs(e[k].x) + mv) + (double)(seq - mt[k].y) * 2.3e-16 * S;
-                const double lo = d == 0 ? r.mn[0] : (d == 1 ? r.mn[1] : r.mn[2]);  // (no dynamic index:
-                const double hi = d == 0 ? r.mx[0] : (d == 1 ? r.mx[1] : r.mx[2]);  //  r stays in registers)
-                skip = mt[k].x == kMemoDead || ((mt[k].x & 1u) ? e[k].x - tol > hi : e[k].x + tol < lo);
-            }
-            // to the block's list: one LDS atomic per wave
-            const bool push = q0 + k * kB + tid < n && !r.empty && !skip;
-            const unsigned long long m = __ballot(push);
-            const int lane = tid & 63;
-            const int leader = m ? __ffsll((long long)m) - 1 : 0;
-            unsigned base = 0;
-            if (m && lane == leader) base = atomicAdd(&s_nl, (unsigned)__popcll(m));
-            base = __shfl(base, leader);
-            if (push) s_list[base + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL))] = make_int2(jj[k], pp[k]);
-        }
-        __syncthreads();
-        const unsigned nl = s_nl;
-        if (tid == 0) s_base = nl ? atomicAdd(&ccnt[shard * kShardStride + kTestWord], nl) : 0u;
-        __syncthreads();
-        int2* out = queue + (long long)shard * qcap;
-        for (unsigned i = (unsigned)tid; i < nl; i += kB)
-            if ((long long)(s_base + i) < qcap) out[s_base + i] = s_list[i];  // (qcap: a whole pass fits)
-        __syncthreads();  // (s_nl, s_list reused)
-    }
-}
-
-__global__ __launch_bounds__(kB) void k_ct_tri_test(StepIn s, const int* tri_nodes, const int* tri_ele,
-                                                    const PairParam* par, const unsigned long long* bbox,
-                                                    unsigned int* ccnt, TriRec* cand, long long cshard_cap,
-                                                    uint2* item, const int2* queue, long long qcap, TriMemo M) {
-    __shared__ unsigned s_pre[68];
-    __shared__ unsigned long long s_app[2];
-    const long long tot = shard_scan(ccnt + kTestWord, qcap, s_pre);
-    const unsigned seq = ld_ctl(&M.ctl[kSeq]);
-    const double S = M.clock[seq & 1u];  // (k_ct_tri_memo's)
-    const int bid = (int)blockIdx.x;
-    for (long long e0 = (long long)bid * kB; e0 < tot; e0 += (long long)gridDim.x * kB) {  // block-uniform
-        const long long e = e0 + threadIdx.x;
-        const bool act = e < tot;
-        const int2 jp = queue[shard_slot(s_pre, qcap, act ? e : tot - 1)];
-        const Range r = pair_range(bbox + 12 * jp.y);
-        tri_test<true>(bid, s, jp.x, jp.y, r, act, tri_nodes, tri_ele, par, ccnt, cand, cshard_cap, item, M, seq, S,
-                       s_app);
-    }
 }
 
 // events of one thread, kept in registers and appended with one atomic per wave (a same-address
@@ -1946,16 +1764,15 @@ __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long 
 
 // A1 of a step without a full rebuild (multi-GPU), ONE 1024-thread workgroup: k_ct_reset's share of
 // the phase (event and candidate counters, this step's partial box words and bin block header, the
-// bucket-head sequence), every rank's deletion records into the global deletion steps and the
-// deletion list, and the surface append (a wave per deleted element). A rank's block that is full
-// (a peer out of step) is unpacked too. The previous step's touched forces and the term counter are
+// bucket-head sequence), and every rank's deletion records into the global deletion steps and the
+// deletion list; k_ct_append follows with a full grid (in this workgroup, a wave per deleted
+// element, the append took 35-63 µs on C4's deletion steps against 15-18 µs for the grid). A rank's
+// block that is full (a peer out of step) is unpacked too. The previous step's touched forces and the term counter are
 // phase B's (k_ct_count_g), the touched counter the previous k_ct_sum's.
 __global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del,
                                                    long long nE_g, int* poison, int t, int* xctl, int* hc,
                                                    unsigned int* ctl, int* dlist, unsigned long long* bbox,
-                                                   int npairs, unsigned int* evs, unsigned int* ccnt, int* zero_hdr,
-                                                   AppendIn A, int* reg, int* ni_live, int* nj_live, int* tri_live,
-                                                   int with_lists) {
+                                                   int npairs, unsigned int* evs, unsigned int* ccnt, int* zero_hdr) {
     __shared__ int4 s_h[kMaxXRanks];
     load_hdrs(xb, nr, s_h);
     x_counts(s_h, nr, 0, xctl, hc);
@@ -1963,7 +1780,7 @@ __global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long l
     if (tid < kEvShards) evs[tid * kShardStride] = 0;
     if (tid < kCandShards)
         ccnt[tid * kShardStride] = ccnt[tid * kShardStride + kTestWord] = ccnt[tid * kShardStride + kItemWord] = 0;
-    for (int q = tid; q < box_words(npairs); q += bd) bbox[q] = box_max(q, npairs) ? 0ULL : ~0ULL;
+    for (int q = tid; q < box_words(npairs); q += bd) bbox[q] = box_max(q) ? 0ULL : ~0ULL;
     if (tid < 2) zero_hdr[tid] = 0;
     if (tid == 0) {
         int mx = 0;
@@ -2004,16 +1821,13 @@ __global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long l
             }
         }
     }
-    __syncthreads();
-    if (with_lists)
-        append_body(tid >> 6, bd >> 6, ctl, dlist, A, g_del, t, nullptr, reg, ni_live, nj_live, tri_live, tid & 63, 64);
 }
 
 // pair boxes of all ranks: min of the min words, max of the max words (exact, order-free). RCCL
 // all-reduces with MIN: the max words travel complemented (k_xr_boxflip before and after).
 __global__ void k_xr_boxflip(unsigned long long* bb, int npairs) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < box_words(npairs) && box_max(q, npairs)) bb[q] = ~bb[q];
+    if (q < box_words(npairs) && box_max(q)) bb[q] = ~bb[q];
 }
 struct XBox {
     const unsigned long long* p[kMaxXRanks];
@@ -2021,7 +1835,7 @@ struct XBox {
 __global__ void k_xr_boxcomb(XBox xb, int nr, int npairs, unsigned long long* out) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= box_words(npairs)) return;
-    const bool mx = box_max(q, npairs);
+    const bool mx = box_max(q);
     unsigned long long v = xb.p[0][q];
     for (int r = 1; r < nr; ++r) {
         const unsigned long long w = xb.p[r][q];
@@ -2046,7 +1860,7 @@ __global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, int ns
     const unsigned long long* bbox = boxg;
     if (nxb > 0) {
         for (int q = (int)threadIdx.x; q < box_words(npairs); q += kB) {
-            const bool mx = box_max(q, npairs);
+            const bool mx = box_max(q);
             unsigned long long v = xb.p[0][q];
             for (int r = 1; r < nxb; ++r) {
                 const unsigned long long w = xb.p[r][q];
@@ -2305,7 +2119,6 @@ void contact_destroy(hakai_ctx* c) {
     dfree(C->d_bbox); dfree(C->d_ctl); dfree(C->d_evs); dfree(C->d_ev_nodes); dfree(C->d_ev_f); dfree(C->d_cnt); dfree(C->d_tpos);
     dfree(C->d_touched[0]); dfree(C->d_touched[1]); dfree(C->d_toff); dfree(C->d_tcnt); if (C->d_cand) (void)hipFree(C->d_cand);
     dfree(C->d_terms); dfree(C->d_velo0); dfree(C->d_ccnt); dfree(C->d_item);
-    dfree(C->d_memo); dfree(C->d_memo_meta); dfree(C->d_memo_clk); dfree(C->d_memo_q);
     if (Xrank* X = C->xr) {
         (void)hipDeviceSynchronize();  // in-process peers may still read this rank's blocks
         dfree(X->d_l2g); dfree(X->d_g2l); dfree(X->g_mass); dfree(X->g_del); dfree(X->d_last_del);
@@ -2474,52 +2287,17 @@ int contact_post_step(hakai_ctx* c) {
 static int search(hakai_ctx* c, const StepIn& in, bool fused);
 static void tri_search(hakai_ctx* c, const StepIn& in);
 
-static bool memo_on(const Contact* C) { return (C->memo < 0 ? !C->small : C->memo != 0) && C->d_memo; }
-
-static TriMemo tri_memo(const Contact* C, const unsigned long long* bbox) {
-    TriMemo M{};
-    M.ctl = C->d_ctl;
-    if (!memo_on(C)) return M;
-    M.clock = C->d_memo_clk;
-    M.rec = C->d_memo;
-    M.meta = C->d_memo_meta;
-    M.motion = bbox + 12 * C->npairs;
-    return M;
-}
-
-// prefilter grid: one live triangle per thread, or kMemoSpan with the memo (size_cand covers both)
+// prefilter grid: one live triangle per thread
 static unsigned filter_grid(const Contact* C) {
-    const int per = memo_on(C) ? kMemoSpan * kB : kB;
-    return (unsigned)std::max(1, std::min((C->n_tri + per - 1) / per, kFilterBlocks));
+    return (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kFilterBlocks));
 }
 
-// the to-test queue of one shard (k_ct_tri_memo): every block iteration of the shard's blocks in a
-// pass over the largest live list
-static long long memo_qcap(const Contact* C) {
-    const long long per = (long long)kMemoSpan * kB, n = std::max<long long>(C->n_tri, 1);
-    const long long g = std::max<long long>(1, std::min<long long>((n + per - 1) / per, kFilterBlocks));
-    return (g + kCandShards - 1) / kCandShards * ((n + g * per - 1) / (g * per)) * per;
-}
-
-// the triangle prefilter against the (combined) pair boxes bbox: one launch, or the memo's two
+// the triangle prefilter against the (combined) pair boxes bbox, as its own launch
 static void tri_prefilter(hakai_ctx* c, const StepIn& in, const unsigned long long* bbox) {
     Contact* C = c->contact;
-    hipStream_t s = c->stream;
-    const int* tri_cnt = C->d_reg + 2 * C->tri_reg + 1;
-    uint2* item = C->small ? nullptr : C->d_item;
-    if (!memo_on(C)) {
-        hipLaunchKernelGGL(k_ct_tri_filter, dim3(filter_grid(C)), dim3(kB), 0, s, in, tri_cnt, C->d_tri_live,
-                           C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, bbox, C->d_ccnt, (TriRec*)C->d_cand,
-                           C->cshard_cap, item);
-        return;
-    }
-    const TriMemo M = tri_memo(C, bbox);
-    const long long qcap = memo_qcap(C);
-    hipLaunchKernelGGL(k_ct_tri_memo, dim3(filter_grid(C)), dim3(kB), 0, s, tri_cnt, C->d_tri_live, C->d_tri_pair, bbox,
-                       C->d_ccnt, C->d_memo_q, qcap, M);
-    const unsigned gt = (unsigned)std::max(1, std::min((C->n_tri + kB - 1) / kB, kTestBlocks));
-    hipLaunchKernelGGL(k_ct_tri_test, dim3(gt), dim3(kB), 0, s, in, C->d_tri_nodes, C->d_tri_ele, C->d_par, bbox,
-                       C->d_ccnt, (TriRec*)C->d_cand, C->cshard_cap, item, C->d_memo_q, qcap, M);
+    hipLaunchKernelGGL(k_ct_tri_filter, dim3(filter_grid(C)), dim3(kB), 0, c->stream, in, C->d_reg + 2 * C->tri_reg + 1,
+                       C->d_tri_live, C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, C->d_par, bbox, C->d_ccnt,
+                       (TriRec*)C->d_cand, C->cshard_cap, C->small ? nullptr : C->d_item);
 }
 
 static StepIn step_in(hakai_ctx* c, double t, double d_time) {
@@ -2580,14 +2358,11 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                            (int)C->nE, C->d_dlist, A, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live,
                            C->ntile > 0 ? 1 : 0);
     } else if (X && !rebuild) {
-        // multi-GPU: the reset's share and every rank's deletions in one workgroup; the surface append
-        // after it with a full grid (one workgroup took 35-63 us on C4's deletion steps, against
-        // 15-18 for the grid, and ~4 us more on steps without deletions)
+        // multi-GPU: the reset's share and every rank's deletions in one workgroup, then the append
         hipLaunchKernelGGL(k_xr_front, dim3(1), dim3(1024), 0, s, xb, X->nranks, X->d_eoff, X->cap[0], X->g_del,
                            X->nE_g, c->d_poison, in.t, X->d_xctl, X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks,
-                           C->d_ctl, C->d_dlist, bbox, C->npairs, C->d_evs, C->d_ccnt, (int*)X->d_send[1][X->par_a], A,
-                           C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live, C->front_append && C->ntile > 0 ? 1 : 0);
-        if (!C->front_append && C->ntile > 0)
+                           C->d_ctl, C->d_dlist, bbox, C->npairs, C->d_evs, C->d_ccnt, (int*)X->d_send[1][X->par_a]);
+        if (C->ntile > 0)
             hipLaunchKernelGGL(k_ct_append, dim3(256), dim3(64), 0, s, C->d_ctl, C->d_dlist, A, del_step, in.t,
                                c->g_trd, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_tri_live);
     } else {
@@ -2629,9 +2404,8 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
     C->last_t = in.t;
     const Seg* sg = (const Seg*)C->d_seg;
     if (C->nseg > 0)
-        hipLaunchKernelGGL((memo_on(C) ? k_ct_bbox<true> : k_ct_bbox<false>), dim3(C->nseg * C->g_box), dim3(kB), 0, s,
-                           in, sg, C->d_reg, C->d_ni_live, C->d_nj_live, C->d_ni_node, C->d_nj_node, bbox, C->g_box,
-                           memo_on(C) || X ? bbox + 12 * C->npairs : nullptr);  // (multi-GPU: a max over ranks)
+        hipLaunchKernelGGL(k_ct_bbox, dim3(C->nseg * C->g_box), dim3(kB), 0, s, in, sg, C->d_reg, C->d_ni_live,
+                           C->d_nj_live, C->d_ni_node, C->d_nj_node, bbox, C->g_box);
     HIPCHK(hipGetLastError());
     if (X) {
         HIPCHK(hipEventRecord(X->ev_box[X->par_a], s));
@@ -2648,9 +2422,8 @@ static int search(hakai_ctx* c, const StepIn& in, bool fused) {
     const int tsel = C->tsel;
     const unsigned gfilt = filter_grid(C);
     // the binning and the triangle prefilter in one launch (both need only the boxes; their
-    // workgroups run side by side): small decks, and larger ones unless tuned off. Not with the
-    // memo, whose prefilter is two launches.
-    const bool fused_mid = (fused || C->fuse_binfilter) && C->nseg > 0 && C->n_tri > 0 && !memo_on(C);
+    // workgroups run side by side): small decks, and larger ones unless tuned off
+    const bool fused_mid = (fused || C->fuse_binfilter) && C->nseg > 0 && C->n_tri > 0;
     const Seg* sg = (const Seg*)C->d_seg;
     if (C->nseg > 0) {
         if (fused_mid) {
@@ -2761,7 +2534,7 @@ static int xr_a3(hakai_ctx* c, double d_time) {
     const unsigned gb = (unsigned)std::min<long long>(std::max<long long>((X->cap[1] + kB - 1) / kB, 1), 128);
     int* hc = X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks;
     StepIn in = step_in(c, X->t_a, d_time);
-    if (C->n_tri > 0 && C->fuse_binfilter && !memo_on(C)) {  // insert and prefilter side by side
+    if (C->n_tri > 0 && C->fuse_binfilter) {  // insert and prefilter side by side
         hipLaunchKernelGGL(k_xr_insfilter, dim3(gb * (unsigned)X->nranks + filter_grid(C)), dim3(kB), 0, s, xb,
                            X->nranks, X->cap[1], C->d_par, C->d_ctl, C->d_head, C->d_blist, C->d_bvel, c->d_poison,
                            X->t_a, X->d_xctl, hc, (int)gb, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
@@ -2892,11 +2665,8 @@ void contact_graph_advance(hakai_ctx* c, double t_last) {
 // triangles fit one pass of the grid cannot overflow a shard -- as the unsharded n_tri-sized
 // buffer could not.
 static void size_cand(Contact* C, long long total) {
-    long long one_pass = 0;
-    for (const long long per : {(long long)kB, (long long)kMemoSpan * kB}) {  // without and with the memo
-        const long long blocks = std::max<long long>(1, std::min<long long>((C->n_tri + per - 1) / per, kFilterBlocks));
-        one_pass = std::max(one_pass, (blocks + kCandShards - 1) / kCandShards * per);
-    }
+    const long long blocks = std::max<long long>(1, std::min<long long>((C->n_tri + kB - 1) / kB, kFilterBlocks));
+    const long long one_pass = (blocks + kCandShards - 1) / kCandShards * kB;
     C->cshard_cap = std::max<long long>((total + kCandShards - 1) / kCandShards, one_pass);
     C->cand_cap = C->cshard_cap * kCandShards;
 }
@@ -2904,12 +2674,6 @@ static void size_cand(Contact* C, long long total) {
 int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     Contact* C = c->contact;
     if (!C) return fail(HAKAI_ERR_STATE, "%s before set_contact", key);
-    if (!std::strcmp(key, "contact_front_append")) {
-        if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_front_append must be 0 or 1");
-        C->front_append = (int)value;
-        graph_invalidate(c);
-        return 0;
-    }
     if (!std::strcmp(key, "contact_fuse_binfilter")) {
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_binfilter must be 0 or 1");
         C->fuse_binfilter = (int)value;
@@ -2919,13 +2683,6 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
     if (!std::strcmp(key, "contact_fuse_small")) {  // small decks: fused single-workgroup phases
         if (value != 0 && value != 1) return fail(HAKAI_ERR_ARG, "contact_fuse_small must be 0 or 1");
         C->fuse_small = (int)value;
-        graph_invalidate(c);
-        return 0;
-    }
-    if (!std::strcmp(key, "contact_filter_memo")) {  // prefilter memo (TriMemo); auto: large decks
-        if (value < -1 || value > 1) return fail(HAKAI_ERR_ARG, "contact_filter_memo must be -1 (auto), 0 or 1");
-        C->memo = (int)value;
-        C->force_rebuild = true;  // (the clock did not run while it was off)
         graph_invalidate(c);
         return 0;
     }
@@ -3431,14 +3188,6 @@ int contact_setup(hakai_ctx* c, const HostMesh& H, int32_t contact_flag, const i
     HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
     HIPCHK(dalloc(&C->d_item, (size_t)kItemsPerCand * C->cand_cap));
     if (C->htot >= (1 << 27)) return fail(HAKAI_ERR_ARG, "contact: %d hash buckets (search items hold 27 bits)", C->htot);
-    if (C->n_tri > 0) {
-        HIPCHK(dalloc(&C->d_memo, (size_t)C->n_tri));
-        HIPCHK(dalloc(&C->d_memo_meta, (size_t)C->n_tri));
-        HIPCHK(hipMemsetAsync(C->d_memo_meta, 0xFF, (size_t)C->n_tri * sizeof(uint2), s));  // no record
-        HIPCHK(dalloc(&C->d_memo_clk, 4));
-        HIPCHK(dalloc(&C->d_memo_q, (size_t)kCandShards * memo_qcap(C)));
-        HIPCHK(hipMemsetAsync(C->d_memo_clk, 0, 4 * sizeof(double), s));
-    }
     HIPCHK(dalloc(&C->d_terms, 12 * (size_t)C->cap));
     HIPCHK(dalloc(&C->d_velo0, 3 * (size_t)c->nN));
     HIPCHK(dalloc(&c->d_fext, 3 * (size_t)c->nN));
@@ -3695,7 +3444,7 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
         if (cap > 8) stats[8] = bytes;
     }
     if (cap > 9) stats[9] = C->htot;  // hash-grid buckets over all pairs
-    if (cap > 10) {  // live triangles the prefilter tested in full (memo: not skipped)
+    if (cap > 10) {  // live triangles the prefilter tested in full (those with a non-empty range box)
         std::vector<unsigned int> cc((size_t)kCandShards * kShardStride);
         HIPCHK(hipMemcpy(cc.data(), C->d_ccnt, cc.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
         long long nt = 0;

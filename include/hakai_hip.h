@@ -194,14 +194,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       contact, records per rank block of each per-step exchange (they also grow
  *                       on their own; call on every rank between steps);
  *   "contact_fuse_small" 1 (default): decks of <= 2^16 elements run fused single-workgroup phases;
- *   "contact_filter_memo" 0 (default), 1, or -1 (on for decks that are not small): the triangle
- *                       prefilter skips a triangle it rejected before while the nodes' accumulated
- *                       motion cannot have brought it to its pair's range box (same candidates;
- *                       measured slower on C4, whose contact-zone triangles dominate the prefilter);
  *   "contact_fuse_binfilter" 1 (default): the binning (multi-GPU: the bucket insert) and the
  *                       triangle prefilter run in one launch, side by side;
- *   "contact_front_append" 0 (default; multi-GPU): a deletion step's surface append runs as its own
- *                       grid after the one-workgroup front; 1: inside the front;
  *   "group_serial"      1 on rank 0 of a hakai_step_group: each rank's phase is drained before the
  *                       next rank's (uncontended per-rank timings on one GPU; default 0); 2: the
  *                       same, each phase enqueued behind a fixed ≈0.3 ms sleep kernel so it runs
@@ -254,8 +248,8 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
  * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
  * [7] contact-zone nodes all ranks binned in the last step, [8] bytes of one rank's per-step
  * exchange blocks at their capacities (hakai_set_contact_global); [9] hash-grid buckets of all pairs;
- * [10] live triangles the prefilter tested in full in the last step (the rest its memo skipped;
- * multi-GPU: this rank's). */
+ * [10] live triangles the prefilter tested in full in the last step (those whose pair has a
+ * non-empty range box; multi-GPU: this rank's). */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);

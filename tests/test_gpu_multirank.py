@@ -75,7 +75,7 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key, tune=None, rank_tune=None):
+def _run_contact_group(glob, world, n_steps, key, tune=None):
     """Range-partitioned contact model on an in-process group (hakai_set_contact_global): each rank
     searches the triangles of its elements against the binned contact nodes of every rank."""
     gdiag, _ = glob.lumped_mass()
@@ -87,7 +87,7 @@ def _run_contact_group(glob, world, n_steps, key, tune=None, rank_tune=None):
         sv.comm_init_local(r, world, key)
         sv.set_interface(*iface)
         sv.set_contact_global(glob, l2g, off, gdiag)
-        for k, v in list((tune or {}).items()) + list(((rank_tune or {}).get(r) or {}).items()):
+        for k, v in (tune or {}).items():
             sv.set_tuning(k, v)
         svs.append(sv)
     step_group(svs, 1, n_steps)
@@ -135,10 +135,9 @@ def test_contact_group_x_slabs_bitexact(world):
 
 
 @pytest.mark.parametrize("world,deck", [(2, "x_slabs"), (3, "deletion")])
-def test_contact_group_filter_memo_bitexact(world, deck):
-    """The prefilter memo on every rank (its clock runs on the all-ranks motion word: a rank's
-    triangles have nodes other ranks own): bit-identical to one context without the memo, the same
-    candidate triangles, fewer triangles tested in full."""
+def test_contact_group_unfused_insert_bitexact(world, deck):
+    """The A3 bucket insert and the triangle prefilter in two launches (contact_fuse_binfilter 0)
+    instead of one (k_xr_insfilter): bit-identical to one context, the same candidate triangles."""
     from hakai import mesh
     if deck == "x_slabs":
         glob = mesh.two_body_model(plate=(8, 8, 2), impactor=(4, 4, 3), v=-3e5, d_time=2e-8, n_steps=400,
@@ -146,27 +145,15 @@ def test_contact_group_filter_memo_bitexact(world, deck):
     else:
         glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
     with Solver(glob) as sv:
-        sv.set_tuning("contact_filter_memo", 0)
         sv.step(1, glob.n_steps)
         g = sv.download()
         gdel = [tuple(x) for x in sv.deleted()]
         gst = sv.contact_stats()
-    parts = _run_contact_group(glob, world, glob.n_steps, key=370 + world, tune={"contact_filter_memo": 1})
+    parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world, tune={"contact_fuse_binfilter": 0})
     _assert_group_equals_single(glob, parts, g, gdel)
     sts = [st for *_, st in parts]
     assert sum(st["candidate_triangles"] for st in sts) == gst["candidate_triangles"]
-    assert sum(st["tested_triangles"] for st in sts) < sum(st["live_triangles"] for st in sts)
-    # the A3 insert and prefilter in two launches (contact_fuse_binfilter 0) instead of one, and the
-    # surface append inside the one-workgroup front (contact_front_append 1) instead of its own grid
-    parts = _run_contact_group(glob, world, glob.n_steps, key=380 + world,
-                               tune={"contact_fuse_binfilter": 0, "contact_front_append": 1})
-    _assert_group_equals_single(glob, parts, g, gdel)
-    # the memo on rank 0 only: the other ranks mark the motion clock unbounded, so rank 0 skips
-    # nothing (and stays exact)
-    parts = _run_contact_group(glob, world, glob.n_steps, key=390 + world, rank_tune={0: {"contact_filter_memo": 1}})
-    _assert_group_equals_single(glob, parts, g, gdel)
-    st0 = parts[0][4]
-    assert st0["tested_triangles"] > 0 or st0["live_triangles"] == 0
+    assert sum(st["tested_triangles"] for st in sts) <= sum(st["live_triangles"] for st in sts)
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
