@@ -770,28 +770,9 @@ __device__ __forceinline__ unsigned block_append(unsigned int* ctr, bool pred, u
     return s_ctl[1] + off + (unsigned)__popcll(m & ((1ULL << lane) - 1ULL));
 }
 
-// The same for a count per thread (every thread of the block calls it): the thread's first slot
-__device__ __forceinline__ unsigned block_append_n(unsigned int* ctr, unsigned cnt, unsigned* s_ctl) {
-    if (threadIdx.x == 0) s_ctl[0] = 0;
-    __syncthreads();
-    const int lane = (int)(threadIdx.x & 63);
-    unsigned x = cnt;  // wave inclusive scan
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    unsigned woff = 0;
-    const unsigned wtot = __shfl(x, 63);
-    if (lane == 63 && wtot) woff = atomicAdd(&s_ctl[0], wtot);
-    woff = __shfl(woff, 63);
-    __syncthreads();
-    if (threadIdx.x == 0) s_ctl[1] = s_ctl[0] ? atomicAdd(ctr, s_ctl[0]) : 0u;
-    __syncthreads();
-    return s_ctl[1] + woff + x - cnt;
-}
-
 // The same for two counts per thread packed in one 64-bit value (low and high 32 bits; a block's
-// sums stay below 2^32 each), appended to one 64-bit counter: the thread's first slots, packed
+// sums stay below 2^32 each), appended to one 64-bit counter with one atomic per block: the
+// thread's first slots, packed (every thread of the block calls it)
 __device__ __forceinline__ unsigned long long block_append2(unsigned long long* ctr, unsigned long long v,
                                                             unsigned long long* s_ctl) {
     if (threadIdx.x == 0) s_ctl[0] = 0;
