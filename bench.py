@@ -26,8 +26,10 @@ Workloads (BASELINE.json):
                    (2 M hex each, the same velocity gradient, preload and plastic share as N = 1),
                    so value_N / (N x value_1) compares the same per-GPU work; N = 8 is 16 M hex.
                    The line also carries `config.c5_strong`: BASELINE config 5, the C5 bar
-                   100x100x1600 (16 M hex) split over the same N ranks, timed in the same run, with
-                   its ratio to the committed one-GPU C5 line (profiles/r03_bench_strong_n1_c5.json).
+                   100x100x1600 (16 M hex) split over the same N ranks, timed in the same run, and the
+                   same bar on rank 0's GPU alone right after it (`n1_reference`), so `speedup_vs_n1`
+                   is a same-run ratio. Every rank builds only its own slab (hakai.dist.bar_slab);
+                   `setup_s_per_rank` reports mesh + upload and the first (planning) step per rank.
                    --weak-shape c5: 2 M-hex z-slabs of the C5 bar 100x100x(200N) instead.
   --strong         the whole C5 bar 100x100x1600 (16 M hex) split over N as the headline (N = 1
                    holds all 16 M), so value_N / value_1 is the strong-scaling speed-up.
@@ -58,7 +60,6 @@ B_E_ELASTIC = 1576
 B_N = 224                      # compulsory bytes per node per step (whole step)
 B_N_ELEMENT_SIDE = 72          # coord, u, u_pre read by the element kernel, once per node
 C5_LAYERS = 1600               # C5: 100x100x1600
-C5_N1_LINE = os.path.join(ROOT, "profiles", "r03_bench_strong_n1_c5.json")
 
 
 def parse():
@@ -78,6 +79,8 @@ def parse():
     ap.add_argument("--c5-strong", type=int, default=1,
                     help="N > 1 weak: also time BASELINE config 5 (C5 16 M split over the ranks)")
     ap.add_argument("--c5-steps", type=int, default=50)
+    ap.add_argument("--c5-n1-ref", type=int, default=1,
+                    help="N > 1 weak: also time the whole C5 bar on rank 0's GPU alone (speedup_vs_n1 of c5_strong)")
     ap.add_argument("--local-ranks", type=int, default=0,
                     help="rehearsal: the N-rank path as an in-process group of R contexts on one GPU")
     ap.add_argument("--same-slab-ref", type=int, default=1,
@@ -95,6 +98,7 @@ def parse():
     return ap.parse_args()
 
 
+TERM_GRACE_S = 30.0            # launcher: SIGTERM -> SIGKILL grace period for the other ranks
 LAUNCH_KEYS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
 
 
@@ -127,6 +131,7 @@ def launch_ranks(a) -> int:
     argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = [subprocess.Popen(argv, env=dict(os.environ, **e)) for e in envs]
     status = 0
+    kill_at = None               # SIGTERM sent: ranks still alive at this time get SIGKILL
     try:
         while procs:
             for p in list(procs):
@@ -140,6 +145,14 @@ def launch_ranks(a) -> int:
                           file=sys.stderr, flush=True)
                     for q in procs:
                         q.send_signal(signal.SIGTERM)
+                    kill_at = time.monotonic() + TERM_GRACE_S
+            if kill_at is not None and procs and time.monotonic() > kill_at:
+                # a rank stuck in the driver or in an RCCL collective may ignore SIGTERM
+                print(f"bench.py launcher: {len(procs)} rank(s) still alive {TERM_GRACE_S:.0f} s after SIGTERM; "
+                      "killing them", file=sys.stderr, flush=True)
+                for q in procs:
+                    q.kill()
+                kill_at = None
             time.sleep(0.2)
     finally:
         for q in procs:          # only reached on an exception in this loop: never leave ranks behind
@@ -150,39 +163,66 @@ def launch_ranks(a) -> int:
 
 def check_launch(a, world: int, local_world: int) -> None:
     """Rank count and devices must be what --gpus asks for; every mismatch is fatal (never one rank
-    timed silently)."""
+    timed silently). That no two ranks drive one GPU is checked after the rendezvous
+    (check_distinct_devices): a visibility mask may be set per rank by the launcher or be one mask
+    for all ranks, and only the ranks together can tell."""
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
     if world > 1 and os.environ.get("HAKAI_RCCL_SHARED_GPU") != "1":
         import torch
-        n = torch.cuda.device_count()      # counts devices without initialising the GPU
-        restricted = any(os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
-                                                     "CUDA_VISIBLE_DEVICES"))
-        if n < 1 or (n < local_world and not restricted):
-            raise SystemExit(f"bench.py: {local_world} ranks on this node but {n} visible GPU(s); ranks would share "
-                             "a device (set HAKAI_RCCL_SHARED_GPU=1 only for a one-GPU rehearsal)")
+        if torch.cuda.device_count() < 1:  # counts devices without initialising the GPU
+            raise SystemExit("bench.py: no visible GPU")
+
+
+def device_identity(device: int) -> str:
+    import torch
+    p = torch.cuda.get_device_properties(device)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x} {p.uuid}"
+
+
+def check_distinct_devices(store, rank: int, world: int, device: int) -> None:
+    """Every rank publishes the PCI address of its GPU in the rendezvous store and reads the others':
+    two ranks on one GPU (e.g. one global HIP_VISIBLE_DEVICES=0 for --gpus 2) stop here with a clear
+    message instead of in RCCL's duplicate-GPU check. HAKAI_RCCL_SHARED_GPU=1 (one-GPU rehearsals
+    over sockets) declares the sharing deliberate."""
+    me = device_identity(device)
+    store.set(f"hakai_bench_dev/{rank}", me)
+    ids = [store.get(f"hakai_bench_dev/{r}").decode() for r in range(world)]
+    if os.environ.get("HAKAI_RCCL_SHARED_GPU") == "1":
+        return
+    dup = [r for r in range(world) if r != rank and ids[r] == me]
+    if dup:
+        raise SystemExit(f"bench.py: rank {rank} and rank(s) {dup} drive the same GPU ({me}); give each rank its "
+                         "own GPU (HIP_VISIBLE_DEVICES per rank, or none), or set HAKAI_RCCL_SHARED_GPU=1 for a "
+                         "one-GPU rehearsal")
+
+
+def _bar_counts(nx, ny, nz):
+    return nx * ny * nz, (nx + 1) * (ny + 1) * (nz + 1)
 
 
 def c5_strong_model(rank, world, layers_override=0):
+    """BASELINE config 5 (the C5 bar 100x100x1600, 16 M hex) split into `world` z-slabs; each rank
+    builds only its own slab (dist.bar_slab, bit-identical to cutting the global bar), so no process
+    ever holds the 16 M-hex host arrays unless world == 1."""
     from hakai import mesh
-    from hakai.dist import slab_partition
+    from hakai.dist import bar_slab
     layers = layers_override or C5_LAYERS
-    glob = mesh.config_c5(layers=layers)
+    ne, nn = _bar_counts(100, 100, layers)
     cfg = {"workload": "C5 100x100x%d elastoplastic impact bar (%d hex), split into %d z-slab(s) (strong scaling)"
-           % (layers, glob.nElement, world), "elements": glob.nElement, "nodes": glob.nNode,
+           % (layers, ne, world), "elements": ne, "nodes": nn,
            "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"
            if world > 1 else "single GPU"}
-    if world == 1:
-        diag, _ = glob.lumped_mass()
-        return glob, diag, None, cfg, 20
-    local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
-    return local, diag, iface, cfg, 20
+    local, diag, iface = bar_slab(100, 100, layers, rank, world, mesh.steel_ductile(), -1e5,
+                                  name=f"C5-100x100x{layers}")
+    return local, diag, (iface if world > 1 else None), cfg, 20
 
 
 def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=False, weak_shape="c3"):
-    """Returns (local Model, local diag_M, interface arrays or None, config dict, preload)."""
+    """Returns (local Model, local diag_M, interface arrays or None, config dict, preload).
+    N > 1: every rank builds its own slab directly (dist.bar_slab), never the global bar."""
     from hakai import mesh
-    from hakai.dist import slab_partition
+    from hakai.dist import bar_slab
     if strong:
         return c5_strong_model(rank, world, layers_override)
     if world == 1 and not dist_path:
@@ -195,19 +235,20 @@ def build_rank_model(rank, world, layers_override=0, dist_path=False, strong=Fal
         return m, diag, None, cfg, 400
     if weak_shape == "c3":
         per = layers_override or 5000
-        glob = mesh.bar_model(20, 20, per * world, mesh.steel_ductile(), lambda z, L: 5e5 * z / per,
-                              name="C3xN")
-        local, diag, iface = slab_partition(glob, rank, world, nx=20, ny=20)
+        ne, nn = _bar_counts(20, 20, per * world)
+        local, diag, iface = bar_slab(20, 20, per * world, rank, world, mesh.steel_ductile(),
+                                      lambda z, L: 5e5 * z / per, name="C3xN")
         cfg = {"workload": "C3 per rank: 20x20x%d elastoplastic tensile bar (steel_Ductile, deletion on, v_z = "
                "5e5 z/%d mm/s), %d z-slabs of 20x20x%d (2 M hex each, the N = 1 workload)"
-               % (per * world, per, world, per), "elements": glob.nElement, "nodes": glob.nNode,
+               % (per * world, per, world, per), "elements": ne, "nodes": nn,
                "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"}
         return local, diag, iface, cfg, 400
     per = layers_override or 200
-    glob = mesh.config_c5(layers=per * world)
-    local, diag, iface = slab_partition(glob, rank, world, nx=100, ny=100)
+    ne, nn = _bar_counts(100, 100, per * world)
+    local, diag, iface = bar_slab(100, 100, per * world, rank, world, mesh.steel_ductile(), -1e5,
+                                  name=f"C5-100x100x{per * world}")
     cfg = {"workload": "C5 family: 100x100x%d elastoplastic impact bar, %d z-slabs of 100x100x%d (2 M hex each)"
-           % (per * world, world, per), "elements": glob.nElement, "nodes": glob.nNode,
+           % (per * world, world, per), "elements": ne, "nodes": nn,
            "partition": "contiguous element ranges (z-slabs), RCCL point-to-point interface exchange"}
     return local, diag, iface, cfg, 20
 
@@ -345,6 +386,52 @@ def sum_over_ranks(x, multi):
     return float(v.item())
 
 
+def gather_floats(x, multi):
+    """x from every rank, in rank order (the value itself on one process)."""
+    if not multi:
+        return [float(x)]
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+    out = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, v)
+    return [float(o.item()) for o in out]
+
+
+def c5_n1_reference(rank, device, exact, steps, multi):
+    """The whole C5 bar on rank 0's GPU alone (no communicator), same preload/warm-up/steps as the
+    N-rank c5_strong run; the other ranks wait at a barrier. Returns the reference dict on rank 0,
+    its value broadcast so every rank can form the ratio."""
+    import torch
+    import torch.distributed as dist
+    res = torch.zeros(3, dtype=torch.float64, device="cuda")
+    if rank == 0:
+        t0 = time.perf_counter()
+        b1 = [c5_strong_model(0, 1, 0)]
+        g1 = Group(b1, [0], 0, 0, 1, device, exact, 2)
+        g1.sync()
+        setup = time.perf_counter() - t0
+        pre = b1[0][4]
+        g1.run(1, pre + 10)
+        g1.sync()
+        e1, el1, _ = timed(g1, pre + 11, steps, False)
+        n1 = active_elements(g1)
+        g1.close()
+        res[0] = n1 * steps / e1 / 1e6
+        res[1] = e1 / steps * 1e3
+        res[2] = el1[0][0] / max(el1[0][1], 1)
+        del b1
+        print(f"bench.py: C5 N = 1 reference on device {device}: setup {setup:.1f} s, "
+              f"{res[1].item():.3f} ms/step", file=sys.stderr, flush=True)
+    if multi:
+        dist.broadcast(res, 0)
+    if res[0].item() <= 0:
+        return None
+    return {"value": round(res[0].item(), 3), "ms_per_step": round(res[1].item(), 4),
+            "element_avg_ms": round(res[2].item(), 4),
+            "source": "timed in this run: the same 16 M bar on rank 0's GPU alone, after the N-rank run"}
+
+
 def active_elements(g):
     return sum(int(sv.download(element_flag=True).element_flag.sum()) for sv in g.svs)
 
@@ -377,18 +464,30 @@ def main():
         # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal) the ranks share them
         device = rank_device(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
         torch.cuda.set_device(device)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        store, _, _ = next(dist.rendezvous("env://", rank, world))
+        check_distinct_devices(store, rank, world, device)
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", device))
     exact = a.element_mode == "exact"
     ids = list(range(R)) if R else [rank]
+    t_setup = time.perf_counter()
     built = [build_rank_model(r, nparts, a.layers, a.dist_path or bool(R), a.strong, a.weak_shape) for r in ids]
     cfg = built[0][3]
     preload = built[0][4] if a.preload < 0 else a.preload
+    t_mesh = time.perf_counter() - t_setup
     g = Group(built, ids, R, rank, world, device, exact, 0)
+    g.sync()
+    t_setup = time.perf_counter() - t_setup
 
     t = 1
-    if preload:
-        g.run(t, preload)
-        t += preload
+    t_first = time.perf_counter()
+    g.run(t, 1)                  # the first step also plans the owner-computed assembly (host)
+    g.sync()
+    t_first = time.perf_counter() - t_first
+    t += 1
+    if preload > 1:
+        g.run(t, preload - 1)
+        t += preload - 1
     if a.warmup:
         g.run(t, a.warmup)
         t += a.warmup
@@ -432,17 +531,22 @@ def main():
                           "reference-order element kernel: trajectories bit-identical to the CPU restatement "
                           "of v2/HAKAI_j.jl (tests/test_gpu_exact.py)")}
 
-    # per-kernel breakdown from a short extra pass after the timed regions (reported, not timed)
+    # per-kernel times: the element kernel and the exchange from the timed region's own events; the
+    # nodal and BC kernels from a short extra pass after it with events around those two only
     k_tot = {}
+    for name, rec in (("element", el_timed), ("exchange", ex_timed)):
+        ms, n = sum(x[0] for x in rec), sum(x[1] for x in rec)
+        if n:
+            k_tot[name] = [ms, n]
     if a.breakdown:
         for sv in g.svs:
-            sv.profile(True)
+            sv.profile(True, kernels=[K_NODAL, K_BC])
         nb = min(20, max(a.steps, 1))
         g.run(t, nb)
         t += nb
         g.sync()
         for sv in g.svs:
-            for k, name in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"), (K_EXCHANGE, "exchange")):
+            for k, name in ((K_NODAL, "nodal"), (K_BC, "bc")):
                 ms, n = sv.profile_read(k)
                 if n:
                     p = k_tot.setdefault(name, [0.0, 0])
@@ -488,10 +592,17 @@ def main():
         ex_ms = sum(x[0] for x in ex_timed) / max(ex_timed[0][1], 1) / len(g.svs)
         extra["exchange_ms_per_step"] = round(max_over_ranks(ex_ms, multi), 4)
     g.close()
+    if nparts > 1:
+        extra["setup_s_per_rank"] = {"mesh_and_upload": [round(x, 2) for x in gather_floats(t_setup, multi)],
+                                     "of_which_mesh": [round(x, 2) for x in gather_floats(t_mesh, multi)],
+                                     "first_step_with_planning": [round(x, 2) for x in gather_floats(t_first, multi)]}
     if nparts > 1 and not a.strong and a.c5_strong:
         # BASELINE config 5: the C5 16 M bar split over the same ranks, timed in the same run
+        t5s = time.perf_counter()
         b5 = [c5_strong_model(r, nparts, 0) for r in ids]
         g5 = Group(b5, ids, R, rank, world, device, exact, 1)
+        g5.sync()
+        t5s = time.perf_counter() - t5s
         pre5 = b5[0][4]
         t5 = 1
         g5.run(t5, pre5 + 10)
@@ -507,17 +618,16 @@ def main():
         c5 = {"workload": b5[0][3]["workload"], "elements": b5[0][3]["elements"], "steps": a.c5_steps,
               "value": round(v5, 3), "unit": "M element-updates/s", "ms_per_step": round(e5 / a.c5_steps * 1e3, 4),
               "exchange_ms_per_step": round(ex5_ms, 4), "element_avg_ms_per_rank": round(el5_ms, 4),
+              "setup_s_per_rank": [round(x, 2) for x in gather_floats(t5s, multi)],
               "n1_reference": None, "speedup_vs_n1": None}
-        if os.path.exists(C5_N1_LINE):
-            try:
-                with open(C5_N1_LINE) as f:
-                    n1 = json.loads([ln for ln in f if ln.strip().startswith("{")][-1])
-                if n1.get("config", {}).get("element_mode") == a.element_mode:
-                    c5["n1_reference"] = {"value": n1["value"], "ms_per_step": n1["ms_per_step"],
-                                          "source": os.path.relpath(C5_N1_LINE, ROOT)}
-                    c5["speedup_vs_n1"] = round(v5 / n1["value"], 3)
-            except Exception:
-                pass
+        del b5
+        if a.c5_n1_ref:
+            # the same 16 M bar on ONE GPU (rank 0's), same steps, timed in this run after the N-rank
+            # run: speedup_vs_n1 is a same-run, same-box ratio
+            n1 = c5_n1_reference(rank, device, exact, a.c5_steps, multi)
+            if n1 is not None:
+                c5["n1_reference"] = n1
+                c5["speedup_vs_n1"] = round(v5 / n1["value"], 3)
         extra["c5_strong"] = c5
     if world > 1 and not a.strong and a.same_slab_ref:
         # the same slab alone on each GPU, concurrently; the slowest rank, like the timed run
@@ -552,7 +662,12 @@ def main():
                        deleted_elements=int(n_deleted),
                        whole_step_roofline_frac=round(whole_bytes * a.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)
                        if nparts == 1 else None,
-                       kernel_ms_per_step=k_ms, other_mode=other, **extra,
+                       kernel_ms_per_step=k_ms,
+                       kernel_ms_source=("element, exchange: HIP events around those kernels inside the timed "
+                                         "region (the roofline's avg_launch_ms); nodal, bc: a %d-step pass after "
+                                         "it with events around those two kernels only" % min(20, max(a.steps, 1))
+                                         if a.breakdown else "element, exchange: HIP events inside the timed region"),
+                       other_mode=other, **extra,
                        assembly=("owner-computed node sums in LDS (own_assembly), element order" if own_steps
                                  else "fe round trip (element forces gathered by the nodal kernel)"),
                        parallelism=(f"dp{world}" if world > 1 else

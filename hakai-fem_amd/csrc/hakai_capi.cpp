@@ -1488,7 +1488,8 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const Call
         if (pz[0]) {
             c->poison_step = pz[1];
             const long long good = (long long)pz[1] - (long long)t_first;  // steps of this call that ran
-            if (good >= 0 && good <= n_steps) {
+            const bool rolled = good >= 0 && good <= n_steps;
+            if (rolled) {
                 c->cur = (good & 1) ? 1 - s0.cur : s0.cur;
                 c->steps_done = s0.done + good;
                 if (good == 0) {  // nothing of the call ran: where the Q of the next nodal update is
@@ -1503,6 +1504,8 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const Call
             }
             hkc::graph_invalidate(c);
             hkc::contact_after_overflow(c, c->steps_done);
+            // a poison step outside this call rolled nothing back: never run the call again from it
+            if (!rolled) (void)hkc::contact_exchange_retry(c);
             HIPCHK(hipMemset(c->d_poison, 0, 2 * sizeof(int)));
             const std::string msg = hakai_last_error();
             return fail(rc, "%s; step %d was not applied: the state is that after step %d", msg.c_str(), pz[1],
@@ -1521,6 +1524,11 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     if (n_steps < 0 || !(d_time > 0)) return fail(HAKAI_ERR_ARG, "step: n_steps=%lld d_time=%g", (long long)n_steps, d_time);
     if (n_steps > 1 && hkc::comm_is_local(c))
         return fail(HAKAI_ERR_ARG, "step: an in-process group is stepped one step per call, rank by rank");
+    // a contact rank of an in-process group needs its peers' phases between its own: refused before
+    // any work, so its contact state (tsel parity, touched lists, bin headers) stays in step with them
+    if (hkc::comm_is_local(c) && hkc::contact_multi(c) && hkc::comm_size(c) > 1)
+        return fail(HAKAI_ERR_STATE, "step: rank %d of an in-process group with multi-GPU contact is stepped by "
+                    "hakai_step_group only", hkc::comm_rank(c));
     HIPCHK(hipSetDevice(c->device));
     // a step that overflowed a multi-GPU contact exchange runs again once its capacity has grown
     // (every rank takes the same decision from the same gathered counts)
@@ -1606,6 +1614,10 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
         for (int r = 0; r < n; ++r) retry = hkc::contact_exchange_retry(ctxs[r]) && retry;
         if (!retry) return rc;
         const long long p = ctxs[0]->poison_step;
+        for (int r = 1; r < n; ++r)  // every rank read the same headers: the same step, or no retry
+            if (ctxs[r]->poison_step != p)
+                return fail(rc, "step_group: ranks disagree on the poisoned step (rank 0: %lld, rank %d: %lld)", p, r,
+                            ctxs[r]->poison_step);
         n_steps -= (int64_t)(p - (long long)t_first);
         t_first = (double)p;
     }

@@ -301,7 +301,8 @@ __device__ __forceinline__ Range pair_range(const unsigned long long* bb_) {
 // incremental update (an element was deleted in the previous step), deleted elements found, and
 // the number of nodes with contact force in each of the two ping-pong "touched" lists.
 enum { kEv = 0, kEvMax = 1, kDirty = 2, kDel = 3, kNdel = 4, kTouched = 5 /* [5], [6] */, kNcand = 7, kTerms = 8,
-       kNcandMax = 9, kEvShardMax = 10, kCandShardMax = 11, kCandOver = 12, kSeq = 13, kCtl = 16 };
+       kNcandMax = 9, kEvShardMax = 10, kCandShardMax = 11, kCandOver = 12, kSeq = 13, kItemShardMax = 14,
+       kCtl = 16 };
 // Events are appended into kEvShards shards, each with its own counter on its own 128-B line: with
 // one counter, every wave that found an event waited on the same memory-side atomic (measured:
 // 0.13 ms of a 0.30 ms contact step on C4).
@@ -1196,6 +1197,7 @@ __device__ __forceinline__ void tri_body(const StepIn& s, unsigned int* ctl, con
         ctl[kNcand] = s_cpre[kCandShards + 2];
         atomicMax(&ctl[kNcandMax], s_cpre[kCandShards + 2]);
         atomicMax(&ctl[kCandShardMax], s_cpre[kCandShards + 3]);
+        atomicMax(&ctl[kItemShardMax], s_ipre[kCandShards + 3]);  // search items: own buffer, own report
         ctl[kCandOver] = s_cpre[kCandShards + 1] | s_ipre[kCandShards + 1];
     }
     const int lane = (int)(threadIdx.x & 63);
@@ -2677,6 +2679,7 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         HIPCHK(hipMalloc(&C->d_cand, (size_t)C->cand_cap * sizeof(TriRec)));
         HIPCHK(dalloc(&C->d_item, (size_t)kItemsPerCand * C->cand_cap));
         HIPCHK(hipMemsetAsync(C->d_ctl + kNcandMax, 0, 3 * sizeof(unsigned int), c->stream));  // + shard max, over
+        HIPCHK(hipMemsetAsync(C->d_ctl + kItemShardMax, 0, sizeof(unsigned int), c->stream));
         return 0;
     }
     if (!std::strcmp(key, "contact_exchange_deletions") || !std::strcmp(key, "contact_exchange_bins") ||
@@ -2748,6 +2751,12 @@ int contact_check(hakai_ctx* c) {
         return fail(HAKAI_ERR_STATE, "contact: %u candidate triangles in one step (%u in one of %d shards) exceed the "
                     "buffer (%lld); raise hakai_set_tuning(\"contact_candidate_cap\")", mc[0],
                     mc[kCandShardMax - kNcandMax], kCandShards, C->cand_cap);
+    unsigned int mi = 0;  // search items (one per candidate and reachable cell, <= 27 per candidate)
+    HIPCHK(hipMemcpy(&mi, C->d_ctl + kItemShardMax, sizeof(unsigned int), hipMemcpyDeviceToHost));
+    if ((long long)mi > kItemsPerCand * C->cshard_cap)
+        return fail(HAKAI_ERR_STATE, "contact: %u search items in one of %d shards exceed the item buffer (%lld per "
+                    "shard, %d per candidate slot); raise hakai_set_tuning(\"contact_candidate_cap\"), which also "
+                    "grows the item buffer", mi, kCandShards, (long long)kItemsPerCand * C->cshard_cap, kItemsPerCand);
     if (Xrank* X = C->xr) {
         int xc = 0;
         HIPCHK(hipMemcpy(&xc, X->d_xctl, sizeof(int), hipMemcpyDeviceToHost));

@@ -522,10 +522,35 @@ __device__ __forceinline__ void gp_all8x2(double* w, int k, double x, double y, 
     ys = b;
 }
 
+// Diagnostic build only (-DHK_DIAG_PHASE, tools/diag_wave.py): per-wave clock totals of the phases of
+// the reference-order element step (sched_barrier pins each stamp between the phases it separates).
+#ifdef HK_DIAG_PHASE
+struct PhaseClock {
+    long long t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long last = 0;
+};
+#define HK_PH(pc, i)                                   \
+    do {                                               \
+        __builtin_amdgcn_sched_barrier(0);             \
+        const long long now_ = clock64();              \
+        (pc).t[i] += now_ - (pc).last;                 \
+        (pc).last = now_;                              \
+        __builtin_amdgcn_sched_barrier(0);             \
+    } while (0)
+#define HK_PH_ARG , PhaseClock& pc
+#define HK_PH_PASS , pc
+#else
+#define HK_PH(pc, i) \
+    do {             \
+    } while (0)
+#define HK_PH_ARG
+#define HK_PH_PASS
+#endif
+
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool WITH_VOL, int NT = 0, bool OWN = false>
 __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat* __restrict__ mats, long long e,
                                                 int k, double* nd8, double* xb, const double* pus,
-                                                const ElemIn& in, double* sfe = nullptr) {
+                                                const ElemIn& in, double* sfe HK_PH_ARG) {
 #pragma clang fp contract(off)
     const DevMat* M = mats + in.mt;
     const bool active = in.fl == 1;
@@ -541,6 +566,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     nd8[6 * k + 4] = in.uu[1] - in.up[1];
     nd8[6 * k + 5] = in.uu[2] - in.up[2];
     wave_lds_fence();
+    HK_PH(pc, 1);
 
     // ---- Jacobian at GP k in node order, det and inverse (cal_Bfinal :1424-1455; cal_BVbar_hexa
     // computes the same J and det at :1716-1740). The first term starts the sum (0 + x == x).
@@ -589,6 +615,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         }
     }
 
+    HK_PH(pc, 2);
     // P2/3 (cal_BVbar_hexa's P2 / 3 at :1745-1750 and Bfinal's -P2/3 at :1482-1490: the same
     // correctly rounded quotient), formed once; it becomes t(i,c) below, in place
     double tk[8][3];
@@ -622,6 +649,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
 #pragma unroll
         for (int c = 0; c < 3; ++c) tk[i][c] = nd8[6 * i + c] - tk[i][c];
     auto tq = [&](int i, int c) { return tk[i][c]; };
+    HK_PH(pc, 3);
 
     // ---- de = Bfinal * d_u (:1204): per row, the fma chain over columns j = 3i+c in order.
     // Bfinal column (i,c) by rows: c=0: (Pix+t0, t0, t0, Piy, 0, Piz); c=1: (t1, Piy+t1, t1, Pix,
@@ -660,6 +688,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         asm volatile("" ::: "memory");  // one node's LDS operands in flight at a time (VGPRs)
     }
 
+    HK_PH(pc, 4);
     // ---- d_o = Dmat * de (:1205): the 6x6 chain without its structural zeros
     const double Dn = M->Dn, Do = M->Do, Ds = M->Ds;
     double fin[6];
@@ -717,6 +746,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         ys = in.ys;
     }
 
+    HK_PH(pc, 5);
     bool kill = false;
     if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
         double v_e, t_e;
@@ -764,9 +794,11 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         }
         fk[2] = gp_sum8(xb, k, w);
     }
+    HK_PH(pc, 6);
     if (WITH_VOL) a.vol[e] = V;
     elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN, true>(a, e, k, in, active, kill, fk, fin, eps,
                                                                             eqp, ys, tri, sfe);
+    HK_PH(pc, 7);
 }
 
 // Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.
@@ -814,9 +846,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
     } else {
         load_stage_b<true>(a, e, k, in);
     }
+#ifdef HK_DIAG_PHASE
+    PhaseClock pc;
+#endif
     if (EXACT)
         elem_step_exact<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride,
-                                                                s_xb + grp * kXbStride, s_pus, in);
+                                                                s_xb + grp * kXbStride, s_pus, in, nullptr HK_PH_PASS);
     else
         elem_step<DO_DELETE, STORE_TRIAX, true, WITH_VOL>(a, a.mats, e, k, s_nd + grp * kLdsStride, in);
 }
@@ -899,18 +934,46 @@ __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const doub
     for (int c = 0; c < 3; ++c) dst[c] = v[c];
 }
 
+// Diagnostic build only (tools/variants.sh with -DHK_DIAG_WAVE, tools/diag_wave.py): per-wave clock
+// totals of the persistent kernel -- loop, block-barrier wait, summing pass -- accumulated over launches
+// into a device table the tool reads back. Product builds compile none of it.
+#ifdef HK_DIAG_WAVE
+constexpr int kDiagWaves = 8192, kDiagWords = 8;
+__device__ unsigned long long g_diag[kDiagWaves * kDiagWords];
+struct PassClock {
+    long long bar = 0, pass = 0, n = 0;
+};
+#define HK_DIAG_ARG , PassClock& dg
+#define HK_DIAG_PASS , dg
+#else
+#define HK_DIAG_ARG
+#define HK_DIAG_PASS
+#endif
+
 // One summing pass: the prefetched entry of this thread, then -- only for a super-batch with more
 // than kBlock entries (wide cross-sections) -- a second one, loaded here (that pass waits for it).
 // Entries of one pass touch distinct LDS slots, so the two rounds need no barrier between them.
 __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long sb, const double* s_fe,
-                                         double* s_part) {
+                                         double* s_part HK_DIAG_ARG) {
+#ifdef HK_DIAG_WAVE
+    const long long t0 = clock64();
+#endif
     lds_barrier();  // the super-batch's forces are in s_fe, the previous pass is done with s_part
+#ifdef HK_DIAG_WAVE
+    const long long t1 = clock64();
+#endif
     own_entry(a, en, s_fe, s_part);
     if (en.y & kOwnRound2) {  // block-uniform
         const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
         const int idx = o0 + kBlock + (int)threadIdx.x;
         own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe, s_part);
     }
+#ifdef HK_DIAG_WAVE
+    const long long t2 = clock64();
+    dg.bar += t1 - t0;
+    dg.pass += t2 - t1;
+    dg.n += 1;
+#endif
 }
 
 // Persistent, software-pipelined form: each block walks a contiguous range of batches (XCD-aware),
@@ -973,6 +1036,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     auto vb_of = [&](long long i) { return OWN ? (long long)a.own_seq[pos_of(i)] : pos_of(i); };
     auto elem_of = [&](long long i) { return vb_of(i) * kEPB + grp; };
 
+#ifdef HK_DIAG_WAVE
+    PassClock dg;
+    const long long dg_t0 = clock64();
+#endif
+#ifdef HK_DIAG_PHASE
+    PhaseClock pc;
+#endif
     ElemIn cur, nxt;
     int4 ent_cur = {0, 0, 0, 0}, ent_nxt = {0, 0, 0, 0};
     load_stage_a<EXACT>(a, elem_of(0), k, cur);
@@ -997,10 +1067,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
         double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
         if (EXACT) {
+#ifdef HK_DIAG_PHASE
+            pc.last = clock64();
+#endif
             load_node_raw(a, cur);
             load_gp<ANY_PLASTIC, NT>(a, elem_of(i), k, cur);
+            HK_PH(pc, 0);
             elem_step_exact<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, xb, s_pus,
-                                                                                 cur, sfe);
+                                                                                 cur, sfe HK_PH_PASS);
         }
         else
             elem_step<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, false, NT, OWN>(a, mats, elem_of(i), k, nd8, cur, sfe);
@@ -1008,13 +1082,43 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
             // block-uniform branch; the compiler's load accounting is the same on both sides
             // (checked in the ISA: identical vmcnt waits with or without balancing stores)
             if ((i + 1) % S == 0 || i + 1 == count)
-                own_pass(a, ent_cur, sb_of(i), s_fe + ((i / S) & 1) * kOwnFe, s_part);
+                own_pass(a, ent_cur, sb_of(i), s_fe + ((i / S) & 1) * kOwnFe, s_part HK_DIAG_PASS);
             ent_cur = ent_nxt;
         }
         cur = nxt;
         nxt = nn;
     }
+#ifdef HK_DIAG_WAVE
+    const long long dg_t1 = clock64();
+    const unsigned gw = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0 && gw < (unsigned)kDiagWaves) {
+        unsigned long long* d = g_diag + (size_t)kDiagWords * gw;
+        atomicAdd(d + 0, (unsigned long long)(dg_t1 - dg_t0));
+        atomicAdd(d + 1, (unsigned long long)dg.bar);
+        atomicAdd(d + 2, (unsigned long long)dg.pass);
+        atomicAdd(d + 3, (unsigned long long)dg.n);
+        atomicAdd(d + 4, (unsigned long long)count);
+        atomicAdd(d + 5, 1ull);
+        atomicExch(d + 6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));  // HW_ID
+#ifdef HK_DIAG_PHASE
+        unsigned long long* q = g_diag + (size_t)kDiagWords * (kDiagWaves / 2 + gw);
+        for (int j = 0; j < 8; ++j) atomicAdd(q + j, (unsigned long long)pc.t[j]);
+#endif
+    }
+#endif
 }
+
+#ifdef HK_DIAG_WAVE
+extern "C" int hk_diag_reset() {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_diag)) != hipSuccess) return -1;
+    return hipMemset(p, 0, sizeof(g_diag)) == hipSuccess ? 0 : -1;
+}
+extern "C" int hk_diag_read(unsigned long long* out, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * (size_t)std::min(n, kDiagWaves * kDiagWords)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Runtime flags -> template instantiations.
 template <bool EXACT>

@@ -151,6 +151,52 @@ def slab_partition(glob: Model, rank: int, world: int, nx: int, ny: int):
     return local, diag, iface
 
 
+def bar_slab(nx: int, ny: int, nz: int, rank: int, world: int, material, v_z, perturb: float = 0.01, seed: int = 0,
+             d_time: float = 1e-7, n_steps: int = 1000, name: str = "bar"):
+    """slab_partition(mesh.bar_model(nx, ny, nz, material, v_z, ...), rank, world, nx, ny) built
+    directly: only the rank's layers (plus one halo layer each side for the lumped mass) are ever
+    materialised, so a rank of a 16 M-hex bar holds 2 M hex of host arrays instead of the whole bar.
+    Bit-identical to the global construction (tests/test_dist_cpu.py); world = 1 gives the whole bar.
+
+    Returns (local Model, local diag_M (3 nN_local), (local_node, rank_lo, rank_hi))."""
+    npl = (nx + 1) * (ny + 1)
+    k0, k1 = partition_ranges(nz, world)[rank]
+    if k1 - k0 < 2 and world > 1:
+        raise ValueError("each slab needs >= 2 element layers (a node may be shared by two ranks only)")
+    h0, h1 = max(0, k0 - 1), min(nz, k1 + 1)
+    hc = _mesh.bar_layer_coords(nx, ny, h0, h1, perturb=perturb, seed=seed)
+    _, he = _bar_layers(nx, ny, 0, h1 - h0, hc)
+    mats = [material]
+    halo = Model(hc, he, np.ones(he.shape[0], np.int64), mats)
+    hdiag, _ = halo.lumped_mass()
+    off = (k0 - h0) * npl
+    nloc = (k1 - k0 + 1) * npl
+    coord = np.ascontiguousarray(hc[off:off + nloc])
+    _, elem = _bar_layers(nx, ny, 0, k1 - k0, coord)
+    diag = np.ascontiguousarray(hdiag[3 * off:3 * (off + nloc)])
+    L = float(nz)
+    vz = v_z(coord[:, 2], L) if callable(v_z) else np.full(nloc, float(v_z))
+    bc = [_mesh.encastre(_mesh.plane_nodes(nx, ny, 0))] if k0 == 0 else []
+    local = Model(coord, elem, np.ones(elem.shape[0], np.int64), mats, bc,
+                  np.arange(1, nloc + 1, dtype=np.int64) * 3, np.ascontiguousarray(vz, dtype=np.float64), d_time,
+                  d_time * n_steps, name=f"{name}[rank {rank}/{world}]" if world > 1 else name)
+    ln, lo, hi = [], [], []
+    if rank > 0:
+        ln.append(np.arange(0, npl))
+        lo.append(np.full(npl, rank - 1))
+        hi.append(np.full(npl, rank))
+    if rank < world - 1:
+        ln.append(np.arange(nloc - npl, nloc))
+        lo.append(np.full(npl, rank))
+        hi.append(np.full(npl, rank + 1))
+    iface = (np.concatenate(ln).astype(np.int64) if ln else np.zeros(0, np.int64),
+             np.concatenate(lo).astype(np.int32) if lo else np.zeros(0, np.int32),
+             np.concatenate(hi).astype(np.int32) if hi else np.zeros(0, np.int32))
+    local.global_node_offset = k0 * npl
+    local.global_element_offset = k0 * nx * ny
+    return local, diag, iface
+
+
 def rank_device(local_rank: int, local_world: int) -> int:
     """The HIP device of a local rank: device = local rank on a node with a GPU per rank; with fewer
     visible GPUs than local ranks, local rank mod the visible count (e.g. one visible GPU per process

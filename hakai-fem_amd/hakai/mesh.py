@@ -55,6 +55,25 @@ def hex_bar(nx: int, ny: int, nz: int, h: float = 1.0, perturb: float = 0.0, see
     return np.ascontiguousarray(coord), np.ascontiguousarray(elem)
 
 
+def bar_layer_coords(nx: int, ny: int, k0: int, k1: int, h: float = 1.0, perturb: float = 0.0,
+                     seed: int = 0) -> np.ndarray:
+    """Node coordinates of layers k0..k1 (inclusive) of hex_bar(nx, ny, nz, h, perturb, seed), for any
+    nz > k1, without building the whole bar: the same values bit for bit. The perturbation of node g
+    is draws 3g..3g+2 of the bar's PCG64 stream (Generator.uniform takes one 64-bit output per
+    double), so the stream is advanced to the first node of layer k0."""
+    npl = (nx + 1) * (ny + 1)
+    xs = np.arange(nx + 1, dtype=np.float64) * h
+    ys = np.arange(ny + 1, dtype=np.float64) * h
+    zs = np.arange(k0, k1 + 1, dtype=np.float64) * h  # hex_bar's z0 + k * h with z0 = 0, k = k0..k1
+    Z, Y, X = np.meshgrid(zs, ys, xs, indexing="ij")
+    coord = np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=1)
+    if perturb > 0:
+        bg = np.random.PCG64(seed)  # = default_rng(seed)'s bit generator
+        bg.advance(3 * k0 * npl)
+        coord += np.random.Generator(bg).uniform(-perturb * h, perturb * h, size=coord.shape)
+    return np.ascontiguousarray(coord)
+
+
 def plane_nodes(nx, ny, iz) -> np.ndarray:
     """1-based ids of the nodes of layer iz."""
     iy, ix = np.meshgrid(np.arange(ny + 1), np.arange(nx + 1), indexing="ij")

@@ -56,3 +56,46 @@ def test_failing_rank_fails_the_launch():
     assert r.returncode != 0
     assert "visible GPU" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _devices_check(idents, shared=None):
+    """bench.check_distinct_devices on `len(idents)` ranks (threads) over one in-memory store, each
+    rank's GPU identity given; returns the per-rank outcome (None or the SystemExit message)."""
+    import threading
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    store = dist.HashStore()
+    out = [None] * len(idents)
+    orig = bench.device_identity
+    bench.device_identity = lambda d: idents[d]
+    old = os.environ.pop("HAKAI_RCCL_SHARED_GPU", None)
+    if shared:
+        os.environ["HAKAI_RCCL_SHARED_GPU"] = "1"
+    try:
+        def rank(r):
+            try:
+                bench.check_distinct_devices(store, r, len(idents), r)
+            except SystemExit as e:
+                out[r] = str(e)
+        ts = [threading.Thread(target=rank, args=(r,)) for r in range(len(idents))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+    finally:
+        bench.device_identity = orig
+        os.environ.pop("HAKAI_RCCL_SHARED_GPU", None)
+        if old is not None:
+            os.environ["HAKAI_RCCL_SHARED_GPU"] = old
+    return out
+
+
+def test_ranks_on_one_gpu_stop_at_the_guard():
+    """one global HIP_VISIBLE_DEVICES=0 with --gpus 2 maps both ranks to the same GPU; the
+    guard compares the ranks' PCI identities after the rendezvous and stops both with a clear message
+    (per-rank masks that give each rank its own GPU pass; HAKAI_RCCL_SHARED_GPU=1 declares sharing)."""
+    assert _devices_check(["0000:05:00 a", "0000:15:00 b", "0000:25:00 c"]) == [None, None, None]
+    out = _devices_check(["0000:05:00 a", "0000:05:00 a"])
+    assert all(o and "same GPU" in o for o in out)
+    assert _devices_check(["0000:05:00 a", "0000:05:00 a"], shared=True) == [None, None]

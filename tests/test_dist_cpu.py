@@ -131,6 +131,43 @@ def test_partition_covers_mesh_and_bcs():
             ld = {int(d) + 3 * n0 for g in loc.bc for d, _ in g.entries for d in d}
             assert gd == ld
 
+def _same_model(a, b):
+    assert np.array_equal(a.coordmat, b.coordmat) and a.coordmat.dtype == b.coordmat.dtype
+    assert np.array_equal(a.elementmat, b.elementmat)
+    assert np.array_equal(a.element_material, b.element_material)
+    assert np.array_equal(a.ic_dofs, b.ic_dofs) and np.array_equal(a.ic_values, b.ic_values)
+    assert (a.d_time, a.end_time, a.mass_scaling, a.name) == (b.d_time, b.end_time, b.mass_scaling, b.name)
+    assert len(a.bc) == len(b.bc)
+    for ga, gb in zip(a.bc, b.bc):
+        assert len(ga.entries) == len(gb.entries)
+        for (da, va), (db, vb) in zip(ga.entries, gb.entries):
+            assert np.array_equal(da, db) and va == vb
+    assert getattr(a, "global_node_offset", 0) == getattr(b, "global_node_offset", 0)
+    assert getattr(a, "global_element_offset", 0) == getattr(b, "global_element_offset", 0)
+
+
+@pytest.mark.parametrize("shape,v_z", [((3, 2, 12), lambda z, L: 5e5 * z / 4), ((2, 2, 9), -1e5)])
+def test_bar_slab_equals_global_partition(shape, v_z):
+    """bench.py's ranks build their slab directly (dist.bar_slab), never the whole bar: the same model,
+    lumped mass and interface bit for bit as slab_partition of the global bar_model (and, with one rank,
+    as the global model itself)."""
+    from hakai import mesh
+    nx, ny, nz = shape
+    glob = mesh.bar_model(nx, ny, nz, mesh.steel_ductile(), v_z, name="B")
+    gdiag, _ = glob.lumped_mass()
+    one, d1, i1 = dist.bar_slab(nx, ny, nz, 0, 1, mesh.steel_ductile(), v_z, name="B")
+    _same_model(one, glob)
+    assert np.array_equal(d1, gdiag) and all(len(x) == 0 for x in i1)
+    for world in (2, 3, 4):
+        for r in range(world):
+            ref = dist.slab_partition(glob, r, world, nx, ny)
+            got = dist.bar_slab(nx, ny, nz, r, world, mesh.steel_ductile(), v_z, name="B")
+            _same_model(got[0], ref[0])
+            assert np.array_equal(got[1], ref[1])
+            for x, y in zip(got[2], ref[2]):
+                assert np.array_equal(x, y) and x.dtype == y.dtype
+
+
 def test_partition_ranges():
     assert dist.partition_ranges(10, 3) == [(0, 4), (4, 7), (7, 10)]
     with pytest.raises(ValueError):

@@ -75,9 +75,11 @@ def test_local_group_rejects_multi_step_calls():
         sv.close()
 
 
-def _run_contact_group(glob, world, n_steps, key, tune=None):
+def _run_contact_group(glob, world, n_steps, key, tune=None, refuse_at=0):
     """Range-partitioned contact model on an in-process group (hakai_set_contact_global): each rank
-    searches the triangles of its elements against the binned contact nodes of every rank."""
+    searches the triangles of its elements against the binned contact nodes of every rank.
+    refuse_at > 0: after that many steps, every rank is first asked to step ALONE (hakai_step), which
+    must be refused before any work (HAKAI_ERR_STATE), then the group goes on."""
     gdiag, _ = glob.lumped_mass()
     parts = [dist.range_partition(glob, r, world, gdiag) for r in range(world)]
     svs = []
@@ -90,7 +92,16 @@ def _run_contact_group(glob, world, n_steps, key, tune=None):
         for k, v in (tune or {}).items():
             sv.set_tuning(k, v)
         svs.append(sv)
-    step_group(svs, 1, n_steps)
+    if refuse_at:
+        from hakai._abi import HAKAI_ERR_STATE, HakaiError
+        step_group(svs, 1, refuse_at)
+        for sv in svs:
+            with pytest.raises(HakaiError) as ei:
+                sv.step(refuse_at + 1, 1)
+            assert ei.value.code == HAKAI_ERR_STATE
+        step_group(svs, refuse_at + 1, n_steps - refuse_at)
+    else:
+        step_group(svs, 1, n_steps)
     if tune and tune.get("own_assembly"):
         assert all(sv.stat("own_steps") == n_steps for sv in svs)
     out = [(loc, l2g, sv.download(), [tuple(x) for x in sv.deleted()], sv.contact_stats())
@@ -178,6 +189,21 @@ def test_contact_group_bitexact_with_deletion(world):
     for k in ("live_triangles", "live_nodes_i", "live_nodes_j", "candidate_triangles"):
         assert sum(st[k] for st in sts) == gst[k], k  # the lists and the search divide
     assert sum(st["candidate_triangles"] > 0 for st in sts) >= 2
+
+
+def test_contact_group_rank_cannot_step_alone():
+    """hakai_step on one contact rank of an in-process group is refused BEFORE any work
+    (no tsel flip, no prologue kernels), so a later hakai_step_group still matches one context bit
+    for bit."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(6, 6, 1), impactor=(2, 2, 3), v=-3e5, d_time=2e-8, n_steps=400)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+        gdel = [tuple(x) for x in sv.deleted()]
+    assert len(gdel) >= 4
+    parts = _run_contact_group(glob, 2, glob.n_steps, key=333, refuse_at=151)
+    _assert_group_equals_single(glob, parts, g, gdel)
 
 
 @pytest.mark.parametrize("flag,myu,surfaces", [(1, None, False), (2, 0.0, False), (1, None, True)])

@@ -1,0 +1,71 @@
+#!/bin/bash
+# Round-5 GPU command, one file with named stages (runs on the gpurun box from the repo root):
+#   bash tools/gpu_r5.sh STAGE [STAGE ...]
+# Every GPU step has its own time limit; the first failing step ends the call (no retries).
+# Stages:
+#   suite      pytest -m gpu (whole suite, thread timeouts) -> gpurun_out/r5_suite.log
+#   smoke      __graft_entry__.smoke()                      -> gpurun_out/r5_smoke.log
+#   bench      python bench.py (N = 1, driver defaults)     -> gpurun_out/r5_bench.json
+#   ab3        same-box A/B: the round-3 tree (ab/r3, its own bench.py and library) against this tree,
+#              C3, both element modes, alternating 5 x 2 runs -> gpurun_out/r5_ab3.jsonl
+#   prof       rocprofv3 kernel trace of a short bench (MODE=fused|exact) -> gpurun_out/r5_prof_$MODE/
+#   sq         rocprofv3 SQ counters of the element kernel (MODE=fused|exact) -> gpurun_out/r5_sq_$MODE/
+#   sweep      tools/sweep.py --variants "$SWEEP" (CONFIG=c3|c4|c5slab) -> gpurun_out/r5_sweep.log
+#   diag       per-wave clock totals of the element kernel (variant DIAGLIB, -DHK_DIAG_WAVE) -> gpurun_out/r5_diag_*.jsonl
+#   rehearse4  python bench.py --gpus 4 self-launched on the one GPU (RCCL sockets) -> gpurun_out/r5_rehearse4.json
+#   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r5_tests.log
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() {  # run <seconds> <log> cmd...
+    local t=$1 log=$2
+    shift 2
+    timeout -k 10 "$t" "$@" > "$log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $* -> rc=$rc"
+    tail -n 12 "$log"
+    return $rc
+}
+BA="--cpu-baseline 0 --breakdown 0"
+for st in "$@"; do
+    case "$st" in
+    suite) run 1500 gpurun_out/r5_suite.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
+               --timeout-method thread -p no:cacheprovider || exit $? ;;
+    smoke) run 300 gpurun_out/r5_smoke.log python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run 600 gpurun_out/r5_bench.json python bench.py || exit $? ;;
+    ab3) : > gpurun_out/r5_ab3.jsonl
+        for i in 1 2 3 4 5; do
+            for tree in r3 cur; do
+                if [ $tree = r3 ]; then b=ab/r3/bench.py; else b=bench.py; fi
+                run 300 gpurun_out/r5_ab3_$tree$i.log python $b --steps 200 --warmup 20 $BA || exit $?
+                python - "$tree" "$i" gpurun_out/r5_ab3_$tree$i.log >> gpurun_out/r5_ab3.jsonl <<'EOF'
+import json, sys
+d = json.loads([l for l in open(sys.argv[3]) if l.startswith("{")][-1])
+o = d["config"].get("other_mode") or {}
+print(json.dumps({"tree": sys.argv[1], "run": int(sys.argv[2]), "value": d["value"], "ms_per_step": d["ms_per_step"],
+                  "element_avg_ms": d["roofline"]["avg_launch_ms"], "frac": d["roofline"]["frac"],
+                  "exact_value": o.get("value"), "exact_ms_per_step": o.get("ms_per_step"),
+                  "exact_element_avg_ms": o.get("element_avg_ms")}))
+EOF
+            done
+        done
+        cat gpurun_out/r5_ab3.jsonl ;;
+    prof) M=${MODE:-fused}; P=gpurun_out/r5_prof_$M; rm -rf $P
+        HAKAI_GRAPH=0 run 600 gpurun_out/r5_prof_$M.log rocprofv3 --kernel-trace --stats -d $P -o run \
+            --output-format csv -- python bench.py --steps 50 --warmup 5 $BA --compare-fused 0 --element-mode $M || exit $? ;;
+    sq) M=${MODE:-fused}; P=gpurun_out/r5_sq_$M; rm -rf $P
+        HAKAI_GRAPH=0 run 300 gpurun_out/r5_sq_$M.log timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU \
+            SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+            -d $P -o run --output-format csv -- python bench.py --steps 10 --warmup 2 $BA --compare-fused 0 \
+            --element-mode $M || exit $? ;;
+    sweep) run 900 gpurun_out/r5_sweep.log python tools/sweep.py --config ${CONFIG:-c3} --rounds ${ROUNDS:-5} \
+               --variants "$SWEEP" || exit $? ;;
+    diag) V=${DIAGLIB:-diagw}; run 600 gpurun_out/r5_diag_$V.jsonl env HAKAI_LIB=hakai-fem_amd/lib/variants/$V.so \
+              python tools/diag_wave.py --config ${CONFIG:-c3} --modes ${MODES:-exact,fused} --tuning "${TUNE:-}" || exit $? ;;
+    rehearse4) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r5_rehearse4.json python bench.py --gpus 4 \
+                   --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
+    tests:*) run 1200 gpurun_out/r5_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
+                 --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+    esac
+done
