@@ -61,7 +61,7 @@ for mode in a.modes.split(","):
     buf = (ctypes.c_uint64 * (KW * NW))()
     assert L.hk_diag_read(buf, KW * NW) == 0
     d = np.frombuffer(buf, dtype=np.uint64).reshape(NW, KW).astype(np.float64)
-    live = d[:, 5] > 0
+    live = d[:NW // 2, 5] > 0  # (rows NW/2.. hold the phase clocks of -DHK_DIAG_PHASE builds)
     n = int(live.sum())
     w = d[:n]
     launches = w[:, 5]
@@ -81,6 +81,9 @@ for mode in a.modes.split(","):
            "compute_cycles_per_batch": round((loop - bar - pas).sum() / max(batches.sum(), 1), 1),
            "block_loop_spread_frac": round(float(np.mean((blk.max(1) - blk.min(1)) / blk.mean(1))), 4),
            "barrier_frac_by_wave_in_block": [round(bar[widx == i].sum() / loop[widx == i].sum(), 4) for i in range(4)],
+           "pass_frac_by_wave_in_block": [round(pas[widx == i].sum() / loop[widx == i].sum(), 4) for i in range(4)],
+           "compute_frac_by_wave_in_block": [round((loop - bar - pas)[widx == i].sum() / loop[widx == i].sum(), 4)
+                                             for i in range(4)],
            "barrier_frac_by_simd": [round(bar[simd == i].sum() / max(loop[simd == i].sum(), 1), 4) for i in range(4)],
            "waves_by_simd": [int((simd == i).sum()) for i in range(4)]}
     ph = d[NW // 2:NW // 2 + n]

@@ -62,6 +62,17 @@ EOF
                --variants "$SWEEP" || exit $? ;;
     diag) V=${DIAGLIB:-diagw}; run 600 gpurun_out/r5_diag_$V.jsonl env HAKAI_LIB=hakai-fem_amd/lib/variants/$V.so \
               python tools/diag_wave.py --config ${CONFIG:-c3} --modes ${MODES:-exact,fused} --tuning "${TUNE:-}" || exit $? ;;
+    ablib) : > gpurun_out/r5_ablib.log  # LIBS="a b ..." under hakai-fem_amd/lib/variants (cur = the product library)
+        for i in 1 2 3; do
+            for v in ${LIBS:-base cur}; do
+                if [ $v = cur ]; then lib=hakai-fem_amd/lib/libhakai_hip.so; else lib=hakai-fem_amd/lib/variants/$v.so; fi
+                echo "== $v $i" >> gpurun_out/r5_ablib.log
+                HAKAI_LIB=$lib run 300 gpurun_out/r5_ablib_cur.log python tools/sweep.py --config ${CONFIG:-c3} \
+                    --rounds 2 --variants "${SWEEP:-exact:elem_exact=1;fused:elem_exact=0}" || exit $?
+                cat gpurun_out/r5_ablib_cur.log >> gpurun_out/r5_ablib.log
+            done
+        done
+        grep -E "^==|element" gpurun_out/r5_ablib.log ;;
     rehearse4) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r5_rehearse4.json python bench.py --gpus 4 \
                    --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
     tests:*) run 1200 gpurun_out/r5_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
