@@ -358,7 +358,15 @@ int hakai_create(hakai_ctx** out, int device) {
     {
         double pus[192];
         hkc::pusai_table(pus);
-        e = hipMemcpy(c->d_pusai, pus, sizeof pus, hipMemcpyHostToDevice);
+        // the reference-order element step forms each P2 product once per partner pair and takes
+        // the partner's as its exact negation (elem_step_exact): the table must be odd in each sign
+        bool odd = true;
+        for (int k = 0; k < 8; ++k)
+            for (int i = 0; i < 8; ++i) {
+                const double* p = pus + 24 * k;
+                odd = odd && p[i] == -p[i ^ 1] && p[8 + i] == -p[8 + (i ^ 3)] && p[16 + i] == -p[16 + (i ^ 4)];
+            }
+        e = odd ? hipMemcpy(c->d_pusai, pus, sizeof pus, hipMemcpyHostToDevice) : hipErrorInvalidValue;
         if (e != hipSuccess) {
             dfree(c->d_negjac);
             dfree(c->d_pusai);

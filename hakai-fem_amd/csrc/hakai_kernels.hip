@@ -156,25 +156,29 @@ __device__ __forceinline__ void load_stage_b(const ElemArgs& a, long long e, int
 // point's state, the element flag and the deletion log.
 // PRESEL: fin/eps/eqp/ys already hold the values to store (the caller selected the previous state
 // for inactive elements early, so in.sig/eps need not stay live until here).
+// PART: kWbAll every store; kWbState the Gauss-point state, flag and deletion log only; kWbForce the
+// node forces only (the state can then be stored before the force pass, freeing its registers).
+enum { kWbAll = 0, kWbState = 1, kWbForce = 2 };
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, int NT, bool EXACT_NODE = false, bool OWN = false,
-          bool PRESEL = false>
+          bool PRESEL = false, int PART = kWbAll>
 __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, int k, const ElemIn& in, bool active,
                                                bool kill, const double (&fk)[3], const double (&fin)[6],
                                                const double (&eps)[6], double eqp, double ys, double tri,
                                                double* sfe = nullptr) {
     const unsigned go = gp_off(e, k);
-    if (OWN) {  // owner-computed assembly: the batch's forces go to LDS [element][local node][3]
+    if (PART != kWbState && OWN) {  // owner-computed assembly: the batch's forces go to LDS [element][local node][3]
         double* fo = sfe + 3 * ((threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k)));
         fo[0] = active ? fk[0] : 0.0;
         fo[1] = active ? fk[1] : 0.0;
         fo[2] = active ? fk[2] : 0.0;
     }
-    if (!OWN || STORE_TRIAX) {  // fe; with owner assembly only on a call's last step (Q / Qe downloads, mode switches)
+    if (PART != kWbState && (!OWN || STORE_TRIAX)) {  // fe; with owner assembly only on a call's last step (Q / Qe downloads, mode switches)
         double* fg = at32(a.fe, 8u * (unsigned)in.fb);
         fg[0] = active ? fk[0] : 0.0;
         fg[1] = active ? fk[1] : 0.0;
         fg[2] = active ? fk[2] : 0.0;
     }
+    if (PART == kWbForce) return;
     // deletion zeroes stress/strain (:742-756); inactive elements keep their state
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -607,12 +611,30 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         const double iJ13 = (J12 * J23 - J13 * J22) * div_v;
         const double iJ23 = (J13 * J21 - J11 * J23) * div_v;
         const double iJ33 = (J11 * J22 - J12 * J21) * div_v;
+        // pd[i][r] = iJr1 * P0[i] + iJr2 * P1[i] + iJr3 * P2[i]. The Pusai table is odd in the node's
+        // r-th sign, ((1/8 * delta_r) * f) * g with delta_r = +-1 (hkc::pusai_table), so
+        // Pusai[k][r][i] == -Pusai[k][r][partner_r(i)] bit for bit with partner_r flipping that sign
+        // (i^1, i^3, i^4 in C3D8 order); RN(-x) = -RN(x), so each product is formed once per
+        // partner pair and the sums take it with a sign modifier: the same bits, 36 fewer multiplies.
+        auto row = [&](int r, double a, double b, double c) {
+            double q0[8], q1[8], q2[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            pd[i][0] = iJ11 * P0[i] + iJ12 * P1[i] + iJ13 * P2[i];
-            pd[i][1] = iJ21 * P0[i] + iJ22 * P1[i] + iJ23 * P2[i];
-            pd[i][2] = iJ31 * P0[i] + iJ32 * P1[i] + iJ33 * P2[i];
-        }
+            for (int i = 0; i < 8; ++i) {
+                if (!(((i + 1) >> 1) & 1)) q0[i] = a * P0[i];
+                if (!((i >> 1) & 1)) q1[i] = b * P1[i];
+                if (!((i >> 2) & 1)) q2[i] = c * P2[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double s0 = (((i + 1) >> 1) & 1) ? -q0[i ^ 1] : q0[i];
+                const double s1 = ((i >> 1) & 1) ? -q1[i ^ 3] : q1[i];
+                const double s2 = ((i >> 2) & 1) ? -q2[i ^ 4] : q2[i];
+                pd[i][r] = s0 + s1 + s2;
+            }
+        };
+        row(0, iJ11, iJ12, iJ13);
+        row(1, iJ21, iJ22, iJ23);
+        row(2, iJ31, iJ32, iJ33);
     }
 
     HK_PH(pc, 2);
@@ -756,6 +778,14 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
     }
 
+    // the Gauss-point state, flag and deletion log are final here: stored before the force pass, so
+    // their registers are free for it and the stores stream out under its arithmetic
+    if (WITH_VOL) a.vol[e] = V;
+    {
+        const double nofk[3] = {0.0, 0.0, 0.0};
+        elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN, true, kWbState>(a, e, k, in, active, kill,
+                                                                                          nofk, fin, eps, eqp, ys, tri);
+    }
     // ---- Qe[:, e] += detJ * Bfinal' * sigma (:1330-1340), GP contributions summed in GP order
     double fk[3];
     {
@@ -795,9 +825,8 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         fk[2] = gp_sum8(xb, k, w);
     }
     HK_PH(pc, 6);
-    if (WITH_VOL) a.vol[e] = V;
-    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN, true>(a, e, k, in, active, kill, fk, fin, eps,
-                                                                            eqp, ys, tri, sfe);
+    elem_writeback<DO_DELETE, STORE_TRIAX, ANY_PLASTIC, NT, true, OWN, true, kWbForce>(a, e, k, in, active, kill, fk,
+                                                                                      fin, eps, eqp, ys, tri, sfe);
     HK_PH(pc, 7);
 }
 
