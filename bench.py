@@ -43,6 +43,7 @@ timed on a bounded sample on this host.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -424,7 +425,16 @@ def c5_n1_reference(rank, device, exact, steps, multi):
         print(f"bench.py: C5 N = 1 reference on device {device}: setup {setup:.1f} s, "
               f"{res[1].item():.3f} ms/step", file=sys.stderr, flush=True)
     if multi:
-        dist.broadcast(res, 0)
+        # the other ranks wait on the host (the rendezvous store), not in a device collective: an RCCL
+        # broadcast would keep a spinning kernel on every other rank's GPU for the whole reference run
+        # (on a shared-GPU rehearsal, on rank 0's GPU itself)
+        store = dist.distributed_c10d._get_default_store()
+        key = "bench_c5_n1_reference"
+        if rank == 0:
+            store.set(key, json.dumps([float(x) for x in res.tolist()]))
+        else:
+            store.wait([key], datetime.timedelta(seconds=1800))
+            res = torch.tensor(json.loads(store.get(key).decode()), dtype=torch.float64)
     if res[0].item() <= 0:
         return None
     return {"value": round(res[0].item(), 3), "ms_per_step": round(res[1].item(), 4),
