@@ -1473,9 +1473,12 @@ struct CallSnap {
     int cur = 0;
     long long done = 0;
     bool fe_ok = true, triax_ok = true, own_valid = false, q_from_buf = false;
+    bool comm_pending = false;  // the interface exchange the call's first nodal update consumes
+    int comm_par = 0;
 };
 static CallSnap call_snap(const hakai_ctx* c) {
     CallSnap s;
+    hkc::comm_pending_get(c, &s.comm_pending, &s.comm_par);
     s.cur = c->cur;
     s.done = c->steps_done;
     s.fe_ok = c->fe_ok;
@@ -1509,6 +1512,7 @@ static int finish_call(hakai_ctx* c, double t_first, int64_t n_steps, const Call
                     c->fe_ok = !c->own_valid;
                     c->triax_ok = false;
                 }
+                hkc::comm_rollback(c, good > 0, (long long)pz[1] - 1, s0.comm_pending, s0.comm_par);
             }
             hkc::graph_invalidate(c);
             hkc::contact_after_overflow(c, c->steps_done);
@@ -1543,6 +1547,7 @@ int hakai_step(hakai_ctx* c, double t_first, int64_t n_steps, double d_time) {
     for (int attempt = 0;; ++attempt) {
         const int rc = step_call(c, t_first, n_steps, d_time);
         if (!rc || attempt >= kExchangeRetries || !hkc::contact_exchange_retry(c)) return rc;
+        ++c->exchange_retries;
         n_steps -= (int64_t)(c->poison_step - (long long)t_first);
         t_first = (double)c->poison_step;
     }
@@ -1626,6 +1631,7 @@ int hakai_step_group(hakai_ctx** ctxs, int32_t n, double t_first, int64_t n_step
             if (ctxs[r]->poison_step != p)
                 return fail(rc, "step_group: ranks disagree on the poisoned step (rank 0: %lld, rank %d: %lld)", p, r,
                             ctxs[r]->poison_step);
+        for (int r = 0; r < n; ++r) ++ctxs[r]->exchange_retries;
         n_steps -= (int64_t)(p - (long long)t_first);
         t_first = (double)p;
     }
@@ -1641,6 +1647,7 @@ int hakai_stat(hakai_ctx* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(HAKAI_ERR_ARG, "null");
     if (!std::strcmp(key, "graph_steps")) *value = c->graph_steps;
     else if (!std::strcmp(key, "own_steps")) *value = c->own_steps;
+    else if (!std::strcmp(key, "exchange_retries")) *value = c->exchange_retries;
     else if (!std::strcmp(key, "own_rows")) *value = c->own_built_g > 0 ? c->own_rows : -1;
     else if (!std::strcmp(key, "own_entries")) *value = c->own_built_g > 0 ? c->own_entries : -1;
     else if (!std::strcmp(key, "own_superbatch")) *value = c->own_built_g > 0 ? c->own_s : 0;

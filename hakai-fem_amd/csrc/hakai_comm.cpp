@@ -357,6 +357,27 @@ int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes)
     return 0;
 }
 
+// RCCL only: every rank's block, each at its own size (bytes[q]), into recv + off[q] for q != this
+// rank (this rank's block stays in `send`); one grouped ncclSend/ncclRecv per peer, ordered on
+// c->stream. The multi-GPU contact's exchanges: each block is sized by what its rank produced, so
+// a rank with few records sends few bytes (an all-gather moves nranks x the largest block).
+int comm_allgatherv_raw(hakai_ctx* c, const void* send, void* recv, const size_t* bytes, const size_t* off) {
+    Comm* m = c->comm;
+    if (!m || m->mode != 0) return fail(HAKAI_ERR_STATE, "all-gather: not an RCCL communicator");
+    HIPCHK(hipEventRecord(m->ev_ag_ready, c->stream));
+    HIPCHK(hipStreamWaitEvent(m->cs, m->ev_ag_ready, 0));
+    NCCLCHK(ncclGroupStart());
+    for (int q = 0; q < m->nranks; ++q) {
+        if (q == m->rank) continue;
+        if (bytes[m->rank]) NCCLCHK(ncclSend(send, bytes[m->rank], ncclUint8, q, m->nc, m->cs));
+        if (bytes[q]) NCCLCHK(ncclRecv(static_cast<char*>(recv) + off[q], bytes[q], ncclUint8, q, m->nc, m->cs));
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(m->ev_ag_done, m->cs));
+    HIPCHK(hipStreamWaitEvent(c->stream, m->ev_ag_done, 0));
+    return 0;
+}
+
 // RCCL only: recv = elementwise MIN over the ranks of send (uint64 words), ordered on c->stream
 // (the multi-GPU contact's pair boxes, hakai_contact.hip)
 int comm_allreduce_min_u64(hakai_ctx* c, const void* send, void* recv, size_t count) {
@@ -383,6 +404,31 @@ hakai_ctx* comm_peer_ctx(hakai_ctx* c, int q) {
 int comm_reset(hakai_ctx* c) {
     if (c->comm) c->comm->pending = false;
     return 0;
+}
+
+// the interface exchange the next nodal update consumes: (pending, buffer parity)
+void comm_pending_get(const hakai_ctx* c, bool* pending, int* par) {
+    *pending = c->comm && c->comm->pending;
+    *par = c->comm ? c->comm->pending_par : 0;
+}
+
+// A poisoned call was rolled back to the state after step `last_good` (finish_call). Its
+// state-writing kernels were no-ops from the poisoned step on, but every step still packed its
+// interface forces -- from the unchanged sums of the last good step -- into the parity of its own
+// step number. The next nodal update must read the parity of the last good step, not the last
+// packed one: the step run again packs into the other parity, and an in-process peer that pulls
+// after it (hakai_step_group runs the ranks one after another) would otherwise read the new sums.
+// had_good: some step of the call ran; otherwise (pending, par) are the call's starting values.
+void comm_rollback(hakai_ctx* c, bool had_good, long long last_good, bool pending, int par) {
+    Comm* m = c->comm;
+    if (!m) return;
+    if (had_good) {
+        m->pending = m->n_up + m->n_dn > 0;
+        m->pending_par = (int)(last_good & 1);
+    } else {
+        m->pending = pending;
+        m->pending_par = par;
+    }
 }
 
 const std::vector<int>* comm_dn_nodes(const hakai_ctx* c) { return c->comm ? &c->comm->h_dn : nullptr; }

@@ -78,6 +78,8 @@ struct PairParam {
 constexpr int kMaxXRanks = 64;
 struct XBlk {
     const char* p[kMaxXRanks];
+    int cap[kMaxXRanks];  // records rank q's block holds
+    int off[kMaxXRanks];  // prefix of cap: rank q's first slot in arrays over every rank's records
 };
 
 struct Xrank {
@@ -96,8 +98,15 @@ struct Xrank {
     size_t send_bytes[kNx] = {0, 0, 0};
     char* d_recv[kNx] = {nullptr, nullptr, nullptr};   // RCCL: [nranks] blocks
     size_t recv_bytes[kNx] = {0, 0, 0};
-    long long cap[kNx] = {0, 0, 0};   // records per rank block (the same on every rank)
+    // records per block: capq[x][q] for rank q's block, computed alike on every rank from the
+    // gathered counts (so every rank knows every block's size); cap[x] = their maximum
+    long long cap[kNx] = {0, 0, 0};
+    std::vector<long long> capq[kNx];
+    std::vector<int> hist[kNx];       // [q][kHist] recent gathered counts of each rank (the headroom window)
+    int hist_pos = 0;
+    static constexpr int kHist = 16;
     long long cap_max[kNx] = {0, 0, 0};
+    long long cap_floor[kNx] = {1024, 256, 256};  // smallest capacity (tuning contact_exchange_*)
     hipEvent_t ev_sent[kNx][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
     bool full_del = true;             // the next deletion block carries every local deletion step
     // partial pair boxes of this rank, by parity (in-process peers read them), and the combined boxes
@@ -1539,12 +1548,12 @@ __global__ void k_ev_pack(unsigned int* ctl, const unsigned int* evs, long long 
 // rank prefix of the blocks' record counts in LDS (each clamped to the block capacity); block 0
 // publishes the event total
 __device__ __forceinline__ long long rank_prefix(unsigned int* ctl, const int4* s_h, int nr, long long* s_off,
-                                                 long long cap, bool publish) {
+                                                 const int* cap, bool publish) {
     if (threadIdx.x == 0) {
         long long run = 0;
         for (int q = 0; q < nr; ++q) {
             s_off[q] = run;
-            run += min((long long)s_h[q].x, cap);
+            run += min(s_h[q].x, cap[q]);
         }
         s_off[nr] = run;
         if (publish && blockIdx.x == 0) {
@@ -1569,13 +1578,13 @@ __device__ __forceinline__ const EvRec* rank_ev(const XBlk& xb, const long long*
 
 // any rank's block over its capacity or flagged: poison step pstep on every rank (all read the same
 // headers); xctl records which exchange (bit) for the retry
-__device__ __forceinline__ void x_overflow_check(const int4* s_h, int nr, long long cap, int* poison, int pstep,
+__device__ __forceinline__ void x_overflow_check(const int4* s_h, int nr, const int* cap, int* poison, int pstep,
                                                  int* xctl, int bit) {
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         bool local = false, over = false;  // a rank's own buffers overflowed / the exchange block
         for (int q = 0; q < nr; ++q) {
             local |= s_h[q].y != 0;
-            over |= (long long)s_h[q].x > cap;
+            over |= s_h[q].x > cap[q];
         }
         if (over) atomicOr(xctl, bit);
         if (over || local) {
@@ -1603,7 +1612,7 @@ __device__ __forceinline__ void x_counts(const int4* s_h, int nr, int x, int* xc
 // every rank's events; only the terms of this rank's nodes (g2l >= 0) are counted and summed
 // (also the reset's share of phase B: the previous step's touched nodes' forces back to 0 -- the
 // nodal update of that step has read them -- and the term counter)
-__global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, const int* g2l, int* cnt, int* touched,
+__global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, int nr, const int* g2l, int* cnt, int* touched,
                              int* tpos, int tsel, int* poison, int pstep, int* xctl, int* hc, const int* touched_prev,
                              double* fext) {
     __shared__ long long s_off[kMaxXRanks + 1];
@@ -1620,9 +1629,9 @@ __global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, 
         if (blockIdx.x == 0 && threadIdx.x == 0) ctl[kTerms] = 0;
     }
     load_hdrs(xb, nr, s_h);
-    x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 4);
+    x_overflow_check(s_h, nr, xb.cap, poison, pstep, xctl, 4);
     x_counts(s_h, nr, 2, xctl, hc);
-    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, cap, true);
+    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, xb.cap, true);
     for (long long e0 = blockIdx.x * (long long)blockDim.x; e0 < n; e0 += (long long)gridDim.x * blockDim.x) {
         const long long e = e0 + threadIdx.x;
         int node = -1;
@@ -1639,13 +1648,13 @@ __global__ void k_ct_count_g(unsigned int* ctl, XBlk xb, long long cap, int nr, 
     }
 }
 
-__global__ void k_ct_scatter_g(XBlk xb, long long cap, int nr, const int* g2l, unsigned int* ctl, const int* toff,
+__global__ void k_ct_scatter_g(XBlk xb, int nr, const int* g2l, unsigned int* ctl, const int* toff,
                                const int* tpos, int* cnt, double* terms) {
 #pragma clang fp contract(off)
     __shared__ long long s_off[kMaxXRanks + 1];
     __shared__ int4 s_h[kMaxXRanks];
     load_hdrs(xb, nr, s_h);
-    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, cap, false);
+    const long long n = 4 * rank_prefix(ctl, s_h, nr, s_off, xb.cap, false);
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
         const EvRec* r = rank_ev(xb, s_off, nr, e >> 2);
@@ -1704,7 +1713,7 @@ __global__ void k_xr_dpack(const int* del_step, const int* del_any, int nEloc, l
 // the deletion list of the live-list update (k_ct_find_del's job on one GPU), and block 0 sets the
 // update flag (after k_ct_reset, which clears the list). A full block comes with a full rebuild
 // of the live lists on every rank (state reset, upload, overflow retry), which needs no list.
-__global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del, long long nE_g,
+__global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, int* g_del, long long nE_g,
                              int* poison, int t, int* xctl, int* hc, unsigned int* ctl, int* dlist) {
     const int q = (int)blockIdx.y;
     const char* b = xb.p[q];
@@ -1717,7 +1726,7 @@ __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long 
         for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < ne; k += (long long)gridDim.x * blockDim.x)
             g_del[e0 + k] = pl[k];
     } else {
-        const long long n = min((long long)s_h[q].x, cap);
+        const long long n = min(s_h[q].x, xb.cap[q]);
         for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n;
              k += (long long)gridDim.x * blockDim.x) {
             const int e = pl[2 * k], d = pl[2 * k + 1];
@@ -1730,7 +1739,7 @@ __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long 
         bool over = false;
         for (int r = 0; r < nr; ++r) {
             mx = max(mx, s_h[r].z);
-            over |= !s_h[r].w && (long long)s_h[r].x > cap;
+            over |= !s_h[r].w && s_h[r].x > xb.cap[r];
         }
         g_del[nE_g + 1] = mx;
         ctl[kDel] = (ctl[kDirty] == 0 && mx == t - 1) ? 1u : 0u;
@@ -1752,7 +1761,7 @@ __global__ void k_xr_dunpack(XBlk xb, int nr, const long long* e_off, long long 
 // element, the append took 35-63 µs on C4's deletion steps against 15-18 µs for the grid). A rank's
 // block that is full (a peer out of step) is unpacked too. The previous step's touched forces and the term counter are
 // phase B's (k_ct_count_g), the touched counter the previous k_ct_sum's.
-__global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long long* e_off, long long cap, int* g_del,
+__global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long long* e_off, int* g_del,
                                                    long long nE_g, int* poison, int t, int* xctl, int* hc,
                                                    unsigned int* ctl, int* dlist, unsigned long long* bbox,
                                                    int npairs, unsigned int* evs, unsigned int* ccnt, int* zero_hdr) {
@@ -1770,7 +1779,7 @@ __global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long l
         bool over = false;
         for (int r = 0; r < nr; ++r) {
             mx = max(mx, s_h[r].z);
-            over |= !s_h[r].w && (long long)s_h[r].x > cap;
+            over |= !s_h[r].w && s_h[r].x > xb.cap[r];
         }
         g_del[nE_g + 1] = mx;
         ctl[kEv] = 0;
@@ -1796,7 +1805,7 @@ __global__ __launch_bounds__(1024) void k_xr_front(XBlk xb, int nr, const long l
             const long long e0 = e_off[q], ne = e_off[q + 1] - e0;
             for (long long k = tid; k < ne; k += bd) g_del[e0 + k] = pl[k];
         } else {
-            const long long n = min((long long)s_h[q].x, cap);
+            const long long n = min(s_h[q].x, xb.cap[q]);
             for (long long k = tid; k < n; k += bd) {
                 const int e = pl[2 * k], d = pl[2 * k + 1];
                 g_del[e] = d;
@@ -1887,17 +1896,17 @@ __global__ __launch_bounds__(kB) void k_xr_bin(StepIn s, const Seg* segs, int ns
     }
 }
 
-// A3: every gathered record (rank q's record k at slot q * cap + k of the bucket list) pushed onto
+// A3: every gathered record (rank q's record k at slot xb.off[q] + k of the bucket list) pushed onto
 // its bucket's chain; xctl bit 2 and the poison when a rank binned more than its block holds
 // (workgroup bx of gbx over rank q's block)
-__device__ __forceinline__ void insert_body(int bx, int gbx, int q, XBlk xb, int nr, long long cap,
+__device__ __forceinline__ void insert_body(int bx, int gbx, int q, const XBlk& xb, int nr,
                                             const PairParam* par, const unsigned int* ctl, unsigned long long* head,
                                             BEnt* blist, BVel* bvel, int* poison, int pstep, int* xctl, int* hc) {
     __shared__ int4 s_h[kMaxXRanks];
     load_hdrs(xb, nr, s_h);
-    x_overflow_check(s_h, nr, cap, poison, pstep, xctl, 2);
+    x_overflow_check(s_h, nr, xb.cap, poison, pstep, xctl, 2);
     x_counts(s_h, nr, 1, xctl, hc);
-    const long long n = min((long long)s_h[q].x, cap);
+    const long long n = min(s_h[q].x, xb.cap[q]);
     const unsigned seq = ctl[kSeq];
     const uint4* rec = reinterpret_cast<const uint4*>(xb.p[q] + kXHdr);  // 6 x 16 B per record
     for (long long k = bx * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gbx * blockDim.x) {
@@ -1908,7 +1917,7 @@ __device__ __forceinline__ void insert_body(int bx, int gbx, int q, XBlk xb, int
         const PairParam& pp = par[(int)w[1].w];  // BEnt: m[3] = w0.xy w0.zw w1.xy, node w1.z, pad w1.w
         const int b = pp.hash_off + (int)(hash3(ll2(w[0].x, w[0].y), ll2(w[0].z, w[0].w), ll2(w[1].x, w[1].y)) &
                                           (unsigned)(pp.hash_size - 1));
-        const int slot = (int)(q * cap + k);
+        const int slot = xb.off[q] + (int)k;
         const unsigned long long old = atomicExch(&head[b], ((unsigned long long)seq << 32) | (unsigned)slot);
         const long long nx = (unsigned)(old >> 32) == seq ? (long long)(unsigned)old : -1LL;
         w[3].z = (unsigned)(unsigned long long)nx;  // BEnt::next, the last 8 B
@@ -1922,15 +1931,15 @@ __device__ __forceinline__ void insert_body(int bx, int gbx, int q, XBlk xb, int
     }
 }
 
-__global__ void k_xr_insert(XBlk xb, int nr, long long cap, const PairParam* par, const unsigned int* ctl,
+__global__ void k_xr_insert(XBlk xb, int nr, const PairParam* par, const unsigned int* ctl,
                             unsigned long long* head, BEnt* blist, BVel* bvel, int* poison, int pstep, int* xctl,
                             int* hc) {
-    insert_body(blockIdx.x, gridDim.x, blockIdx.y, xb, nr, cap, par, ctl, head, blist, bvel, poison, pstep, xctl, hc);
+    insert_body(blockIdx.x, gridDim.x, blockIdx.y, xb, nr, par, ctl, head, blist, bvel, poison, pstep, xctl, hc);
 }
 
 // A3 with the triangle prefilter in the same launch (workgroups [0, gb * nr) insert, the rest
 // filter: independent work, side by side)
-__global__ __launch_bounds__(kB) void k_xr_insfilter(XBlk xb, int nr, long long cap, const PairParam* par,
+__global__ __launch_bounds__(kB) void k_xr_insfilter(XBlk xb, int nr, const PairParam* par,
                                                      const unsigned int* ctl, unsigned long long* head, BEnt* blist,
                                                      BVel* bvel, int* poison, int pstep, int* xctl, int* hc, int gb,
                                                      StepIn s, const int* tri_cnt, const int* tri_live,
@@ -1939,7 +1948,7 @@ __global__ __launch_bounds__(kB) void k_xr_insfilter(XBlk xb, int nr, long long 
                                                      long long cshard_cap, uint2* item) {
     const int ni = gb * nr;
     if ((int)blockIdx.x < ni)
-        insert_body(blockIdx.x % gb, gb, blockIdx.x / gb, xb, nr, cap, par, ctl, head, blist, bvel, poison, pstep,
+        insert_body(blockIdx.x % gb, gb, blockIdx.x / gb, xb, nr, par, ctl, head, blist, bvel, poison, pstep,
                     xctl, hc);
     else
         tri_filter_body(blockIdx.x - ni, gridDim.x - ni, s, tri_cnt, tri_live, tri_pair, tri_nodes, tri_ele, par, bbox,
@@ -2127,30 +2136,62 @@ void contact_destroy(hakai_ctx* c) {
 
 // ---- multi-GPU exchange (Xrank) ------------------------------------------------------------------
 static size_t xr_rec_bytes(int x) { return x == 0 ? 8 : (x == 1 ? sizeof(BRec) : sizeof(EvRec)); }
-// block bytes of exchange x at the current capacity (deletions: also room for a full block)
-static size_t xr_blk(const Xrank* X, int x, bool full = false) {
-    size_t b = kXHdr + xr_rec_bytes(x) * (size_t)X->cap[x];
+// block bytes of rank q's block of exchange x at its capacity (deletions, full: room for every local
+// deletion step of the largest rank)
+static size_t xr_blkq(const Xrank* X, int x, int q, bool full = false) {
+    size_t b = kXHdr + xr_rec_bytes(x) * (size_t)X->capq[x][q];
     if (x == 0 && full) b = kXHdr + 4 * (size_t)X->maxEloc;
     return (b + 15) / 16 * 16;
 }
-static size_t xr_alloc_blk(const Xrank* X, int x) {
-    return x == 0 ? std::max(xr_blk(X, 0, false), xr_blk(X, 0, true)) : xr_blk(X, x);
+static size_t xr_alloc_blk(const Xrank* X, int x, int q) {
+    return x == 0 ? std::max(xr_blkq(X, 0, q, false), xr_blkq(X, 0, q, true)) : xr_blkq(X, x, q);
+}
+// every rank's block bytes and their offsets in the receive buffer
+static size_t xr_layout(const Xrank* X, int x, bool full, size_t* bytes, size_t* off) {
+    size_t run = 0;
+    for (int q = 0; q < X->nranks; ++q) {
+        bytes[q] = xr_blkq(X, x, q, full);
+        off[q] = run;
+        run += bytes[q];
+    }
+    return run;
+}
+// records of the largest block / of all blocks of exchange x
+static void xr_cap_sums(Xrank* X, int x) {
+    long long mx = 0;
+    for (long long v : X->capq[x]) mx = std::max(mx, v);
+    X->cap[x] = mx;
+}
+static long long xr_cap_total(const Xrank* X, int x) {
+    long long t = 0;
+    for (long long v : X->capq[x]) t += v;
+    return t;
 }
 
 // send (both parities) and receive buffers for the current capacities; bucket-record and
-// bucket-list arrays for the binned records of all ranks
+// bucket-list arrays for the binned records of all ranks. Capacities may shrink (xr_grow); a
+// buffer is reallocated only when a capacity outgrows it, then with 1.25x room (a reallocation
+// synchronises the device).
 static int xr_buffers(hakai_ctx* c) {
     Contact* C = c->contact;
     Xrank* X = C->xr;
+    const int nr = X->nranks, me = X->rank;
     bool sync = false;
-    for (int x = 0; x < Xrank::kNx; ++x)
-        sync |= X->send_bytes[x] < xr_alloc_blk(X, x) || (comm_is_rccl(c) && X->recv_bytes[x] < (size_t)X->nranks * xr_alloc_blk(X, x));
-    sync |= C->blist_cap < (long long)X->nranks * X->cap[1];
+    size_t need_send[Xrank::kNx], need_recv[Xrank::kNx];
+    for (int x = 0; x < Xrank::kNx; ++x) {
+        need_send[x] = xr_alloc_blk(X, x, me);
+        need_recv[x] = 0;
+        for (int q = 0; q < nr; ++q) need_recv[x] += xr_alloc_blk(X, x, q);
+        sync |= X->send_bytes[x] < need_send[x] || (comm_is_rccl(c) && X->recv_bytes[x] < need_recv[x]);
+    }
+    const long long nb = xr_cap_total(X, 1);
+    sync |= C->blist_cap < nb;
     if (!sync) return 0;
     HIPCHK(hipDeviceSynchronize());  // (in-process peers read the send blocks)
+    auto room = [](size_t b) { return (b + b / 4 + 15) / 16 * 16; };
     for (int x = 0; x < Xrank::kNx; ++x) {
-        const size_t b = xr_alloc_blk(X, x);
-        if (X->send_bytes[x] < b) {
+        if (X->send_bytes[x] < need_send[x]) {
+            const size_t b = room(need_send[x]);
             for (int p = 0; p < 2; ++p) {
                 dfree(X->d_send[x][p]);
                 HIPCHK(dalloc(&X->d_send[x][p], b));
@@ -2158,40 +2199,52 @@ static int xr_buffers(hakai_ctx* c) {
             }
             X->send_bytes[x] = b;
         }
-        if (comm_is_rccl(c) && X->recv_bytes[x] < (size_t)X->nranks * b) {
+        if (comm_is_rccl(c) && X->recv_bytes[x] < need_recv[x]) {
+            const size_t b = room(need_recv[x]);
             dfree(X->d_recv[x]);
-            HIPCHK(dalloc(&X->d_recv[x], (size_t)X->nranks * b));
-            X->recv_bytes[x] = (size_t)X->nranks * b;
+            HIPCHK(dalloc(&X->d_recv[x], b));
+            X->recv_bytes[x] = b;
         }
     }
-    const long long nb = (long long)X->nranks * X->cap[1];
     if (C->blist_cap < nb) {
+        const long long n = nb + nb / 4;
         dfree(C->d_blist);
         dfree(C->d_bvel);
-        HIPCHK(dalloc(&C->d_blist, (size_t)nb));
-        HIPCHK(dalloc(&C->d_bvel, (size_t)nb));
-        C->blist_cap = nb;
+        HIPCHK(dalloc(&C->d_blist, (size_t)n));
+        HIPCHK(dalloc(&C->d_bvel, (size_t)n));
+        C->blist_cap = n;
     }
     return 0;
 }
 
-// the blocks of exchange x, parity par, of every rank: gathered over RCCL into the receive buffer,
-// or read in place from the in-process peers (after a stream wait on their "sent" event)
-static int xr_gather(hakai_ctx* c, int x, int par, size_t blk, XBlk& xb) {
+// the blocks of exchange x, parity par, of every rank: gathered over RCCL into the receive buffer
+// (one grouped send/receive per peer, each block at its own rank's size), or read in place from the
+// in-process peers (after a stream wait on their "sent" event); with every block's capacity and
+// slot offset
+static int xr_gather(hakai_ctx* c, int x, int par, bool full, XBlk& xb) {
     Xrank* X = c->contact->xr;
-    if (X->nranks > kMaxXRanks) return fail(HAKAI_ERR_COMM, "multi-GPU contact: more than %d ranks", kMaxXRanks);
+    const int nr = X->nranks;
+    if (nr > kMaxXRanks) return fail(HAKAI_ERR_COMM, "multi-GPU contact: more than %d ranks", kMaxXRanks);
+    long long run = 0;
+    for (int q = 0; q < nr; ++q) {
+        xb.cap[q] = (int)X->capq[x][q];
+        xb.off[q] = (int)run;
+        run += X->capq[x][q];
+    }
     if (comm_is_rccl(c)) {
-        if (int rc = comm_allgather_raw(c, X->d_send[x][par], X->d_recv[x], blk)) return rc;
-        for (int q = 0; q < X->nranks; ++q) xb.p[q] = X->d_recv[x] + (size_t)q * blk;
+        size_t bytes[kMaxXRanks], off[kMaxXRanks];
+        xr_layout(X, x, full, bytes, off);
+        if (int rc = comm_allgatherv_raw(c, X->d_send[x][par], X->d_recv[x], bytes, off)) return rc;
+        for (int q = 0; q < nr; ++q) xb.p[q] = q == X->rank ? X->d_send[x][par] : X->d_recv[x] + off[q];
         return 0;
     }
-    for (int q = 0; q < X->nranks; ++q) {
+    for (int q = 0; q < nr; ++q) {
         hakai_ctx* pc = comm_peer_ctx(c, q);
         Xrank* P = pc && pc->contact ? pc->contact->xr : nullptr;
         // the peer packed this step's block: deletions at the end of the previous step (seq), bins in
         // this step's A2 (same seq and step), events in this step's A3 (same A3 count; a peer may have
         // ended the step already)
-        const bool same = P && P->cap[x] == X->cap[x] &&
+        const bool same = P && P->capq[x] == X->capq[x] &&
                           (x == 0 ? P->seq == X->seq
                                   : x == 1 ? P->seq == X->seq && P->t_a == X->t_a : P->phase_a == X->phase_a);
         if (!same)
@@ -2212,28 +2265,44 @@ static int xr_dpack(hakai_ctx* c, bool full) {
     const int n = (int)std::max<long long>(X->nEloc, 1);
     hipLaunchKernelGGL(k_xr_dpack, dim3((unsigned)std::min((n + kB - 1) / kB, 1024)), dim3(kB), 0, c->stream,
                        c->d_del_step, c->d_del_step + c->nEp + 1, (int)X->nEloc, X->E0, X->d_last_del,
-                       X->d_send[0][par], X->d_send[0][1 - par], X->cap[0], full ? 1 : 0, X->t_a);
+                       X->d_send[0][par], X->d_send[0][1 - par], X->capq[0][X->rank], full ? 1 : 0, X->t_a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(X->ev_sent[0][par], c->stream));
     X->full_del = full;
     return 0;
 }
 
-// capacities from the counts gathered two steps ago (the same numbers on every rank, so every rank
-// sizes its collectives alike): a count past half a capacity doubles it (at least 4x the count), up
-// to the largest possible. Exchange x in [x0, x1): the deletion block grows before it is packed
-// (end of a step), the bin and event blocks at the start of the step that packs them -- never
-// while an in-process peer may still read the block of the step before.
+// Capacity of a block from its rank's recent counts: 1.25x the largest of the last kHist gathered
+// counts plus a floor of records (the counts are two steps old when read: a burst beyond the
+// headroom overflows, and the step runs again with the capacity grown past it, contact_after_overflow).
+// Deletion blocks (8 B records, bursts at deletion waves) keep a floor of 1024 records.
+static long long xr_cap_target(const Xrank* X, int x, long long mx) {
+    return std::min<long long>(X->cap_max[x], std::max<long long>(X->cap_floor[x], mx + mx / 4 + (mx > 0 ? 32 : 0)));
+}
+// Capacities from the counts gathered two steps ago (the same numbers on every rank, so every rank
+// sizes every block alike): a rank's block grows to its target at once and shrinks to it once it
+// exceeds 1.5x the target (the headroom window keeps a recent burst's size). Exchange x in [x0, x1):
+// the deletion block changes before it is packed (end of a step), the bin and event blocks at the
+// start of the step that packs them -- never while an in-process peer may still read the block of
+// the step before.
 static int xr_grow(hakai_ctx* c, int x0, int x1) {
     Xrank* X = c->contact->xr;
     if (X->cnt_seq < 2) return 0;
     const long long sl = (X->cnt_seq - 2) & 3;
     HIPCHK(hipEventSynchronize(X->ev_cnt[sl]));
     const int* h = X->h_cnt + (size_t)sl * Xrank::kNx * X->nranks;
+    const int nr = X->nranks, H = Xrank::kHist;
     for (int x = x0; x < x1; ++x) {
-        long long mx = 0;
-        for (int q = 0; q < X->nranks; ++q) mx = std::max<long long>(mx, h[x * X->nranks + q]);
-        if (2 * mx > X->cap[x]) X->cap[x] = std::min(X->cap_max[x], std::max(2 * X->cap[x], 4 * mx));
+        for (int q = 0; q < nr; ++q) {
+            int* hq = X->hist[x].data() + (size_t)q * H;
+            hq[(X->cnt_seq - 2) % H] = h[x * nr + q];
+            long long mx = 0;
+            for (int j = 0; j < H; ++j) mx = std::max<long long>(mx, hq[j]);
+            const long long tg = xr_cap_target(X, x, mx);
+            long long& cq = X->capq[x][q];
+            if (tg > cq || 2 * cq > 3 * tg) cq = tg;
+        }
+        xr_cap_sums(X, x);
     }
     return xr_buffers(c);
 }
@@ -2317,7 +2386,7 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
         X->t_a = in.t;
         X->par_a = (int)(X->seq & 1);
         X->sl_a = (int)(X->cnt_seq & 3);
-        if (int rc = xr_gather(c, 0, X->par_a, xr_blk(X, 0, X->full_del), xb)) return rc;
+        if (int rc = xr_gather(c, 0, X->par_a, X->full_del, xb)) return rc;
         del_step = X->g_del;
         del_any = X->g_del + X->nE_g + 1;
         bbox = X->d_box[X->par_a];
@@ -2342,7 +2411,7 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
                            C->ntile > 0 ? 1 : 0);
     } else if (X && !rebuild) {
         // multi-GPU: the reset's share and every rank's deletions in one workgroup, then the append
-        hipLaunchKernelGGL(k_xr_front, dim3(1), dim3(1024), 0, s, xb, X->nranks, X->d_eoff, X->cap[0], X->g_del,
+        hipLaunchKernelGGL(k_xr_front, dim3(1), dim3(1024), 0, s, xb, X->nranks, X->d_eoff, X->g_del,
                            X->nE_g, c->d_poison, in.t, X->d_xctl, X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks,
                            C->d_ctl, C->d_dlist, bbox, C->npairs, C->d_evs, C->d_ccnt, (int*)X->d_send[1][X->par_a]);
         if (C->ntile > 0)
@@ -2355,7 +2424,7 @@ static int step_start(hakai_ctx* c, double t, double d_time) {
         if (X) {  // the deletions of every rank (after the reset: they fill its deletion list)
             const unsigned gx = (unsigned)std::min<long long>(std::max<long long>((X->maxEloc + kB - 1) / kB, 1), 256);
             hipLaunchKernelGGL(k_xr_dunpack, dim3(gx, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks,
-                               X->d_eoff, X->cap[0], X->g_del, X->nE_g, c->d_poison, in.t, X->d_xctl,
+                               X->d_eoff, X->g_del, X->nE_g, c->d_poison, in.t, X->d_xctl,
                                X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks, C->d_ctl, C->d_dlist);
         }
         if (C->ntile > 0) {
@@ -2498,7 +2567,7 @@ static int xr_a2(hakai_ctx* c, double d_time) {
         StepIn in = step_in(c, X->t_a, d_time);
         hipLaunchKernelGGL(k_xr_bin, dim3((unsigned)std::max(1, C->nseg * C->g_seg)), dim3(kB), 0, s, in,
                            (const Seg*)C->d_seg, C->nseg, C->d_reg, C->d_ni_live, C->d_ni_pair, C->d_ni_node, C->d_par,
-                           xb, nxb, flip, C->npairs, X->d_boxg, X->d_send[1][par], X->cap[1], C->g_seg);
+                           xb, nxb, flip, C->npairs, X->d_boxg, X->d_send[1][par], X->capq[1][X->rank], C->g_seg);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(X->ev_sent[1][par], s));
@@ -2513,19 +2582,19 @@ static int xr_a3(hakai_ctx* c, double d_time) {
     hipStream_t s = c->stream;
     const int par = X->par_a;
     XBlk xb;
-    if (int rc = xr_gather(c, 1, par, xr_blk(X, 1), xb)) return rc;
+    if (int rc = xr_gather(c, 1, par, false, xb)) return rc;
     const unsigned gb = (unsigned)std::min<long long>(std::max<long long>((X->cap[1] + kB - 1) / kB, 1), 128);
     int* hc = X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * X->nranks;
     StepIn in = step_in(c, X->t_a, d_time);
     if (C->n_tri > 0 && C->fuse_binfilter) {  // insert and prefilter side by side
         hipLaunchKernelGGL(k_xr_insfilter, dim3(gb * (unsigned)X->nranks + filter_grid(C)), dim3(kB), 0, s, xb,
-                           X->nranks, X->cap[1], C->d_par, C->d_ctl, C->d_head, C->d_blist, C->d_bvel, c->d_poison,
+                           X->nranks, C->d_par, C->d_ctl, C->d_head, C->d_blist, C->d_bvel, c->d_poison,
                            X->t_a, X->d_xctl, hc, (int)gb, in, C->d_reg + 2 * C->tri_reg + 1, C->d_tri_live,
                            C->d_tri_pair, C->d_tri_nodes, C->d_tri_ele, X->d_boxg, C->d_ccnt, (TriRec*)C->d_cand,
                            C->cshard_cap, C->small ? nullptr : C->d_item);
         tri_search(c, in);
     } else {
-        hipLaunchKernelGGL(k_xr_insert, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks, X->cap[1],
+        hipLaunchKernelGGL(k_xr_insert, dim3(gb, (unsigned)X->nranks), dim3(kB), 0, s, xb, X->nranks,
                            C->d_par, C->d_ctl, C->d_head, C->d_blist, C->d_bvel, c->d_poison, X->t_a, X->d_xctl, hc);
         if (C->n_tri > 0) {
             tri_prefilter(c, in, X->d_boxg);
@@ -2533,7 +2602,7 @@ static int xr_a3(hakai_ctx* c, double d_time) {
         }
     }
     hipLaunchKernelGGL(k_ev_pack, dim3((unsigned)C->g_ev), dim3(kB), 0, s, C->d_ctl, C->d_evs, C->cap / kEvShards,
-                       C->d_ev_nodes, C->d_ev_f, X->d_send[2][par], X->cap[2]);
+                       C->d_ev_nodes, C->d_ev_f, X->d_send[2][par], X->capq[2][X->rank]);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(X->ev_sent[2][par], s));
     ++X->phase_a;
@@ -2568,15 +2637,15 @@ int contact_step_b(hakai_ctx* c) {
     hipStream_t s = c->stream;
     const int par = X->par_a, nr = X->nranks;
     XBlk xb;
-    if (int rc = xr_gather(c, 2, par, xr_blk(X, 2), xb)) return rc;
+    if (int rc = xr_gather(c, 2, par, false, xb)) return rc;
     const int tsel = C->tsel;
     const unsigned ge = (unsigned)C->g_ev;
-    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, X->cap[2], nr, X->d_g2l, C->d_cnt,
+    hipLaunchKernelGGL(k_ct_count_g, dim3(ge), dim3(kB), 0, s, C->d_ctl, xb, nr, X->d_g2l, C->d_cnt,
                        C->d_touched[tsel], C->d_tpos, tsel, c->d_poison, X->t_a, X->d_xctl,
                        X->d_hcnt + (size_t)X->sl_a * Xrank::kNx * nr, C->d_touched[1 - tsel], c->d_fext);
     hipLaunchKernelGGL(k_ct_alloc, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_cnt, C->d_toff,
                        C->d_tcnt);
-    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, X->cap[2], nr, X->d_g2l, C->d_ctl, C->d_toff,
+    hipLaunchKernelGGL(k_ct_scatter_g, dim3(ge), dim3(kB), 0, s, xb, nr, X->d_g2l, C->d_ctl, C->d_toff,
                        C->d_tpos, C->d_cnt, C->d_terms);
     hipLaunchKernelGGL(k_ct_sum, dim3(C->g_node), dim3(kB), 0, s, C->d_ctl, tsel, C->d_touched[tsel], C->d_toff, C->d_tcnt,
                        C->d_terms, c->d_fext, X->d_g2l);
@@ -2619,9 +2688,14 @@ void contact_after_overflow(hakai_ctx* c, long long steps_since_reset) {
         X->retry = false;
         if (xc[0] & 7) {  // past the largest count of the call (its steps after the poisoned one included)
             for (int x = 0; x < Xrank::kNx; ++x) {
-                long long mx = 0;
-                for (int q = 0; q < nr; ++q) mx = std::max<long long>(mx, xc[4 + (Xrank::kNx + x) * nr + q]);
-                if (xc[0] & (1 << x)) X->cap[x] = std::min(X->cap_max[x], std::max(2 * X->cap[x], 4 * mx));
+                if (!(xc[0] & (1 << x))) continue;
+                for (int q = 0; q < nr; ++q) {  // every block past its rank's largest count of the call
+                    const long long mx = xc[4 + (Xrank::kNx + x) * nr + q];
+                    X->capq[x][q] = std::max(X->capq[x][q], xr_cap_target(X, x, mx));
+                    int* hq = X->hist[x].data() + (size_t)q * Xrank::kHist;  // (kept by the window)
+                    for (int j = 0; j < Xrank::kHist; ++j) hq[j] = std::max<int>(hq[j], (int)std::min<long long>(mx, 1 << 30));
+                }
+                xr_cap_sums(X, x);
             }
             X->retry = true;
         }
@@ -2691,7 +2765,9 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         const int x = key[17] == 'd' ? 0 : (key[17] == 'b' ? 1 : 2);
         if (value < 1 || value > (1LL << 28)) return fail(HAKAI_ERR_ARG, "%s out of range", key);
         HIPCHK(hipDeviceSynchronize());
-        X->cap[x] = std::min<long long>(value, X->cap_max[x]);
+        for (auto& v : X->capq[x]) v = std::min<long long>(value, X->cap_max[x]);
+        X->cap_floor[x] = value;  // (the capacities then follow the counts from there)
+        xr_cap_sums(X, x);
         if (int rc = xr_buffers(c)) return rc;
         // the next step's deletion block again, in the new layout (a full block: every rank
         // rebuilds its live lists)
@@ -2720,7 +2796,8 @@ int contact_tuning(hakai_ctx* c, const char* key, long long value) {
         C->tcap = std::min<long long>(C->nN, 4 * C->cap);
         if (Xrank* X = C->xr) {  // the event block can hold at most the event buffer
             X->cap_max[2] = C->cap;
-            X->cap[2] = std::min(X->cap[2], C->cap);
+            for (auto& v : X->capq[2]) v = std::min(v, C->cap);
+            xr_cap_sums(X, 2);
         }
         HIPCHK(dalloc(&C->d_ev_nodes, 4 * (size_t)C->cap));
         HIPCHK(dalloc(&C->d_ev_f, 3 * (size_t)C->cap));
@@ -3221,9 +3298,14 @@ int xr_build(hakai_ctx* c, const OwnFilter& own, long long nNode, long long nEle
     X->cap_max[0] = X->maxEloc;
     X->cap_max[1] = nimax;
     X->cap_max[2] = C->cap;
-    X->cap[0] = std::min<long long>(X->cap_max[0], 1024);
-    X->cap[1] = std::min<long long>(X->cap_max[1], std::max<long long>(4096, ci0 / (8 * nr)));
-    X->cap[2] = std::min<long long>(X->cap_max[2], 4096);
+    const long long cap0[hkc::Xrank::kNx] = {std::min<long long>(X->cap_max[0], 1024),
+                                        std::min<long long>(X->cap_max[1], std::max<long long>(4096, ci0 / (8 * nr))),
+                                        std::min<long long>(X->cap_max[2], 4096)};
+    for (int x = 0; x < hkc::Xrank::kNx; ++x) {
+        X->capq[x].assign((size_t)nr, cap0[x]);
+        X->hist[x].assign((size_t)nr * hkc::Xrank::kHist, 0);
+        xr_cap_sums(X, x);
+    }
     std::vector<int> l2g((size_t)c->nN);
     for (long long l = 0; l < c->nN; ++l) l2g[l] = (int)(local_node_global[l] - 1);
     std::vector<double> gmass((size_t)nNode);
@@ -3422,13 +3504,22 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
     const int64_t v[7] = {ctl[kEv], ctl[kEvMax], ctl[kNcand], ctl[kTouched + C->tsel], 0, 0, 0};
     for (int r = 0; r < C->nreg; ++r) live[C->reg_list_h[r]] += reg[2 * r + 1];
     for (int k = 0; k < cap && k < 7; ++k) stats[k] = k < 4 ? v[k] : live[k == 4 ? 2 : k - 5];
-    if (cap > 7) {  // multi-GPU: contact-zone i-nodes all ranks binned in the last step, exchange bytes per rank
+    long long rec_bytes = 0;
+    if (cap > 7) {  // multi-GPU: contact-zone i-nodes all ranks binned in the last step; the bytes this
+                    // rank's exchanges receive per step (the other ranks' blocks at their capacities)
+                    // and the bytes of the records in them (headers + the last step's gathered counts)
         long long binned = 0, bytes = 0;
         if (hkc::Xrank* X = C->xr) {
-            std::vector<int> cnt((size_t)X->nranks);
-            HIPCHK(hipMemcpy(cnt.data(), X->d_xctl + 4 + X->nranks, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
-            for (int q : cnt) binned += q;
-            bytes = (long long)(hkc::xr_blk(X, 0) + hkc::xr_blk(X, 1) + hkc::xr_blk(X, 2));
+            const int nr = X->nranks;
+            std::vector<int> cnt((size_t)hkc::Xrank::kNx * nr);
+            HIPCHK(hipMemcpy(cnt.data(), X->d_xctl + 4, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+            for (int q = 0; q < nr; ++q) binned += cnt[(size_t)nr + q];
+            for (int x = 0; x < hkc::Xrank::kNx; ++x)
+                for (int q = 0; q < nr; ++q) {
+                    if (q == X->rank) continue;
+                    bytes += (long long)hkc::xr_blkq(X, x, q);
+                    rec_bytes += (long long)kXHdr + (long long)hkc::xr_rec_bytes(x) * cnt[(size_t)x * nr + q];
+                }
         }
         stats[7] = binned;
         if (cap > 8) stats[8] = bytes;
@@ -3441,6 +3532,7 @@ int hakai_contact_stats(hakai_ctx* c, int64_t* stats, int32_t cap) {
         for (int q = 0; q < kCandShards; ++q) nt += cc[(size_t)q * kShardStride + kTestWord];
         stats[10] = nt;
     }
+    if (cap > 11) stats[11] = rec_bytes;
     return 0;
 }
 

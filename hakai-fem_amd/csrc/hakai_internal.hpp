@@ -95,6 +95,7 @@ struct hakai_ctx {
     unsigned long long* d_negjac = nullptr;
     int* d_poison = nullptr;     // [2]: contact buffer overflow in this call (flag, step); see ElemArgs
     long long poison_step = -1;  // the step a contact overflow poisoned in the last failed call
+    long long exchange_retries = 0;  // steps run again after a multi-GPU contact exchange overflow
     bool any_plastic = false;
     bool model_ok = false;
     bool state_ok = false;
@@ -159,6 +160,8 @@ void prof_begin(hakai_ctx* c, int kernel, EventPair* p);
 void prof_end(hakai_ctx* c, EventPair* p);
 void comm_destroy(hakai_ctx* c);
 int comm_reset(hakai_ctx* c);
+void comm_pending_get(const hakai_ctx* c, bool* pending, int* par);
+void comm_rollback(hakai_ctx* c, bool had_good, long long last_good, bool pending, int par);
 // Multi-GPU hooks used by hakai_step (no-ops without a communicator).
 int comm_pre_nodal(hakai_ctx* c);                    // save u_pre of interface nodes
 int comm_post_nodal(hakai_ctx* c, double d_time);    // wait exchange, fix interface nodes
@@ -178,6 +181,7 @@ struct LocalGather {
 int gather_local(hakai_ctx* c, const LocalGather& g, int n, void* dst);
 // RCCL only, ordered on c->stream: recv[q*bytes ..] = rank q's send; recv = MIN over ranks (uint64)
 int comm_allgather_raw(hakai_ctx* c, const void* send, void* recv, size_t bytes);
+int comm_allgatherv_raw(hakai_ctx* c, const void* send, void* recv, const size_t* bytes, const size_t* off);
 int comm_allreduce_min_u64(hakai_ctx* c, const void* send, void* recv, size_t count);
 bool comm_is_rccl(const hakai_ctx* c);
 hakai_ctx* comm_peer_ctx(hakai_ctx* c, int q);                          // in-process group member q

@@ -153,11 +153,11 @@ class Solver:
     # -- contact ----------------------------------------------------------------------------------
     def contact_stats(self) -> dict:
         """Counters of the last contact step (hakai_contact_stats)."""
-        st = np.zeros(11, np.int64)
-        check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 11))
+        st = np.zeros(12, np.int64)
+        check(self.L.hakai_contact_stats(self.ctx, ptr(st, I64), 12))
         keys = ("events", "max_events", "candidate_triangles", "touched_nodes", "live_triangles", "live_nodes_i",
                 "live_nodes_j", "binned_contact_nodes", "exchange_bytes_per_rank", "hash_buckets",
-                "tested_triangles")
+                "tested_triangles", "exchange_record_bytes_per_rank")
         return {k: int(v) for k, v in zip(keys, st)}
 
     def contact_info(self):

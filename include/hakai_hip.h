@@ -124,7 +124,8 @@ int hakai_graph_steps(hakai_ctx* ctx, int64_t* n_steps);
  * entries for this mesh), "own_superbatch" (batches of 32 elements per LDS summing pass: 2, or 1
  * for wide meshes), "own_slots" (LDS running sums a block keeps open at most), "own_banded" (1: the
  * blocks walk row bands of a structured wide cross-section), "own_grid" (blocks of that schedule),
- * "own_round2" (summing passes that take a second entry per thread). */
+ * "own_round2" (summing passes that take a second entry per thread), "exchange_retries" (steps run
+ * again after a multi-GPU contact exchange block overflowed). */
 int hakai_stat(hakai_ctx* ctx, const char* key, int64_t* value);
 int hakai_sync(hakai_ctx* ctx);
 /* Deletions so far (v2/HAKAI_j.jl:733-736): count, and up to cap (step, element 1-based) pairs. */
@@ -246,10 +247,12 @@ int hakai_contact_info(hakai_ctx* ctx, int32_t* n_pairs, int64_t* info, int32_t 
  * max events in any step, prefiltered triangles, nodes with contact force, live triangles, live
  * i-node entries, live j-node entries (the last three = the lengths of the reference's c_triangles,
  * c_nodes_i, c_nodes_j summed over pairs, deleted elements' triangles included); multi-GPU only:
- * [7] contact-zone nodes all ranks binned in the last step, [8] bytes of one rank's per-step
- * exchange blocks at their capacities (hakai_set_contact_global); [9] hash-grid buckets of all pairs;
- * [10] live triangles the prefilter tested in full in the last step (those whose pair has a
- * non-empty range box; multi-GPU: this rank's). */
+ * [7] contact-zone nodes all ranks binned in the last step, [8] bytes this rank's exchanges receive
+ * per step (the other ranks' deletion, bin and event blocks, each at its rank's capacity;
+ * hakai_set_contact_global); [9] hash-grid buckets of all pairs; [10] live triangles the prefilter
+ * tested in full in the last step (those whose pair has a non-empty range box; multi-GPU: this
+ * rank's); [11] multi-GPU: bytes of the records in those blocks in the last step (headers + the
+ * gathered counts), what [8] would be with blocks sized exactly. */
 int hakai_contact_stats(hakai_ctx* ctx, int64_t* stats, int32_t cap);
 /* Probe: the contact force (3nN, = external_force of step t) at the current state, no step. */
 int hakai_contact_force(hakai_ctx* ctx, double t, double d_time, double* external_force);

@@ -274,6 +274,38 @@ def test_contact_group_exchange_capacities_grow(caps):
     assert sorted(dels) == gdel
 
 
+@pytest.mark.parametrize("chunk", [1, 300])
+def test_contact_group_deletion_exchange_overflow_retry_bitexact(chunk):
+    """The deletion block at its smallest capacity (1 record, capacities follow the counts from there
+    and shrink back after the burst): a deletion burst overflows it, the next step is poisoned on
+    every rank and runs again -- here at an even step, whose retry packs the interface sums into the
+    parity the rerun's peers must not read (the rolled-back exchange parity, hakai_comm.cpp
+    comm_rollback). Bit-identical to one context, one step per call and one call."""
+    from hakai import mesh
+    glob = mesh.two_body_model(plate=(16, 16, 8), impactor=(4, 4, 4), v=-3e5, d_time=2e-8, n_steps=300)
+    with Solver(glob) as sv:
+        sv.step(1, glob.n_steps)
+        g = sv.download()
+    gdiag, _ = glob.lumped_mass()
+    parts = [dist.range_partition(glob, r, 2, gdiag) for r in range(2)]
+    svs = []
+    for r, (loc, diag, iface, l2g, off) in enumerate(parts):
+        sv = Solver(loc, diag_M=diag)
+        sv.set_element_offset(loc.global_element_offset)
+        sv.comm_init_local(r, 2, 8180 + chunk)
+        sv.set_interface(*iface)
+        sv.set_contact_global(glob, l2g, off, gdiag)
+        sv.set_tuning("contact_exchange_deletions", 1)
+        svs.append(sv)
+    for t in range(1, glob.n_steps + 1, chunk):
+        step_group(svs, t, min(chunk, glob.n_steps + 1 - t))
+    assert min(sv.stat("exchange_retries") for sv in svs) >= 1
+    for sv, (loc, _, _, l2g, _) in zip(svs, parts):
+        st = sv.download()
+        assert np.array_equal(st.disp.reshape(-1, 3), g.disp.reshape(-1, 3)[l2g - 1])
+        sv.close()
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_multi_gpu_driver_writes_the_same_vtk(tmp_path, ranks):
     """HAKAI(fname) over ranks (hakai.run.hakai_multi, here as an in-process group): contact with

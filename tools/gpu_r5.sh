@@ -13,6 +13,8 @@
 #   sweep      tools/sweep.py --variants "$SWEEP" (CONFIG=c3|c4|c5slab) -> gpurun_out/r5_sweep.log
 #   diag       per-wave clock totals of the element kernel (variant DIAGLIB, -DHK_DIAG_WAVE) -> gpurun_out/r5_diag_*.jsonl
 #   rehearse4  python bench.py --gpus 4 self-launched on the one GPU (RCCL sockets) -> gpurun_out/r5_rehearse4.json
+#   ablib      LIBS="a b cur" alternating libraries (hakai-fem_amd/lib/variants/<a>.so) under tools/sweep.py
+#   contact    tools/bench_contact.py on C4: one context, 2/4 ranks with z- and x-slab ranges -> r5_contact_c4.jsonl
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r5_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -73,6 +75,13 @@ EOF
             done
         done
         grep -E "^==|element" gpurun_out/r5_ablib.log ;;
+    contact) : > gpurun_out/r5_contact_c4.jsonl  # C4 contact per rank: one context, 2 and 4 ranks (z- and x-slabs)
+        for spec in "1 0" "2 0" "4 0" "2 1" "4 1"; do
+            set -- $spec
+            run 600 gpurun_out/r5_contact_cur.log python tools/bench_contact.py --ranks $1 --x-slabs $2 \
+                --serial 2 --steps 40 || exit $?
+            grep '^{' gpurun_out/r5_contact_cur.log >> gpurun_out/r5_contact_c4.jsonl
+        done ;;
     rehearse4) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r5_rehearse4.json python bench.py --gpus 4 \
                    --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
     tests:*) run 1200 gpurun_out/r5_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
