@@ -25,6 +25,7 @@
 
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -2231,6 +2232,8 @@ static int xr_gather(hakai_ctx* c, int x, int par, bool full, XBlk& xb) {
         xb.off[q] = (int)run;
         run += X->capq[x][q];
     }
+    if (run > (long long)INT_MAX)  // (record slots and bucket-list indices are 32-bit)
+        return fail(HAKAI_ERR_STATE, "multi-GPU contact: %lld exchange records over the ranks exceed 2^31", run);
     if (comm_is_rccl(c)) {
         size_t bytes[kMaxXRanks], off[kMaxXRanks];
         xr_layout(X, x, full, bytes, off);
