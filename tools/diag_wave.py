@@ -23,7 +23,7 @@ from hakai.solver import Solver  # noqa: E402
 
 KW, NW = 8, 8192
 ap = argparse.ArgumentParser()
-ap.add_argument("--config", choices=("c3", "c5slab", "c4"), default="c3")
+ap.add_argument("--config", choices=("c3", "c5slab", "c5", "c4"), default="c3")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--preload", type=int, default=400)
 ap.add_argument("--modes", default="exact,fused")
@@ -39,6 +39,8 @@ if a.config == "c3":
     m = mesh.config_c3(v_end=5e5)
 elif a.config == "c5slab":
     m = mesh.config_c5(layers=200)
+elif a.config == "c5":
+    m = mesh.config_c5(layers=1600)
 else:
     m = mesh.config_c4()
 diag, _ = m.lumped_mass()
