@@ -998,7 +998,7 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
     const long long G = (long long)sc.bstart.size() - 1;
     if (G <= 0 || c->max_inc > 8 || c->h_ptr.size() != (size_t)nN + 1) return false;
     pl.S = S;
-    struct Ent { int target, slot, flags, n; int lanes[8]; };
+    struct Ent { int target, slot, flags, n; int lanes[8]; int inc[4]; };  // inc: an EXP entry's incidences
     // pos_of[b]: schedule position of batch b; block_of[b]; sb_pos[b] = position of the first batch
     // of b's super-batch (runs of S positions from each block's first), which indexes the lists
     std::vector<int> pos_of(nb), block_of(nb);
@@ -1046,7 +1046,7 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
         sg.s0 = -1;
         while (j < j1 && block_of[batch_of(j)] == hb) {  // the head segment, super-batch by super-batch
             const long long sb = sb_pos[batch_of(j)];
-            Ent en{(int)n, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+            Ent en{(int)n, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0}};
             while (j < j1 && sb_pos[batch_of(j)] == sb) {
                 if (en.n == 8) return false;
                 en.lanes[en.n++] = lane_of(j);
@@ -1070,14 +1070,50 @@ static bool own_plan(const hakai_ctx* c, const OwnSched& sc, int S, int slot_cap
     std::vector<int> row_of_inc(c->h_inc0.size(), -1);
     for (size_t q = 0; q < exports.size();) {
         const long long sb = exports[q].first;
-        Ent en{(int)rows, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
+        Ent en{0, 0, kOwnExpH, 0, {0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0}};
         while (q < exports.size() && exports[q].first == sb && en.n < kOwnExpRowsHost) {
             const int j = exports[q].second;
+            en.inc[en.n] = j;
             en.lanes[en.n++] = lane_of(j);
-            row_of_inc[j] = (int)rows++;
             ++q;
         }
         per[sb].push_back(en);
+    }
+    // Row numbers, coalesced by wave: the EXP entries of a super-batch that one wave of the pass
+    // takes (list positions in one 64-aligned window, a contiguous run: they follow the node
+    // entries) form a group of g entries with m <= 4 g contributions in export order (node, then
+    // element). Contribution q of the group goes to row base + q, dealt to entry q mod g as its
+    // (q / g)-th: so the wave's k-th stores cover g consecutive rows, and a node's rows stay
+    // consecutive for the nodal kernel. An entry's target is base + i, its stride g rides in the
+    // unused slot field.
+    for (long long b = 0; b < nb; ++b) {
+        std::vector<Ent>& v = per[b];
+        for (size_t p = 0; p < v.size();) {
+            if (!(v[p].flags & kOwnExpH)) {
+                ++p;
+                continue;
+            }
+            size_t p1 = p;
+            while (p1 < v.size() && (v[p1].flags & kOwnExpH) && p1 / 64 == p / 64) ++p1;
+            const int g = (int)(p1 - p);
+            std::vector<std::pair<int, int>> cs;  // (incidence, lane) in export order
+            for (size_t i = p; i < p1; ++i)
+                for (int k = 0; k < v[i].n; ++k) cs.emplace_back(v[i].inc[k], v[i].lanes[k]);
+            const int m = (int)cs.size();
+            for (int i = 0; i < g; ++i) {
+                Ent& en = v[p + (size_t)i];
+                en.target = (int)(rows + i);
+                en.slot = g;
+                en.n = 0;
+                for (int q = i; q < m; q += g) {
+                    en.inc[en.n] = cs[(size_t)q].first;
+                    en.lanes[en.n++] = cs[(size_t)q].second;
+                    row_of_inc[cs[(size_t)q].first] = (int)(rows + q);
+                }
+            }
+            rows += m;
+            p = p1;
+        }
     }
     // per node: its rows in element order (CSR rp / ridx)
     std::vector<int>& ridx = pl.ridx;

@@ -943,11 +943,13 @@ __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const doub
     const int slot = (en.y & 1023) | ((en.y >> 18) & 1024), flags = (en.y >> 10) & 15, n = (en.y >> 14) & 15;
     double* dump = a.own_dump + 8 * (long long)blockIdx.x;
     double v[3];
-    if (flags & (kOwnExp | kOwnNop)) {  // EXP: up to kOwnExpRows contributions -> rows target, target+1, ...
+    if (flags & (kOwnExp | kOwnNop)) {  // EXP: up to kOwnExpRows contributions -> rows target + j * stride
+        // (stride: the entry's group of EXP entries in this wave, in the slot field; consecutive
+        // lanes write consecutive rows, own_plan)
 #pragma unroll
         for (int j = 0; j < kOwnExpRows; ++j) {
             const int l = own_lane(en, j);
-            double* dst = ((flags & kOwnExp) && j < n) ? a.own_rows + 3 * ((long long)en.x + j) : dump;
+            double* dst = ((flags & kOwnExp) && j < n) ? a.own_rows + 3 * ((long long)en.x + (long long)j * slot) : dump;
 #pragma unroll
             for (int c = 0; c < 3; ++c) dst[c] = s_fe[3 * l + c];
         }

@@ -142,7 +142,7 @@ int main(int argc, char** argv) {
                 const int slot = (w[1] & 1023) | ((w[1] >> 18) & 1024), flags = (w[1] >> 10) & 15,
                           n = (w[1] >> 14) & 15;
                 if (flags & kOwnExpH) {
-                    for (int j = 0; j < n; ++j) rows[w[0] + j] = stage[lane_of(w, j)];
+                    for (int j = 0; j < n; ++j) rows[w[0] + (long long)j * slot] = stage[lane_of(w, j)];
                     continue;
                 }
                 if (flags & kOwnNopH) continue;
