@@ -10,6 +10,7 @@
 #              C3, both element modes, alternating 5 x 2 runs -> gpurun_out/r5_ab3.jsonl
 #   prof       rocprofv3 kernel trace of a short bench (MODE=fused|exact) -> gpurun_out/r5_prof_$MODE/
 #   sq         rocprofv3 SQ counters of the element kernel (MODE=fused|exact) -> gpurun_out/r5_sq_$MODE/
+#   lds        rocprofv3 LDS bank-conflict counters of the element kernel (MODE=fused|exact) -> gpurun_out/r5_lds_$MODE/
 #   sweep      tools/sweep.py --variants "$SWEEP" (CONFIG=c3|c4|c5slab) -> gpurun_out/r5_sweep.log
 #   diag       per-wave clock totals of the element kernel (variant DIAGLIB, -DHK_DIAG_WAVE) -> gpurun_out/r5_diag_*.jsonl
 #   rehearse4  python bench.py --gpus 4 self-launched on the one GPU (RCCL sockets) -> gpurun_out/r5_rehearse4.json
@@ -60,6 +61,10 @@ EOF
             SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
             -d $P -o run --output-format csv -- python bench.py --steps 10 --warmup 2 $BA --compare-fused 0 \
             --element-mode $M || exit $? ;;
+    lds) M=${MODE:-exact}; P=gpurun_out/r5_lds_$M; rm -rf $P
+        HAKAI_GRAPH=0 run 300 gpurun_out/r5_lds_$M.log timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT \
+            SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES -d $P -o run --output-format csv -- python bench.py --steps 10 \
+            --warmup 2 $BA --compare-fused 0 --element-mode $M || exit $? ;;
     sweep) run 900 gpurun_out/r5_sweep.log python tools/sweep.py --config ${CONFIG:-c3} --rounds ${ROUNDS:-5} \
                --variants "$SWEEP" || exit $? ;;
     diag) V=${DIAGLIB:-diagw}; run 600 gpurun_out/r5_diag_$V.jsonl env HAKAI_LIB=hakai-fem_amd/lib/variants/$V.so \
