@@ -21,6 +21,14 @@ namespace hk {
 constexpr int kBlock = 256;
 constexpr int kEPB = kBlock / 8;     // elements per block
 constexpr int kLdsStride = 50;       // doubles per element slot: 8 nodes x (X,du) + pad (bank spread)
+// Owner-assembly force staging: [element][local node][3] with one pad double per element, so a
+// pass's entries reading the same local node of consecutive elements (lane stride 8) hit spread
+// banks (stride 24 doubles = 48 dwords put a 32-lane read on 4 banks: 8-way conflicts)
+constexpr int kFeStride = 25;
+__device__ __forceinline__ int fe_at(int l, int c) { return (l >> 3) * kFeStride + 3 * (l & 7) + c; }
+// Pusai table in LDS: 24 doubles per Gauss point padded to 26 (lanes k and k+4 of an element read
+// rows 4 x 24 doubles apart: the same bank; 26 keeps the rows 16-byte aligned for 128-bit reads)
+constexpr int kPusStride = 26;
 
 // Reference node index (C3D8 order) of the node with sign bits s = (x>0)<<2 | (y>0)<<1 | (z>0).
 __device__ __forceinline__ int ref_of_sign(int s) {
@@ -167,7 +175,7 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
                                                double* sfe = nullptr) {
     const unsigned go = gp_off(e, k);
     if (PART != kWbState && OWN) {  // owner-computed assembly: the batch's forces go to LDS [element][local node][3]
-        double* fo = sfe + 3 * ((threadIdx.x & ~7) + (EXACT_NODE ? k : ref_of_sign(k)));
+        double* fo = sfe + (threadIdx.x >> 3) * kFeStride + 3 * (EXACT_NODE ? k : ref_of_sign(k));
         fo[0] = active ? fk[0] : 0.0;
         fo[1] = active ? fk[1] : 0.0;
         fo[2] = active ? fk[2] : 0.0;
@@ -438,7 +446,8 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
 //     reference's eigvals agree to rounding; it only enters the deletion test and the output).
 // ---------------------------------------------------------------------------------------------
 constexpr int kXbStride = 74;  // doubles of LDS per element: exchange area [8 nodes][8 lanes] + one scalar row + pad
-static_assert(kEPB * kLdsStride * 8 == 12800 && kEPB * 24 * 8 == 6144 && kEPB * kXbStride * 8 + 192 * 8 == 20480,
+static_assert(kEPB * kLdsStride * 8 == 12800 && kEPB * kFeStride * 8 == 6400 &&
+                  kEPB * kXbStride * 8 + 8 * kPusStride * 8 == 20608,
               "own_slot_cap (hakai_kernels.hpp) assumes these LDS sizes");
 
 // x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
@@ -551,7 +560,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
 
     // ---- Jacobian at GP k in node order, det and inverse (cal_Bfinal :1424-1455; cal_BVbar_hexa
     // computes the same J and det at :1716-1740). The first term starts the sum (0 + x == x).
-    const double* P0 = pus + 24 * k;  // Pusai_mat[k][r][i] = pus[24k + 8r + i]
+    const double* P0 = pus + kPusStride * k;  // Pusai_mat[k][r][i] = pus[26k + 8r + i] (stage_pusai pads)
     const double* P1 = P0 + 8;
     const double* P2 = P0 + 16;
     double J11, J12, J13, J21, J22, J23, J31, J32, J33;
@@ -838,7 +847,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
 
 // Pusai table (cal_Pusai_hexa, 192 doubles, built on the host) into LDS.
 __device__ __forceinline__ void stage_pusai(const ElemArgs& a, double* s_pus) {
-    for (int w = threadIdx.x; w < 192; w += blockDim.x) s_pus[w] = a.pusai[w];
+    for (int w = threadIdx.x; w < 192; w += blockDim.x) s_pus[w / 24 * kPusStride + w % 24] = a.pusai[w];
 }
 
 // Graph mode (hipGraph of two steps, hakai_step): the step number is not a kernel argument but a
@@ -862,7 +871,7 @@ template <bool DO_DELETE, bool STORE_TRIAX, bool WITH_VOL, bool EXACT>
 __global__ __launch_bounds__(kBlock, 2) void k_element(ElemArgs a) {
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
-    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
+    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 8 * kPusStride : 1];
     const long long vb = xcd_remap(blockIdx.x, gridDim.x);
     if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
@@ -951,7 +960,7 @@ __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const doub
             const int l = own_lane(en, j);
             double* dst = ((flags & kOwnExp) && j < n) ? a.own_rows + 3 * ((long long)en.x + (long long)j * slot) : dump;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dst[c] = s_fe[3 * l + c];
+            for (int c = 0; c < 3; ++c) dst[c] = s_fe[fe_at(l, c)];
         }
         return;
     }
@@ -960,7 +969,7 @@ __device__ __forceinline__ void own_entry(const ElemArgs& a, int4 en, const doub
     for (int j = 0; j < n; ++j) {
         const int l = own_lane(en, j);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) v[c] += s_fe[3 * l + c];
+        for (int c = 0; c < 3; ++c) v[c] += s_fe[fe_at(l, c)];
     }
     if (!(flags & kOwnFin)) {
 #pragma unroll
@@ -1020,7 +1029,7 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS = 0>
 __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
-    constexpr int kOwnFe = OS * kEPB * 24;       // staged forces per pass (doubles)
+    constexpr int kOwnFe = OS * kEPB * kFeStride;  // staged forces per pass (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];
     __shared__ __attribute__((aligned(16))) double s_fe[OWN ? 2 * kOwnFe : 1];
     // dynamic LDS (sized by the launch, launch_pipe): [own_slots][3] running sums, then the
@@ -1029,7 +1038,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     double* s_part = s_dyn;
     DevMat* s_mats = reinterpret_cast<DevMat*>(s_dyn + (OWN ? 3 * a.own_slots : 0));
     __shared__ __attribute__((aligned(16))) double s_xb[EXACT ? kEPB * kXbStride : 1];
-    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 192 : 1];
+    __shared__ __attribute__((aligned(16))) double s_pus[EXACT ? 8 * kPusStride : 1];
     if (poisoned(a.poison)) return;  // block-uniform
     graph_step(a);
     const int k = threadIdx.x & 7;
@@ -1102,7 +1111,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
         // its summing pass) spills and measured 1.18-1.28 against 1.10 ms, profiles/r03_exact_early_loads_ab.log.)
         if (!EXACT) load_stage_b<ANY_PLASTIC, NT>(a, elem_of(i + 1), k, nxt);
         if (OWN) ent_nxt = own_load(a, sb_of(i + 1));
-        double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * 24);
+        double* sfe = s_fe + ((i / S) & 1) * kOwnFe + (i % S) * (kEPB * kFeStride);
         if (EXACT) {
 #ifdef HK_DIAG_PHASE
             pc.last = clock64();

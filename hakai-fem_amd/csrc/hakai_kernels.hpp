@@ -108,8 +108,8 @@ struct NodalArgs {
 // 2048 (11-bit slot ids in the entry lists).
 constexpr int kOwnSlotsMax = 2048;
 inline int own_slot_cap(bool exact, int batches_per_pass, int nmat) {
-    // (force staging: 6 KB per batch, two buffers)
-    const int stat = 12800 + 6144 * batches_per_pass * 2 + (exact ? 20480 : 0) + 64;
+    // (force staging: 6400 B per batch -- 32 elements x 25 doubles, padded -- two buffers)
+    const int stat = 12800 + 6400 * batches_per_pass * 2 + (exact ? 20608 : 0) + 64;
     const int left = 81920 - 256 - stat - nmat * (int)sizeof(DevMat);
     return left < 24 ? 0 : (left / 24 > kOwnSlotsMax ? kOwnSlotsMax : left / 24);
 }
