@@ -926,7 +926,8 @@ static bool own_banded(const hakai_ctx* c, long long G, const std::vector<int>& 
         const double Gr = std::max(1.0, (double)G * (double)ne / (double)nE);
         const long long Rcap = (slot_cap - slot_cap / 16) / (nx[e0] + 1) - 1;
         const long long Ropt = (long long)std::llround(std::sqrt(1.5 * (double)layers * (double)rows / Gr));
-        Rreg[r] = std::max<long long>(1, std::min(Rcap, std::max<long long>(Ropt, 1)) - shrink);
+        const long long Rwant = c->own_band_rows > 0 ? (long long)c->own_band_rows : std::max<long long>(Ropt, 1);
+        Rreg[r] = std::max<long long>(1, std::min(Rcap, Rwant) - shrink);
     }
     std::vector<long long> key(nb);
     bool any_split = false;
@@ -1780,6 +1781,12 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
         if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_assembly must be 0, 1 or 2");
         c->own_assembly = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "own_band_rows")) {  // row-band height of the banded owner schedule (0: planned)
+        if (value < 0 || value > 4096) return fail(HAKAI_ERR_ARG, "own_band_rows must be in [0, 4096]");
+        if (c->own_band_rows != (int)value) c->own_for_g0 = -1;  // re-plan at the next step
+        c->own_band_rows = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "graph")) {

@@ -186,6 +186,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       reference-order kernel where the lists need two entries per thread in some
  *                       pass (wide sections, hakai_stat "own_round2": the array is faster there);
  *                       2: the owner sums wherever they fit;
+ *   "own_band_rows"     0 (default): the banded owner schedule plans its row-band height; >0: that
+ *                       height (capped by the block's LDS slots), re-planned at the next step;
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);

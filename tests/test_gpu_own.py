@@ -283,3 +283,28 @@ def test_own_elem_exact_switch_mid_run_replans():
     assert steps2 == 90, res[2][1:]
     assert sf > 923 >= se, (sf, se)  # the two kernels really needed different plans
     _same(g2, res[0][0])
+
+
+def test_own_band_rows_change_between_calls_replans():
+    """own_band_rows forces the row-band height (2, 3, then the planned 4 again); each change
+    re-plans the lists at the next step, handing the previous step's sums to the nodal update through
+    the uploaded-Q path: bit-identical to the fe path, and each height gives its own list set."""
+    m = small_bar(100, 100, 16, n_steps=90, v_end=5e5)
+    tune = {"elem_pipe_blocks": 128}
+    g0, _, _ = _run(m, [(1, 31), (32, 30), (62, 29)], tune, 0)
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("own_assembly", 1)
+        rows = []
+        for (t0, n), r in zip(((1, 31), (32, 30), (62, 29)), (2, 3, 0)):
+            sv.set_tuning("own_band_rows", r)
+            sv.step(t0, n)
+            assert sv.stat("own_banded") == 1
+            rows.append(sv.stat("own_rows"))
+        g1 = sv.download()
+        assert sv.stat("own_steps") == 90
+        with pytest.raises(Exception):
+            sv.set_tuning("own_band_rows", -1)
+    assert rows[0] > rows[1] > rows[2], rows  # lower bands export more rows (CPU replay: 543 k, 412 k, 402 k)
+    _same(g1, g0)

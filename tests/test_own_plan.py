@@ -30,6 +30,8 @@ CASES = [
     ("60 60 6 --G 1", {"grid": 8}),                                 # too many open sums: 8x finer grid
     ("4 4 40 --G 3", {"grid": 3}),
     ("5 1 1 --G 1", {}),                                            # Tensile5e-sized: one batch
+    ("100 100 16 --G 128 --band-rows 2 --schedule 2", {"banded": 1}),  # forced band heights (own_band_rows)
+    ("100 100 16 --G 128 --band-rows 3 --schedule 2 --exact 1", {"banded": 1}),
 ]
 
 

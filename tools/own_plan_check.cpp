@@ -11,7 +11,7 @@
 // (v2/HAKAI_j.jl:668-675) for random contributions with mixed signs and magnitudes.
 //
 //   own_plan_check nx ny nz [--plate px py pz] [--G n] [--exact 0|1] [--schedule 0|1|2]
-//                  [--shuffle seed]
+//                  [--shuffle seed] [--band-rows R]
 // Prints one JSON line: {"ok": ..., "planned": ..., "epb", "grid", "superbatch", "banded", "rows",
 // "entries", "slots", "mismatch"} and exits 0 when the replay matches (or no plan fits: planned false).
 #include "../hakai-fem_amd/csrc/hakai_capi.cpp"
@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int nx = std::atoi(argv[1]), ny = std::atoi(argv[2]), nz = std::atoi(argv[3]);
-    int px = 0, py = 0, pz = 0, exact = 0, schedule = 0;
+    int px = 0, py = 0, pz = 0, exact = 0, schedule = 0, band_rows = 0;
     long long G0 = 512;
     long long shuffle = -1;
     for (int a = 4; a < argc; ++a) {
@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
         else if (k == "--exact" && a + 1 < argc) exact = std::atoi(argv[++a]);
         else if (k == "--schedule" && a + 1 < argc) schedule = std::atoi(argv[++a]);
         else if (k == "--shuffle" && a + 1 < argc) shuffle = std::atoll(argv[++a]);
+        else if (k == "--band-rows" && a + 1 < argc) band_rows = std::atoi(argv[++a]);
         else {
             std::fprintf(stderr, "bad argument %s\n", argv[a]);
             return 2;
@@ -86,6 +87,7 @@ int main(int argc, char** argv) {
     c.h_conn = conn;
     c.nmat = 1;
     c.elem_exact = exact;
+    c.own_band_rows = band_rows;
     // node -> (8e + k) CSR in ascending element order (hakai_upload_model)
     std::vector<int> cnt(nN + 1, 0);
     for (long long e = 0; e < nE; ++e)
