@@ -16,6 +16,7 @@
 #   rehearse4  python bench.py --gpus 4 self-launched on the one GPU (RCCL sockets) -> gpurun_out/r5_rehearse4.json
 #   ablib      LIBS="a b cur" alternating libraries (hakai-fem_amd/lib/variants/<a>.so) under tools/sweep.py
 #   contact    tools/bench_contact.py on C4: one context, 2/4 ranks with z- and x-slab ranges -> r5_contact_c4.jsonl
+#   pmcwide    FETCH_SIZE / WRITE_SIZE passes + kernel trace on C5 16 M and C4 -> gpurun_out/r5_pmc_{c5,c4}.json
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r5_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -89,6 +90,17 @@ EOF
         done ;;
     rehearse4) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r5_rehearse4.json python bench.py --gpus 4 \
                    --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
+    pmcwide) for w in c5 c4; do  # HBM bytes per launch on the wide sections: C5 16 M (--strong, N = 1), C4
+            if [ $w = c5 ]; then CMD="python bench.py --strong --steps 10 --warmup 2 $BA --compare-fused 0"
+            else CMD="python tools/sweep.py --config c4 --rounds 1 --steps 10 --variants fused:elem_exact=0"; fi
+            P=gpurun_out/r5_pmc_$w; rm -rf $P
+            HAKAI_GRAPH=0 run 600 $P.kt.log rocprofv3 --kernel-trace -d $P/kt -o run --output-format csv -- $CMD || exit $?
+            HAKAI_GRAPH=0 run 600 $P.fetch.log timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run \
+                --output-format csv -- $CMD || exit $?
+            HAKAI_GRAPH=0 run 600 $P.write.log timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run \
+                --output-format csv -- $CMD || exit $?
+            python tools/pmc_kernels.py --fetch $P/fetch --write $P/write --kt $P/kt --label $w > $P.json || exit $?
+        done ;;
     tests:*) run 1200 gpurun_out/r5_tests.log python -u -m pytest tests -m gpu -x -v --timeout 300 \
                  --timeout-method thread -p no:cacheprovider -k "${st#tests:}" || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
