@@ -1257,6 +1257,7 @@ static bool own_choose(hakai_ctx* c, long long G0, OwnSched& best_sc, OwnPlan& b
     bool have = false;
     auto consider = [&](const OwnSched& sc) {
         for (int S : {2, 1}) {
+            if (c->own_pass_batches > 0 && S != c->own_pass_batches) continue;
             OwnPlan pl;
             if (!own_plan(c, sc, S, cap_of(S), pl)) continue;
             if (!have || pl.cost() < best.cost()) {
@@ -1781,6 +1782,12 @@ int hakai_set_tuning(hakai_ctx* c, const char* key, int64_t value) {
     if (!std::strcmp(key, "own_assembly")) {  // owner-computed node sums in the element kernel
         if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_assembly must be 0, 1 or 2");
         c->own_assembly = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "own_pass_batches")) {  // batches per owner summing pass (0: planned)
+        if (value < 0 || value > 2) return fail(HAKAI_ERR_ARG, "own_pass_batches must be 0, 1 or 2");
+        if (c->own_pass_batches != (int)value) c->own_for_g0 = -1;  // re-plan at the next step
+        c->own_pass_batches = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "own_band_rows")) {  // row-band height of the banded owner schedule (0: planned)

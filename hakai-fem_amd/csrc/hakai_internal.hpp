@@ -134,6 +134,7 @@ struct hakai_ctx {
     long long own_built_g = -1;        // grid the lists were built for (-1 none, -2 mesh not suitable)
     long long own_for_g0 = -1;         // persistent-kernel grid that build was for (a change rebuilds)
     int own_band_rows = 0;             // tuning: row-band height of the banded schedule (0: planned)
+    int own_pass_batches = 0;          // tuning: batches per summing pass (0: 2 where they fit, else 1)
     bool own_valid = false;            // d_own_q/d_own_rows hold the last element step's sums
     int* d_own_off = nullptr;          // [nb+1] entry offsets per schedule position (super-batch starts)
     int* d_own_seq = nullptr;          // [nb] batch at each schedule position (ascending within a block)

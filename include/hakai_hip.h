@@ -188,6 +188,8 @@ int hakai_profile_read(hakai_ctx* ctx, int kernel, double* total_ms, int64_t* la
  *                       2: the owner sums wherever they fit;
  *   "own_band_rows"     0 (default): the banded owner schedule plans its row-band height; >0: that
  *                       height (capped by the block's LDS slots), re-planned at the next step;
+ *   "own_pass_batches"  0 (default): owner summing passes over 2 batches where the lists fit, else 1;
+ *                       1 or 2: that many (re-planned at the next step);
  *   "nodal_padded"      0: CSR force gather instead of the padded [nN][8] table;
  *   "fuse_bc"           1 (default): one GPU, <= 2^18 nodes: the nodal kernel applies the BCs;
  *   "graph"             steps per captured hipGraph (even, default 16; 0 = stream mode);
