@@ -308,3 +308,26 @@ def test_own_band_rows_change_between_calls_replans():
             sv.set_tuning("own_band_rows", -1)
     assert rows[0] > rows[1] > rows[2], rows  # lower bands export more rows (CPU replay: 543 k, 412 k, 402 k)
     _same(g1, g0)
+
+
+def test_own_pass_batches_forced_one_bitexact():
+    """own_pass_batches 1: one batch per summing pass where the planner would take two (a 100-wide
+    section, whose two-batch passes need second entry rounds): re-planned between calls, bit-identical
+    to the fe path, no second rounds."""
+    m = small_bar(100, 100, 16, n_steps=60, v_end=5e5)
+    tune = {"elem_pipe_blocks": 128}
+    g0, _, _ = _run(m, [(1, 31), (32, 29)], tune, 0)
+    with Solver(m) as sv:
+        for k, v in tune.items():
+            sv.set_tuning(k, v)
+        sv.set_tuning("own_assembly", 1)
+        sv.step(1, 31)
+        assert sv.stat("own_superbatch") == 2
+        sv.set_tuning("own_pass_batches", 1)
+        sv.step(32, 29)
+        assert sv.stat("own_superbatch") == 1 and sv.stat("own_round2") == 0
+        assert sv.stat("own_steps") == 60
+        g1 = sv.download()
+        with pytest.raises(Exception):
+            sv.set_tuning("own_pass_batches", 3)
+    _same(g1, g0)
