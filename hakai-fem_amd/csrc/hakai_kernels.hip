@@ -1008,11 +1008,14 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
 #ifdef HK_DIAG_WAVE
     const long long t1 = clock64();
 #endif
-    own_entry(a, en, s_fe, s_part);
+    // a wave whose threads hold no entry of this round skips it (wave-uniform: no-op entries only
+    // store to the dump line; C3 -0.8 to -1.0 %, C4 -1.0 %, profiles/r05_pass_skip_empty_waves_ab.log)
+    const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
+    if (o0 + (int)(threadIdx.x & ~63u) < o1) own_entry(a, en, s_fe, s_part);
     if (en.y & kOwnRound2) {  // block-uniform
-        const int o0 = a.own_off[sb], o1 = a.own_off[sb + 1];
         const int idx = o0 + kBlock + (int)threadIdx.x;
-        own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe, s_part);
+        if (o0 + kBlock + (int)(threadIdx.x & ~63u) < o1)
+            own_entry(a, a.own_list[idx < o1 ? idx : a.own_nop], s_fe, s_part);
     }
 #ifdef HK_DIAG_WAVE
     const long long t2 = clock64();
