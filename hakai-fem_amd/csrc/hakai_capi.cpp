@@ -152,6 +152,17 @@ int build_devmat(const hakai_material_t& in, DevMat& o) {
         o.du_eps[r] = in.ductile[3 * r + 0];
         o.du_tri[r] = in.ductile[3 * r + 1];
     }
+    // ductile_fr returns a table value or a linear interpolation between two neighbouring ones,
+    // i.e. at least the smallest fracture strain less a few rounding errors of its terms: an element
+    // average below min - (|max| + |min|) * 2^-40 cannot reach it, and the kernels skip the table
+    // search (the same deletion decisions, tests/test_gpu_exact.py, test_gpu_fullsize.py)
+    double lo = 0.0, hi = 0.0;
+    for (int r = 0; r < in.n_ductile; ++r) {
+        lo = r == 0 ? o.du_eps[r] : std::min(lo, o.du_eps[r]);
+        hi = r == 0 ? o.du_eps[r] : std::max(hi, o.du_eps[r]);
+    }
+    o.du_floor = in.n_ductile > 0 ? lo - (std::fabs(hi) + std::fabs(lo)) * 0x1p-40 : 0.0;
+    if (!(o.du_floor == o.du_floor)) o.du_floor = -HUGE_VAL;  // (a NaN table: never skip)
     return 0;
 }
 

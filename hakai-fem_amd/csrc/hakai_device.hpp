@@ -30,6 +30,7 @@ struct DevMat {
     double Hd[kMaxPlastic];       // hardening slope of segment j
     double du_eps[kMaxDuctile];   // ductile[:,1] fracture strain
     double du_tri[kMaxDuctile];   // ductile[:,2] triaxiality
+    double du_floor;              // below every fracture strain ductile_fr can return (skips the table)
 };
 
 // DPP control words (gfx9 encoding).

@@ -391,7 +391,8 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     if (DO_DELETE && nd > 0) {
         const double v_e = allreduce8(eqp) * 0.125;
         const double t_e = allreduce8(tri) * 0.125;
-        if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);  // ductile table (:720-733)
+        if (!(t_e < 0.0) && v_e >= M->du_floor)  // (below du_floor no table value is reached)
+            kill = active && v_e >= ductile_fr(M, nd, t_e);  // ductile table (:720-733)
     }
 
     // ---- internal force (Qe[:,e] += detJ * Bfinal' * sigma, :1330-1340), reduce-scattered so
@@ -790,7 +791,7 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         gp_all8x2(xb, k, eqp, tri, v_e, t_e);
         v_e = v_e * 0.125;  // /8, exact
         t_e = t_e * 0.125;
-        if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
+        if (!(t_e < 0.0) && v_e >= M->du_floor) kill = active && v_e >= ductile_fr(M, nd, t_e);
     }
 
     // the Gauss-point state, flag and deletion log are final here: stored before the force pass, so
