@@ -492,25 +492,18 @@ __device__ __forceinline__ double gp_sum8(double* w, int k, const double (&v)[8]
     return acc;
 }
 
-// Ordered sums over the 8 lanes of two scalars (one LDS round trip); every lane gets both.
-__device__ __forceinline__ void gp_all8x2(double* w, int k, double x, double y, double& xs, double& ys) {
+// Ordered sum over the 8 lanes of a scalar (one LDS round trip); every lane gets it.
+__device__ __forceinline__ double gp_all8(double* w, int k, double x) {
     w[k] = x;
-    w[8 + k] = y;
     wave_lds_fence();
-    double r[8], q[8];
+    double r[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) r[kk] = w[kk];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) q[kk] = w[8 + kk];
     wave_lds_fence();
-    double a = 0.0 + r[0], b = 0.0 + q[0];
+    double a = 0.0 + r[0];
 #pragma unroll
-    for (int kk = 1; kk < 8; ++kk) {
-        a += r[kk];
-        b += q[kk];
-    }
-    xs = a;
-    ys = b;
+    for (int kk = 1; kk < 8; ++kk) a += r[kk];
+    return a;
 }
 
 // Diagnostic build only (-DHK_DIAG_PHASE, tools/diag_wave.py): per-wave clock totals of the phases of
@@ -763,15 +756,16 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
         }
     }
     // ---- triaxiality of the final stress (invariant form of :995-1018; the reference's eigenvalue
-    // differences give the same value to rounding -- it enters only the deletion test and the output)
-    double tri;
-    {
+    // differences give the same value to rounding -- it enters only the deletion test and the output).
+    // Formed where it is stored (a call's last step) or the deletion test needs it (below); an
+    // inactive element's value is never used, so forming it after the inactive select changes nothing.
+    auto triax = [&]() {
         const double mean = div3(fin[0] + fin[1] + fin[2]);
         const double a01 = fin[0] - fin[1], a12 = fin[1] - fin[2], a20 = fin[2] - fin[0];
         const double oeq = sqrt(0.5 * (a01 * a01 + a12 * a12 + a20 * a20) +
                                 3.0 * (fin[3] * fin[3] + fin[4] * fin[4] + fin[5] * fin[5]));
-        tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
-    }
+        return (oeq < 1e-10) ? 0.0 : mean / oeq;
+    };
     double eps[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) eps[c] = active ? in.eps[c] + de[c] : in.eps[c];
@@ -785,13 +779,18 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     }
 
     HK_PH(pc, 5);
+    double tri = STORE_TRIAX ? triax() : 0.0;
     bool kill = false;
     if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
-        double v_e, t_e;
-        gp_all8x2(xb, k, eqp, tri, v_e, t_e);
-        v_e = v_e * 0.125;  // /8, exact
-        t_e = t_e * 0.125;
-        if (!(t_e < 0.0) && v_e >= M->du_floor) kill = active && v_e >= ductile_fr(M, nd, t_e);
+        const double v_e = gp_all8(xb, k, eqp) * 0.125;  // /8, exact
+        // below du_floor no fracture strain of the table is reached whatever the triaxiality: the
+        // average triaxiality (a second round trip) only where it can matter; the 8 lanes of an
+        // element share v_e, so the branch is uniform over them
+        if (v_e >= M->du_floor) {
+            if (!STORE_TRIAX) tri = triax();
+            const double t_e = gp_all8(xb, k, tri) * 0.125;
+            if (!(t_e < 0.0)) kill = active && v_e >= ductile_fr(M, nd, t_e);
+        }
     }
 
     // the Gauss-point state, flag and deletion log are final here: stored before the force pass, so
