@@ -163,6 +163,9 @@ int build_devmat(const hakai_material_t& in, DevMat& o) {
     }
     o.du_floor = in.n_ductile > 0 ? lo - (std::fabs(hi) + std::fabs(lo)) * 0x1p-40 : 0.0;
     if (!(o.du_floor == o.du_floor)) o.du_floor = -HUGE_VAL;  // (a NaN table: never skip)
+    // an element average of eight values below du_skip (rounded sums: at most 8 ulps above their
+    // bound) stays below du_floor: a wave whose Gauss points all lie below it needs no averages
+    o.du_skip = o.du_floor > 0.0 ? o.du_floor - o.du_floor * 0x1p-40 : -HUGE_VAL;
     return 0;
 }
 

@@ -31,6 +31,7 @@ struct DevMat {
     double du_eps[kMaxDuctile];   // ductile[:,1] fracture strain
     double du_tri[kMaxDuctile];   // ductile[:,2] triaxiality
     double du_floor;              // below every fracture strain ductile_fr can return (skips the table)
+    double du_skip;               // a wave whose Gauss points all lie below this skips the deletion test
 };
 
 // DPP control words (gfx9 encoding).

@@ -386,10 +386,14 @@ __device__ __forceinline__ void elem_step(const ElemArgs& a, const DevMat* __res
     // ---- triaxiality (cal_triax_stress, :995-1018): mean / Mises of the final stress. The Mises
     // of the returned stress is sc*q (radial return scales the deviator), so no second sqrt.
     const double oeq = q * sc;
-    const double tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
+    // (formed where stored, a call's last step, or where the deletion test can need it)
+    double tri = STORE_TRIAX ? ((oeq < 1e-10) ? 0.0 : mean / oeq) : 0.0;
     bool kill = false;
-    if (DO_DELETE && nd > 0) {
+    // a wave whose Gauss points all lie below du_skip has no element average that can reach the
+    // ductile table (wave-uniform skip)
+    if (DO_DELETE && nd > 0 && __builtin_amdgcn_ballot_w64(eqp >= M->du_skip) != 0) {
         const double v_e = allreduce8(eqp) * 0.125;
+        if (!STORE_TRIAX) tri = (oeq < 1e-10) ? 0.0 : mean / oeq;
         const double t_e = allreduce8(tri) * 0.125;
         if (!(t_e < 0.0) && v_e >= M->du_floor)  // (below du_floor no table value is reached)
             kill = active && v_e >= ductile_fr(M, nd, t_e);  // ductile table (:720-733)
@@ -781,7 +785,9 @@ __device__ __forceinline__ void elem_step_exact(const ElemArgs& a, const DevMat*
     HK_PH(pc, 5);
     double tri = STORE_TRIAX ? triax() : 0.0;
     bool kill = false;
-    if (DO_DELETE && nd > 0) {  // element averages in GP order (:701-712)
+    // element averages in GP order (:701-712); a wave whose Gauss points all lie below du_skip has
+    // none that can reach the ductile table (wave-uniform skip, the same decisions)
+    if (DO_DELETE && nd > 0 && __builtin_amdgcn_ballot_w64(eqp >= M->du_skip) != 0) {
         const double v_e = gp_all8(xb, k, eqp) * 0.125;  // /8, exact
         // below du_floor no fracture strain of the table is reached whatever the triaxiality: the
         // average triaxiality (a second round trip) only where it can matter; the 8 lanes of an
