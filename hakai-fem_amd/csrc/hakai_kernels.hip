@@ -198,7 +198,9 @@ __device__ __forceinline__ void elem_writeback(const ElemArgs& a, long long e, i
         gp_st<NT>(at32(a.yield, go), PRESEL || active ? ys : in.ys);
     }
     if (STORE_TRIAX) *at32(a.triax, go) = active ? tri : 0.0;
-    if (DO_DELETE) {
+    // (a wave without a deletion and without an element deleted in the previous step changes no flag
+    // and logs nothing: it skips both stores; C3 fused -1.0 %, profiles/r05_flag_store_skip_ab.log)
+    if (DO_DELETE && __builtin_amdgcn_ballot_w64(kill || in.fl == 2) != 0) {
         *at32(a.flag, 4u * (unsigned)e) = kill ? 2 : (in.fl == 2 ? 0 : in.fl);  // 8 lanes, same value
         // lane 0: the element's deletion step; lanes 1-7 of a killed element: slot nEp+1, "last step
         // with a deletion" (contact rebuilds its live surface lists from it); others: dump slot nEp
