@@ -88,6 +88,10 @@ def parse():
                     help="N > 1 weak: also time one rank's slab alone (single_gpu_same_slab)")
     ap.add_argument("--breakdown", type=int, default=1,
                     help="per-kernel breakdown pass after the timed region (profiling scripts: 0)")
+    ap.add_argument("--deletion-window", type=int, default=1,
+                    help="N = 1, C3: also time steps %d-%d (both ductile deletion waves) in both element modes "
+                         "(config.deletion_window); the CPU baseline then runs the oracle over that window" %
+                         (7941, 7960))
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -277,6 +281,37 @@ def cpu_baseline(seconds, threads):
                       f"{n} steps in {dt:.1f} s, {threads} OpenMP threads"}
 
 
+def cpu_baseline_window(model, s0, end_exact, gpu_dels, steps, threads, report):
+    """CPU baseline on the C3 workload itself: the oracle (C restatement of v0.0.2, OpenMP element
+    loop) takes the GPU's hand-off state at step DEL_WINDOW_FIRST - 1 and runs the same `steps` steps
+    as deletion_window -- the deletion regime, 2 M hex. Its end state is the checker of the GPU's
+    reference-order run over the window: report["bitexact_vs_oracle"] (disp, disp_pre, stress,
+    strain, eqps, flags, Q and the deletion log compared bit for bit)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = threads or min(16, os.cpu_count() or 1)
+    o = O.Oracle(model, nthreads=threads)
+    s = o.s
+    for k in ("disp", "disp_pre", "velo", "Q", "Qe", "integ_stress", "integ_strain", "integ_yield_stress",
+              "integ_eq_plastic_strain", "integ_triax_stress", "element_flag"):
+        s[k][...] = getattr(s0, k)
+    s["position"][...] = model.coordmat + s0.disp.reshape(-1, 3)
+    t0 = time.perf_counter()
+    o.run(DEL_WINDOW_FIRST, steps)
+    dt = time.perf_counter() - t0
+    n_act = (int(s0.element_flag.sum()) + int(s["element_flag"].sum())) / 2
+    odel = sorted((int(a), int(b)) for a, b in o.deletions)
+    same = {k: bool(np.array_equal(getattr(end_exact, k), s[k]))
+            for k in ("disp", "disp_pre", "integ_stress", "integ_strain", "integ_eq_plastic_strain", "element_flag", "Q")}
+    report["bitexact_vs_oracle"] = bool(all(same.values()) and odel == gpu_dels)
+    report["oracle_compare"] = dict(same, deletions_oracle=len(odel))
+    return {"value": n_act * steps / dt / 1e6, "unit": "M element-updates/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (C restatement of v0.0.2, {threads} OpenMP threads) on the C3 bar itself "
+                      f"({model.nElement} hex), steps {DEL_WINDOW_FIRST}-{DEL_WINDOW_FIRST + steps - 1} (both "
+                      f"deletion waves) from the GPU's hand-off state: {steps} steps in {dt:.1f} s; its end state "
+                      "checks the GPU's reference-order run of the same window (config.deletion_window)"}
+
+
 def same_slab_rate(model, diag, exact, preload, warmup, steps):
     """One rank's slab alone on its GPU (no communicator, no interface): wall time of `steps`."""
     import torch
@@ -399,7 +434,7 @@ def gather_floats(x, multi):
     return [float(o.item()) for o in out]
 
 
-def c5_n1_reference(rank, device, exact, steps, multi):
+def c5_n1_reference(rank, device, exact, steps, multi, store=None):
     """The whole C5 bar on rank 0's GPU alone (no communicator), same preload/warm-up/steps as the
     N-rank c5_strong run; the other ranks wait at a barrier. Returns the reference dict on rank 0,
     its value broadcast so every rank can form the ratio."""
@@ -428,7 +463,6 @@ def c5_n1_reference(rank, device, exact, steps, multi):
         # the other ranks wait on the host (the rendezvous store), not in a device collective: an RCCL
         # broadcast would keep a spinning kernel on every other rank's GPU for the whole reference run
         # (on a shared-GPU rehearsal, on rank 0's GPU itself)
-        store = dist.distributed_c10d._get_default_store()
         key = "bench_c5_n1_reference"
         if rank == 0:
             store.set(key, json.dumps([float(x) for x in res.tolist()]))
@@ -444,6 +478,63 @@ def c5_n1_reference(rank, device, exact, steps, multi):
 
 def active_elements(g):
     return sum(int(sv.download(element_flag=True).element_flag.sum()) for sv in g.svs)
+
+
+DEL_WINDOW_FIRST = 7941        # C3 (v_end 5e5): first ductile deletion wave at step 7950, second at 7953
+DEL_WINDOW_STEPS = 20          # (tests/test_gpu_fullsize.py, tools/diag_fullsize_deletion.py)
+
+
+def deletion_window(g, t, exact, steps):
+    """the deletion regime timed. The C3 bar (one context) runs on in the headline
+    mode to step DEL_WINDOW_FIRST - 1; its state is downloaded once and both element modes time the
+    same `steps` steps from it (state uploaded again before each), across the two deletion waves.
+    Returns (report dict, hand-off state, (reference-order end state, its window deletions)) -- the
+    last two feed the CPU
+    baseline leg, which runs the oracle over the same window and compares bits."""
+    sv = g.svs[0]
+    w0 = DEL_WINDOW_FIRST
+    if t > w0:
+        return None, None, None
+    t_run = time.perf_counter()
+    g.run(t, w0 - t)
+    g.sync()
+    t_run = time.perf_counter() - t_run
+    s0 = sv.download()
+    out = {"first_step": w0, "steps": steps, "reached_in_s": round(t_run, 2),
+           "what": "C3 (2 M hex) steps %d-%d, both ductile deletion waves (7950, 7953) inside: flag and deletion-log "
+                   "stores, element averages and the ductile table run in the waves that delete; same hand-off "
+                   "state for both modes" % (w0, w0 + steps - 1)}
+    end_exact, dels_exact = None, None
+    for mode_exact in (exact, not exact):
+        # the first step in a mode plans its owner-computed assembly on the host (the reference-order
+        # kernel has its own LDS budget): one untimed step from the hand-off state, then the state again
+        g.set("elem_exact", int(mode_exact))
+        sv.upload(s0)
+        g.run(w0, 1)
+        g.sync()
+        sv.upload(s0)
+        e, el, _ = timed(g, w0, steps, False)
+        dels = [(int(a), int(b)) for a, b in sv.deleted() if w0 <= a < w0 + steps]
+        st = sv.download()
+        n_act = int(st.element_flag.sum())
+        n_start = int(s0.element_flag.sum())
+        out["exact" if mode_exact else "fused"] = {
+            "value": round((n_start + n_act) / 2 * steps / e / 1e6, 3), "unit": "M element-updates/s",
+            "ms_per_step": round(e / steps * 1e3, 4),
+            "element_avg_ms": round(el[0][0] / max(el[0][1], 1), 4),
+            "deletions": len(dels), "deletion_steps": sorted({d[0] for d in dels}),
+            "elements_active_start_end": [n_start, n_act]}
+        if mode_exact:
+            end_exact, dels_exact = st, sorted(dels)
+    g.set("elem_exact", int(exact))
+    f, x = out["fused"], out["exact"]
+    out["same_deletions_both_modes"] = (f["deletions"] == x["deletions"]
+                                        and f["deletion_steps"] == x["deletion_steps"])
+    out["bitexact_vs_oracle"] = None      # filled by the CPU baseline leg (cpu_baseline_window)
+    return out, s0, (end_exact, dels_exact)
+
+
+T_START = time.perf_counter()
 
 
 def main():
@@ -466,6 +557,7 @@ def main():
     nparts = R or world                      # subdomains of the workload
     multi = world > 1 or a.dist_path
     device = 0
+    store = None
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29571")
@@ -490,11 +582,13 @@ def main():
     t_setup = time.perf_counter() - t_setup
 
     t = 1
-    t_first = time.perf_counter()
-    g.run(t, 1)                  # the first step also plans the owner-computed assembly (host)
-    g.sync()
-    t_first = time.perf_counter() - t_first
-    t += 1
+    t_first = 0.0
+    if preload >= 1:
+        t_first = time.perf_counter()
+        g.run(t, 1)              # the preload's first step also plans the owner-computed assembly (host)
+        g.sync()
+        t_first = time.perf_counter() - t_first
+        t += 1
     if preload > 1:
         g.run(t, preload - 1)
         t += preload - 1
@@ -584,20 +678,40 @@ def main():
                                  / len(g.svs) if own_steps else 0)
     achieved = alg_bytes / el_avg_s / 1e9
     whole_bytes = B_E_PLASTIC * n_active + B_N * n_node_local
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "element_pmc.json")
-    if os.path.exists(pmc) and not R:
+    def pmc_of(mode):
+        """Calibrated HBM bytes per element launch for `mode` on this workload, measured by separate
+        rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/gpu_r6.sh pmc, tools/pmc_report.py):
+        profiles/element_pmc.json (fused), profiles/element_pmc_exact.json (reference order). Attached
+        only to the one-GPU C3 workload and the mode it was measured in."""
+        f = os.path.join(ROOT, "profiles", "element_pmc.json" if mode == "fused" else "element_pmc_exact.json")
+        if R or world != 1 or not cfg["workload"].startswith("C3") or not os.path.exists(f):
+            return None
         try:
-            with open(pmc) as f:
-                pm = json.load(f)
-            # measured on the one-GPU C3 workload (tools/gpu_prof.sh): attached to that workload and mode only
-            if (pm.get("elements") == n_elem_local and world == 1 and cfg["workload"].startswith("C3")
-                    and pm.get("element_mode", "fused") == a.element_mode):
-                traffic = pm.get("hbm_bytes_per_launch")
+            with open(f) as fh:
+                pm = json.load(fh)
         except Exception:
-            traffic = None
+            return None
+        if pm.get("elements") != n_elem_local or pm.get("element_mode", "fused") != mode:
+            return None
+        return pm
+    pm_head = pmc_of(a.element_mode)
+    traffic = pm_head.get("hbm_bytes_per_launch") if pm_head else None
+    if other is not None:
+        pm_other = pmc_of(other["element_mode"])
+        if pm_other:
+            other["traffic"] = pm_other.get("hbm_bytes_per_launch")
+            other["traffic_over_algorithmic"] = round(pm_other["traffic_over_algorithmic"], 4)
+            other["traffic_kernel_trace_avg_ms"] = round(pm_other["kernel_trace_avg_ms"], 4)
+            other["traffic_source"] = "profiles/element_pmc_exact.json" if other["element_mode"] == "exact" \
+                else "profiles/element_pmc.json"
     k_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in k_tot.items()}
     extra = {}
+    win, win_s0, win_end = None, None, None
+    if (a.deletion_window and nparts == 1 and not a.strong and not multi and cfg["workload"].startswith("C3")
+            and built[0][0].nElement == 2_000_000):
+        win, win_s0, win_end = deletion_window(g, t, exact, DEL_WINDOW_STEPS)
+        if win is not None:
+            extra["deletion_window"] = win
     if nparts > 1:
         ex_ms = sum(x[0] for x in ex_timed) / max(ex_timed[0][1], 1) / len(g.svs)
         extra["exchange_ms_per_step"] = round(max_over_ranks(ex_ms, multi), 4)
@@ -634,7 +748,7 @@ def main():
         if a.c5_n1_ref:
             # the same 16 M bar on ONE GPU (rank 0's), same steps, timed in this run after the N-rank
             # run: speedup_vs_n1 is a same-run, same-box ratio
-            n1 = c5_n1_reference(rank, device, exact, a.c5_steps, multi)
+            n1 = c5_n1_reference(rank, device, exact, a.c5_steps, multi, store)
             if n1 is not None:
                 c5["n1_reference"] = n1
                 c5["speedup_vs_n1"] = round(v5 / n1["value"], 3)
@@ -649,6 +763,11 @@ def main():
             "ms_per_step": round(e_ref / a.steps * 1e3, 4),
             "what": "one rank's slab alone on its GPU (no exchange), same preload/warmup/steps, slowest rank; "
                     "weak-scaling efficiency = value / (n_gpus x this)"}
+    if nparts > 1:
+        import resource
+        rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0 ** 2  # ru_maxrss: KiB on Linux
+        extra["peak_host_rss_gb_per_rank"] = [round(x, 2) for x in gather_floats(rss_gb, multi)]
+        extra["wall_s_rank_process"] = round(time.perf_counter() - T_START, 1)
     out = {
         "metric": "M element-updates/sec (hex8, 8 Gauss pts) at 1/2/4/8 MI355X; % HBM roofline",
         "value": round(value, 3),
@@ -686,8 +805,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": ("static: rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this kernel, mode and "
-                                        "workload, calibrated (profiles/element_pmc.json); not measured in this run")
+                                        "workload, calibrated (profiles/%s, round %s tree; its kernel-trace average "
+                                        "%.4f ms); not measured in this run"
+                                        % ("element_pmc.json" if a.element_mode == "fused" else "element_pmc_exact.json",
+                                           pm_head.get("round", "?"), pm_head.get("kernel_trace_avg_ms", 0.0)))
                      if traffic else None,
+                     "traffic_over_algorithmic": round(pm_head["traffic_over_algorithmic"], 4) if traffic else None,
                      "kernel": "k_element_pipe", "alg_bytes_per_launch": int(alg_bytes),
                      "alg_bytes_per_launch_with_assembly_outputs": int(alg_bytes_own),
                      "avg_launch_ms": round(el_avg_s * 1e3, 4), "measured_peak_GBs": HBM_MEASURED_GBS},
@@ -695,7 +818,11 @@ def main():
     }
     if rank == 0 and world == 1 and not R and not a.strong and a.cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_threads)
+            if win is not None:
+                out["cpu_baseline"] = cpu_baseline_window(built[0][0], win_s0, win_end[0], win_end[1],
+                                                          DEL_WINDOW_STEPS, a.cpu_threads, win)
+            else:
+                out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_threads)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:

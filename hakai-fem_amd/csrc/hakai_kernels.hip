@@ -457,17 +457,19 @@ static_assert(kEPB * kLdsStride * 8 == 12800 && kEPB * kFeStride * 8 == 6400 &&
                   kEPB * kXbStride * 8 + 8 * kPusStride * 8 == 20608,
               "own_slot_cap (hakai_kernels.hpp) assumes these LDS sizes");
 
-// x / 3.0 correctly rounded, in three FP64 operations instead of an IEEE division sequence:
-// q = RN(x*y) with y = RN(1/3), then one exact-remainder correction q + (x - 3q)*y. The exact
-// quotient x/3 (a multiple of 1/3 of the last place) is never within 1/6 ulp of a rounding
-// boundary, and the corrected value is within |x - 3q| * |y - 1/3| < 2^-52 ulp of it, so both round
-// the same way (tests/test_div3.py checks the identity against IEEE division on the CPU). A zero
-// comes out as +0 (see the zero-sign note above).
+// x / 3.0 correctly rounded, in two FP64 operations instead of an IEEE division sequence:
+// RN(x*yh + RN(x*yl)) with yh = RN(1/3) and yl = RN(1/3 - yh) = yh * 2^-54 (1/3 = yh + yl + 2^-108/3).
+// The fma's exact operand differs from x/3 by at most |x| * 2^-106 (the double-double reciprocal's
+// remainder plus the rounding of x*yl), while x/3 (a multiple of 1/3 of the result's last place) is
+// either representable or at least 1/6 ulp from every rounding boundary: both round the same way.
+// (Round 5 used q = x*yh, q + (x - 3q)*yh, three operations, which also turned -0 into +0; this
+// form keeps IEEE's -0/3 = -0.) tests/test_div3.py checks the identity against IEEE division on the
+// CPU, zeros and exact multiples included. Normal-range operands (stresses, shape-function
+// derivatives): x*yl stays normal for |x| > 2^-960.
 __device__ __forceinline__ double div3(double x) {
-    constexpr double y = 1.0 / 3.0;
-    const double q = x * y;
-    const double r = __builtin_fma(-q, 3.0, x);
-    return __builtin_fma(r, y, q);
+    constexpr double yh = 1.0 / 3.0;
+    constexpr double yl = 0x1.5555555555555p-56;  // RN(1/3 - yh)
+    return __builtin_fma(x, yh, x * yl);
 }
 
 // a / b correctly rounded given rb = RN(1/b) (one IEEE division per divisor): two Newton-Markstein
@@ -1038,7 +1040,10 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS = 0>
-__global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
+#ifndef HK_EXACT_MINB
+#define HK_EXACT_MINB 2
+#endif
+__global__ __launch_bounds__(kBlock, EXACT ? HK_EXACT_MINB : 2) void k_element_pipe(ElemArgs a) {
     constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
     constexpr int kOwnFe = OS * kEPB * kFeStride;  // staged forces per pass (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];

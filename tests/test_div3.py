@@ -1,8 +1,8 @@
 """The exact element kernel's divisions must equal IEEE division bit for bit:
-  * x/3.0 (div3 in csrc/hakai_kernels.hip: q = x*y, y = RN(1/3), then q + (x - 3q)*y with fused
-    multiply-adds), checked against `x / 3.0` on 2e7 doubles: random bit patterns over the exponent
-    range the kernel meets, multiples of 3 (exact quotients), values next to powers of two; a zero
-    comes out as +0 (the kernel's zero-sign argument, tests/test_exact_chains.py);
+  * x/3.0 (div3 in csrc/hakai_kernels.hip since round 6: RN(x*yh + RN(x*yl)), yh = RN(1/3),
+    yl = RN(1/3 - yh), one multiply and one fused multiply-add), checked against `x / 3.0` on 2e7
+    doubles: random bit patterns over the exponent range the kernel meets, multiples of 3 (exact
+    quotients), values next to powers of two, signed zeros (bit for bit: -0/3 = -0);
   * a/b given rb = RN(1/b) (div_cr: two Newton-Markstein corrections of a*rb), checked against
     `a / b` on 2e7 random pairs over the kernel's exponent range and on pairs whose quotient lies
     next to a rounding midpoint (the hard cases of correct rounding).
@@ -18,17 +18,16 @@ SRC = r"""
 #include <stdint.h>
 #include <string.h>
 static double div3(double x) {
-    const double y = 1.0 / 3.0;
-    const double q = x * y;
-    const double r = fma(-q, 3.0, x);
-    return fma(r, y, q);
+    const double yh = 1.0 / 3.0;
+    const double yl = 0x1.5555555555555p-56;  /* RN(1/3 - yh) */
+    return fma(x, yh, x * yl);
 }
-/* number of x with div3(x) != x / 3.0 (bitwise; a zero may come out as +0) */
+/* number of x with div3(x) != x / 3.0 (bitwise, signed zeros included) */
 int64_t check(const double* x, int64_t n) {
     int64_t bad = 0;
     for (int64_t i = 0; i < n; ++i) {
         const double a = div3(x[i]), b = x[i] / 3.0;
-        if (x[i] == 0.0 ? a != 0.0 : memcmp(&a, &b, sizeof a) != 0) ++bad;
+        if (memcmp(&a, &b, sizeof a) != 0) ++bad;
     }
     return bad;
 }

@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--element-mode", default=None, help="bench element mode the counters were taken in")
     ap.add_argument("--elements", type=int, default=None, help="elements of the profiled model (bench checks it)")
     ap.add_argument("--out", default="profiles/element_pmc.json")
+    ap.add_argument("--round", default=None, help="round / tree label recorded in the file")
     a = ap.parse_args()
     fac = calib_factors(a.calib_fetch, a.calib_write)
     fr, fw = fac.get("read 8B/lane"), fac.get("write 8B/lane")
@@ -110,6 +111,7 @@ def main():
     avg_ms, kname, n_kt = trace_avg_ms(a.kt, a.kt_steps)
     res = {
         "kernel": kname,
+        "round": a.round,
         "element_mode": a.element_mode,
         "elements": a.elements,
         "calibration_counter_bytes_per_byte": fac,

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Kernel-trace summary of bench.py's deletion window.
+
+`tools/gpu_r6.sh window` runs `bench.py --deletion-window 1 --compare-fused 0 --breakdown 0
+--cpu-baseline 0` under `rocprofv3 --kernel-trace`. Nothing runs after the window, so the last
+2 x steps element dispatches (k_element_pipe, any instantiation) are the window in the headline mode
+then in the other mode (bench.deletion_window), and the `steps` element dispatches before them are
+the last steps of the run-up (steps 7921-7940: the same bar just before its first deletion, no
+deletion yet). Prints one JSON object: per mode the element kernel's duration per window step (so the
+deletion steps show), their mean against the run-up's, and the nodal/BC time per step."""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def rows(d):
+    fs = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not fs:
+        raise SystemExit(f"no kernel_trace.csv under {d}")
+    out = []
+    for f in fs:
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    out.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return out
+
+
+def dur_ms(r):
+    return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kt", required=True)
+    ap.add_argument("--log", required=True, help="bench output (its JSON line carries config.deletion_window)")
+    a = ap.parse_args()
+    line = json.loads([l for l in open(a.log) if l.startswith("{")][-1])
+    win = line["config"]["deletion_window"]
+    steps, first = win["steps"], win["first_step"]
+    head = line["config"]["element_mode"]
+    modes = [head, "exact" if head == "fused" else "fused"]
+    rs = rows(a.kt)
+    el_idx = [i for i, r in enumerate(rs) if "k_element_pipe<" in r["Kernel_Name"]]
+    if len(el_idx) < 3 * steps:
+        raise SystemExit("too few element dispatches in the trace")
+    groups = {"run_up": el_idx[-3 * steps:-2 * steps], modes[0]: el_idx[-2 * steps:-steps], modes[1]: el_idx[-steps:]}
+    out = {"source": "rocprofv3 --kernel-trace of bench.py --deletion-window 1 (tools/gpu_r6.sh window)",
+           "window_first_step": first, "steps": steps, "bench_deletion_window": win}
+    for name, idx in groups.items():
+        el = [dur_ms(rs[i]) for i in idx]
+        # the nodal / BC kernels of a step run before its element kernel (k_nodal -> k_bc -> element)
+        other = []
+        for j, i in enumerate(idx):
+            lo = idx[j - 1] + 1 if j > 0 else i
+            other.append(sum(dur_ms(rs[k]) for k in range(lo, i)) if j > 0 else None)
+        step0 = first - steps if name == "run_up" else first
+        out[name] = {"steps": [step0, step0 + steps - 1],
+                     "element_ms_per_step": [round(x, 4) for x in el],
+                     "element_mean_ms": round(statistics.mean(el), 4),
+                     "element_median_ms": round(statistics.median(el), 4),
+                     "element_max_ms": round(max(el), 4),
+                     "step_of_max": step0 + el.index(max(el)),
+                     "nodal_bc_mean_ms": round(statistics.mean([x for x in other if x is not None]), 4),
+                     "instantiations": sorted({rs[i]["Kernel_Name"].split("(")[0] for i in idx})}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
