@@ -1040,10 +1040,7 @@ __device__ __forceinline__ void own_pass(const ElemArgs& a, int4 en, long long s
 // before computing batch b, so HBM latency hides under the FP64 work even at 2 waves per SIMD.
 // Material tables are staged in LDS (segment searches hit LDS, not L2).
 template <bool DO_DELETE, bool STORE_TRIAX, bool ANY_PLASTIC, bool LDS_MATS, int NT, bool EXACT, int OS = 0>
-#ifndef HK_EXACT_MINB
-#define HK_EXACT_MINB 2
-#endif
-__global__ __launch_bounds__(kBlock, EXACT ? HK_EXACT_MINB : 2) void k_element_pipe(ElemArgs a) {
+__global__ __launch_bounds__(kBlock, 2) void k_element_pipe(ElemArgs a) {
     constexpr bool OWN = OS > 0;                 // owner-computed assembly, OS batches per super-batch
     constexpr int kOwnFe = OS * kEPB * kFeStride;  // staged forces per pass (doubles)
     __shared__ __attribute__((aligned(16))) double s_nd[kEPB * kLdsStride];

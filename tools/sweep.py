@@ -45,7 +45,7 @@ sv.sync()
 t = a.preload + 1
 res = {n: {"el": [], "nd": [], "step": []} for n, _ in variants}
 DEFAULTS = {"elem_exact": 0, "fuse_bc": 1, "elem_pipe_blocks": 512, "elem_pipe_min": 2, "elem_gp_nt": 1,
-            "own_assembly": 1}
+            "own_assembly": 1, "own_pass_batches": 0}
 for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
@@ -66,6 +66,8 @@ for r in range(a.rounds):
         dt = time.perf_counter() - t0
         t += a.steps
         res[name]["step"].append(dt / a.steps * 1e3)
+        print(f"round {r} {name:10s} element {el[0] / a.steps:.4f} nodal {nd[0] / a.steps:.4f} step {dt / a.steps * 1e3:.4f} "
+              f"superbatch {sv.stat('own_superbatch')}", flush=True)
         res[name]["own"] = {k: sv.stat(k) for k in ("own_steps", "own_rows", "own_entries", "own_banded", "own_grid", "own_round2", "own_superbatch", "own_slots")}
 for name, d in res.items():
     print(f"{name:10s} element {statistics.median(d['el']):.4f} ms/step (min {min(d['el']):.4f})  "
