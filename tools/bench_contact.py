@@ -107,13 +107,17 @@ def group(a):
     for sv in svs:
         sv.sync()
         sv.profile(True)
+    # exchange blocks are sized from recent counts; a burst past a capacity reruns the poisoned step
+    # and the rest of the call (hakai_stat "exchange_retries"): counted across the timed window
+    retries0 = [sv.stat("exchange_retries") for sv in svs]
     ts = time.perf_counter()
     step_group(svs, 1 + a.preload, a.steps)
     for sv in svs:
         sv.sync()
     el = time.perf_counter() - ts
+    retries1 = [sv.stat("exchange_retries") for sv in svs]
     ranks = []
-    for sv, (loc, *_) in zip(svs, parts):
+    for r, (sv, (loc, *_)) in enumerate(zip(svs, parts)):
         k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
                                                 (K_CONTACT, "contact"), (K_CONTACT_SUM, "contact_sum"),
                                                 (K_EXCHANGE, "exchange"))}
@@ -121,6 +125,7 @@ def group(a):
         per = {n: round(v[0] / (a.steps if n == "contact" else max(v[1], 1)), 4) for n, v in k.items() if v[1]}
         ranks.append({"elements": loc.nElement, "nodes": loc.nNode, "kernel_ms_per_step": per,
                       "contact_total_ms_per_step": round(per.get("contact", 0) + per.get("contact_sum", 0), 4),
+                      "exchange_retries_in_timed_window": retries1[r] - retries0[r],
                       "contact_stats_last_step": sv.contact_stats()})
     out = {"workload": f"{m.name} two-body impact, scale 1/{a.scale}, {a.ranks} ranks on ONE GPU (in-process group), "
                        f"owner-computed search, group_serial={a.serial}",

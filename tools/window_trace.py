@@ -3,8 +3,9 @@
 
 `tools/gpu_r6.sh window` runs `bench.py --deletion-window 1 --compare-fused 0 --breakdown 0
 --cpu-baseline 0` under `rocprofv3 --kernel-trace`. Nothing runs after the window, so the last
-2 x steps element dispatches (k_element_pipe, any instantiation) are the window in the headline mode
-then in the other mode (bench.deletion_window), and the `steps` element dispatches before them are
+2 x steps + 2 element dispatches (k_element_pipe, any instantiation) are, per mode, one untimed
+planning step and the window (headline mode, then the other; bench.deletion_window), and the `steps`
+element dispatches before them are
 the last steps of the run-up (steps 7921-7940: the same bar just before its first deletion, no
 deletion yet). Prints one JSON object: per mode the element kernel's duration per window step (so the
 deletion steps show), their mean against the run-up's, and the nodal/BC time per step."""
@@ -44,9 +45,12 @@ def main():
     modes = [head, "exact" if head == "fused" else "fused"]
     rs = rows(a.kt)
     el_idx = [i for i, r in enumerate(rs) if "k_element_pipe<" in r["Kernel_Name"]]
-    if len(el_idx) < 3 * steps:
+    if len(el_idx) < 3 * steps + 2:
         raise SystemExit("too few element dispatches in the trace")
-    groups = {"run_up": el_idx[-3 * steps:-2 * steps], modes[0]: el_idx[-2 * steps:-steps], modes[1]: el_idx[-steps:]}
+    # per mode: one untimed planning step from the hand-off state, then the timed window
+    # (bench.deletion_window), so the dispatch order is run-up, warm, headline window, warm, other window
+    groups = {"run_up": el_idx[-3 * steps - 2:-2 * steps - 2], modes[0]: el_idx[-2 * steps - 1:-steps - 1],
+              modes[1]: el_idx[-steps:]}
     out = {"source": "rocprofv3 --kernel-trace of bench.py --deletion-window 1 (tools/gpu_r6.sh window)",
            "window_first_step": first, "steps": steps, "bench_deletion_window": win}
     for name, idx in groups.items():
@@ -55,7 +59,8 @@ def main():
         other = []
         for j, i in enumerate(idx):
             lo = idx[j - 1] + 1 if j > 0 else i
-            other.append(sum(dur_ms(rs[k]) for k in range(lo, i)) if j > 0 else None)
+            other.append(sum(dur_ms(rs[k]) for k in range(lo, i)
+                             if "k_nodal" in rs[k]["Kernel_Name"] or "k_bc" in rs[k]["Kernel_Name"]) if j > 0 else None)
         step0 = first - steps if name == "run_up" else first
         out[name] = {"steps": [step0, step0 + steps - 1],
                      "element_ms_per_step": [round(x, 4) for x in el],
