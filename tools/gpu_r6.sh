@@ -109,6 +109,35 @@ for st in "$@"; do
             --deletion-window 1 || exit $?
         python tools/window_trace.py --kt $P --log $P.log > gpurun_out/r6_window_summary.json || exit $?
         cat gpurun_out/r6_window_summary.json ;;
+    winab) : > gpurun_out/r6_winab.jsonl  # LIBS="a cur": bench lines (idle + deletion window, both modes) alternating
+        for i in 1 2; do
+            for v in ${LIBS:-base cur}; do
+                if [ $v = cur ]; then lib=hakai-fem_amd/lib/libhakai_hip.so; else lib=hakai-fem_amd/lib/variants/$v.so; fi
+                HAKAI_LIB=$lib run 400 gpurun_out/r6_winab_cur.log python bench.py --steps 100 --warmup 10 \
+                    --cpu-baseline 0 --breakdown 0 || exit $?
+                python - "$v" "$i" gpurun_out/r6_winab_cur.log >> gpurun_out/r6_winab.jsonl <<'EOP'
+import json, sys
+d = json.loads([l for l in open(sys.argv[3]) if l.startswith("{")][-1])
+c = d["config"]; o = c.get("other_mode") or {}; w = c.get("deletion_window") or {}
+print(json.dumps({"lib": sys.argv[1], "run": int(sys.argv[2]), "fused_element_ms": d["roofline"]["avg_launch_ms"],
+                  "fused_ms_per_step": d["ms_per_step"], "exact_element_ms": o.get("element_avg_ms"),
+                  "exact_ms_per_step": o.get("ms_per_step"),
+                  "window_fused": {k: w.get("fused", {}).get(k) for k in ("ms_per_step", "element_avg_ms", "deletions")},
+                  "window_exact": {k: w.get("exact", {}).get(k) for k in ("ms_per_step", "element_avg_ms", "deletions")}}))
+EOP
+            done
+        done
+        cat gpurun_out/r6_winab.jsonl ;;
+    windowsq) P=gpurun_out/r6_windowsq; rm -rf $P  # SQ / fetch counters per dispatch over the deletion window
+        HAKAI_GRAPH=0 run 900 $P.log timeout -s KILL 800 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU \
+            SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $P/sq -o run \
+            --output-format csv -- python bench.py --steps 20 --warmup 2 --cpu-baseline 0 --breakdown 0 \
+            --compare-fused 0 --deletion-window 1 || exit $?
+        HAKAI_GRAPH=0 run 900 $P.fetch.log timeout -s KILL 800 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run \
+            --output-format csv -- python bench.py --steps 20 --warmup 2 --cpu-baseline 0 --breakdown 0 \
+            --compare-fused 0 --deletion-window 1 || exit $?
+        python tools/window_counters.py --dirs $P/sq $P/fetch --steps 20 > gpurun_out/r6_windowsq_summary.json || exit $?
+        cat gpurun_out/r6_windowsq_summary.json ;;
     pmcwide) for w in c5 c4; do  # HBM bytes per launch on the wide sections: C5 16 M (--strong, N = 1), C4
             if [ $w = c5 ]; then CMD="python bench.py --strong --steps 10 --warmup 2 $BA --compare-fused 0"
             else CMD="python tools/sweep.py --config c4 --rounds 1 --steps 10 --variants fused:elem_exact=0"; fi
