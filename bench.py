@@ -527,6 +527,26 @@ def deletion_window(g, t, exact, steps):
         if mode_exact:
             end_exact, dels_exact = st, sorted(dels)
     g.set("elem_exact", int(exact))
+    # what the element kernel's ductile test meets in the window: Gauss points (and waves of 8
+    # elements = 64 Gauss points) at or above du_skip, where the wave-uniform skip of the deletion
+    # test no longer applies (hakai_capi.cpp build_devmat: du_floor = the smallest fracture strain
+    # less a relative 2^-40, du_skip = du_floor (1 - 2^-40)), at the hand-off and at the window's end;
+    # and the Gauss points that yielded during the window (eqps grew)
+    tab = sv.model.materials[0].ductile
+    if tab is not None and len(tab):
+        lo, hi = float(np.min(tab[:, 0])), float(np.max(tab[:, 0]))
+        du_floor = lo - (abs(hi) + abs(lo)) * 2.0 ** -40
+        du_skip = du_floor - du_floor * 2.0 ** -40
+        ep0, ep1 = s0.integ_eq_plastic_strain, end_exact.integ_eq_plastic_strain
+        nw = ep0.size // 64
+        out["ductile_test_load"] = {
+            "du_skip": du_skip,
+            "gp_frac_at_or_above_du_skip": [round(float(np.mean(e >= du_skip)), 6) for e in (ep0, ep1)],
+            "waves_running_the_test_frac": [round(float(np.mean((e[:64 * nw].reshape(nw, 64) >= du_skip).any(axis=1))), 6)
+                                            for e in (ep0, ep1)],
+            "gp_frac_yielding_in_window": round(float(np.mean(ep1 > ep0)), 4),
+            "eqps_max": [round(float(e.max()), 4) for e in (ep0, ep1)],
+            "at": [w0 - 1, w0 + steps - 1]}
     f, x = out["fused"], out["exact"]
     out["same_deletions_both_modes"] = (f["deletions"] == x["deletions"]
                                         and f["deletion_steps"] == x["deletion_steps"])
