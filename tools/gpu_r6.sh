@@ -138,6 +138,11 @@ EOP
             --compare-fused 0 --deletion-window 1 || exit $?
         python tools/window_counters.py --dirs $P/sq $P/fetch --steps 20 > gpurun_out/r6_windowsq_summary.json || exit $?
         cat gpurun_out/r6_windowsq_summary.json ;;
+    wcontrol) P=gpurun_out/r6_wcontrol; rm -rf $P  # the window's hand-off sequence in the idle regime (step 441)
+        HAKAI_GRAPH=0 run 600 $P.log rocprofv3 --kernel-trace --stats -d $P -o run --output-format csv -- \
+            python tools/window_control.py --first ${FIRST:-441} || exit $?
+        python tools/window_trace.py --kt $P --first ${FIRST:-441} > gpurun_out/r6_wcontrol_summary.json || exit $?
+        cat gpurun_out/r6_wcontrol_summary.json ;;
     pmcwide) for w in c5 c4; do  # HBM bytes per launch on the wide sections: C5 16 M (--strong, N = 1), C4
             if [ $w = c5 ]; then CMD="python bench.py --strong --steps 10 --warmup 2 $BA --compare-fused 0"
             else CMD="python tools/sweep.py --config c4 --rounds 1 --steps 10 --variants fused:elem_exact=0"; fi

@@ -36,21 +36,40 @@ def dur_ms(r):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kt", required=True)
-    ap.add_argument("--log", required=True, help="bench output (its JSON line carries config.deletion_window)")
+    ap.add_argument("--log", default=None, help="bench output (its JSON line carries config.deletion_window)")
+    ap.add_argument("--first", type=int, default=0, help="without --log (tools/window_control.py): first window step")
+    ap.add_argument("--steps", type=int, default=20)
     a = ap.parse_args()
-    line = json.loads([l for l in open(a.log) if l.startswith("{")][-1])
-    win = line["config"]["deletion_window"]
-    steps, first = win["steps"], win["first_step"]
-    head = line["config"]["element_mode"]
+    if a.log:
+        line = json.loads([l for l in open(a.log) if l.startswith("{")][-1])
+        win = line["config"]["deletion_window"]
+        steps, first = win["steps"], win["first_step"]
+        head = line["config"]["element_mode"]
+    else:  # the control sequence: fused, then reference order
+        win, steps, first, head = None, a.steps, a.first, "fused"
     modes = [head, "exact" if head == "fused" else "fused"]
     rs = rows(a.kt)
     el_idx = [i for i, r in enumerate(rs) if "k_element_pipe<" in r["Kernel_Name"]]
-    if len(el_idx) < 3 * steps + 2:
-        raise SystemExit("too few element dispatches in the trace")
-    # per mode: one untimed planning step from the hand-off state, then the timed window
-    # (bench.deletion_window), so the dispatch order is run-up, warm, headline window, warm, other window
-    groups = {"run_up": el_idx[-3 * steps - 2:-2 * steps - 2], modes[0]: el_idx[-2 * steps - 1:-steps - 1],
-              modes[1]: el_idx[-steps:]}
+    warm = win.get("warm_steps_per_mode") if win else None
+    if warm:
+        # bench.deletion_window (round 6): headline run on to the hand-off, 'warm' more steps (the
+        # checker's start), then per mode 'warm' untimed steps from the hand-off and the timed window,
+        # then the checked reference-order run from the checker's start (after an upload)
+        n = steps
+        if len(el_idx) < 2 * n + 2 * (warm + n) + warm:
+            raise SystemExit("too few element dispatches in the trace")
+        k_other = len(el_idx) - n - n              # other mode's timed window
+        k_head = k_other - warm - n                # headline's timed window
+        k_cont = k_head - warm - warm              # continuation after the hand-off
+        groups = {"run_up": el_idx[k_cont + warm - n:k_cont + warm], modes[0]: el_idx[k_head:k_head + n],
+                  modes[1]: el_idx[k_other:k_other + n], "checked_run_after_upload": el_idx[-n:]}
+    else:
+        if len(el_idx) < 3 * steps + 2:
+            raise SystemExit("too few element dispatches in the trace")
+        # one untimed planning step per mode from the hand-off state, then the timed window (round-6
+        # first protocol, and tools/window_control.py): run-up, warm, headline window, warm, other window
+        groups = {"run_up": el_idx[-3 * steps - 2:-2 * steps - 2], modes[0]: el_idx[-2 * steps - 1:-steps - 1],
+                  modes[1]: el_idx[-steps:]}
     out = {"source": "rocprofv3 --kernel-trace of bench.py --deletion-window 1 (tools/gpu_r6.sh window)",
            "window_first_step": first, "steps": steps, "bench_deletion_window": win}
     for name, idx in groups.items():
