@@ -24,6 +24,9 @@ ap.add_argument("--preload", type=int, default=400)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--variants", default="simple:elem_pipe_blocks=0;pipe512:elem_pipe_blocks=512")
+ap.add_argument("--settle", type=int, default=30,
+                help="untimed steps after each variant's settings (a re-plan idles the GPU, and the steps after "
+                     "an idle gap run slow for ~20 steps: profiles/r06_window_control_trace.json)")
 a = ap.parse_args()
 
 variants = []
@@ -50,6 +53,9 @@ for r in range(a.rounds):
     for name, settings in variants:
         for k, v in {**DEFAULTS, **dict(settings)}.items():  # every variant from the same baseline
             sv.set_tuning(k, v)
+        if a.settle:
+            sv.step(t, a.settle)
+            t += a.settle
         sv.profile(True)
         sv.sync()
         sv.step(t, a.steps)
