@@ -128,16 +128,6 @@ EOP
             done
         done
         cat gpurun_out/r6_winab.jsonl ;;
-    windowsq) P=gpurun_out/r6_windowsq; rm -rf $P  # SQ / fetch counters per dispatch over the deletion window
-        HAKAI_GRAPH=0 run 900 $P.log timeout -s KILL 800 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU \
-            SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $P/sq -o run \
-            --output-format csv -- python bench.py --steps 20 --warmup 2 --cpu-baseline 0 --breakdown 0 \
-            --compare-fused 0 --deletion-window 1 || exit $?
-        HAKAI_GRAPH=0 run 900 $P.fetch.log timeout -s KILL 800 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run \
-            --output-format csv -- python bench.py --steps 20 --warmup 2 --cpu-baseline 0 --breakdown 0 \
-            --compare-fused 0 --deletion-window 1 || exit $?
-        python tools/window_counters.py --dirs $P/sq $P/fetch --steps 20 > gpurun_out/r6_windowsq_summary.json || exit $?
-        cat gpurun_out/r6_windowsq_summary.json ;;
     wcontrol) P=gpurun_out/r6_wcontrol; rm -rf $P  # the window's hand-off sequence in the idle regime (step 441)
         HAKAI_GRAPH=0 run 600 $P.log rocprofv3 --kernel-trace --stats -d $P -o run --output-format csv -- \
             python tools/window_control.py --first ${FIRST:-441} || exit $?
