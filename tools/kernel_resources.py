@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel resource report: VGPRs, AGPRs, SGPRs, spills, static LDS and the compiler's waves per SIMD.
 
-Compiles a HIP source for gfx950 with the Makefile's flags and `-Rpass-analysis=kernel-resource-usage`
+Compiles a HIP source for gfx950 with the Makefile's flags (its -ffp-contract per file) and `-Rpass-analysis=kernel-resource-usage`
 (the compiler's own per-kernel report, no GPU needed) and prints one JSON object. The element
 kernel's template arguments are named (`hk::k_element_pipe<DO_DELETE, STORE_TRIAX, ANY_PLASTIC,
 LDS_MATS, NT, EXACT, OS>`, csrc/hakai_kernels.hip), so the two instantiations the C3 bench times are
@@ -24,6 +24,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "hakai-fem_amd")
 FLAGS = ["--offload-arch=gfx950", "-std=c++17", "-O3", "-fPIC", "-munsafe-fp-atomics"]
+CONTRACT = {"hakai_kernels.hip": "-ffp-contract=on", "hakai_contact.hip": "-ffp-contract=off"}  # as the Makefile
 FIELDS = {"TotalSGPRs": "sgprs", "VGPRs": "vgprs", "AGPRs": "agprs", "ScratchSize [bytes/lane]": "scratch_bytes_per_lane",
           "Occupancy [waves/SIMD]": "waves_per_simd", "SGPRs Spill": "sgpr_spill", "VGPRs Spill": "vgpr_spill",
           "LDS Size [bytes/block]": "lds_static_bytes", "Dynamic Stack": "dynamic_stack"}
@@ -73,9 +74,13 @@ def describe(sym):
     return d
 
 
+def flags(src):
+    return FLAGS + ([CONTRACT[os.path.basename(src)]] if os.path.basename(src) in CONTRACT else [])
+
+
 def compile_remarks(src):
     with tempfile.TemporaryDirectory() as td:
-        p = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "-I", os.path.join(PKG, "csrc"), "-c", src,
+        p = subprocess.run(["/opt/rocm/bin/hipcc", *flags(src), "-I", os.path.join(PKG, "csrc"), "-c", src,
                             "-o", os.path.join(td, "k.o"), "-Rpass-analysis=kernel-resource-usage"],
                            capture_output=True, text=True)
     if p.returncode:
@@ -97,7 +102,7 @@ def main():
             bench[f"{r['mode']} {r['assembly']}"] = {k: r.get(k) for k in ("vgprs", "agprs", "sgprs", "vgpr_spill",
                                                                           "sgpr_spill", "scratch_bytes_per_lane",
                                                                           "lds_static_bytes", "waves_per_simd")}
-    print(json.dumps({"source": os.path.relpath(a.src, ROOT), "arch": "gfx950", "flags": FLAGS,
+    print(json.dumps({"source": os.path.relpath(a.src, ROOT), "arch": "gfx950", "flags": flags(a.src),
                       "c3_bench_instantiations": bench,
                       "lds_dynamic_note": "static __shared__ only; launch_pipe adds owner-sum slots and staged "
                                           "materials as dynamic LDS",
