@@ -29,6 +29,9 @@ def main():
                          "enqueues each phase behind a fixed sleep kernel, so it runs back to back as in a "
                          "pipelined run instead of at the host's enqueue pace")
     ap.add_argument("--tuning", default="", help="extra hakai_set_tuning keys, e.g. contact_exchange_bins=4096")
+    ap.add_argument("--profile", type=int, default=1,
+                    help="one context: 0 times the steps without the per-kernel event timers, so the steps can "
+                         "replay from hipGraphs (HAKAI_GRAPH; events keep a context in stream mode)")
     ap.add_argument("--x-slabs", type=int, default=0,
                     help="1: C4 with its elements numbered x slowest, so the rank ranges are x-slabs that "
                          "share the contact zone (the default z-slab ranges put it on two ranks)")
@@ -50,13 +53,15 @@ def main():
     pairs, sizes = sv.contact_info()
     sv.step(1, a.preload)
     sv.sync()
-    sv.profile(True)
+    sv.profile(bool(a.profile))
+    g0 = sv.stat("graph_steps")
     ts = time.perf_counter()
     sv.step(1 + a.preload, a.steps)
     sv.sync()
     el = time.perf_counter() - ts
+    graph_steps = sv.stat("graph_steps") - g0
     k = {n: sv.profile_read(i) for i, n in ((K_ELEMENT, "element"), (K_NODAL, "nodal"), (K_BC, "bc"),
-                                            (K_CONTACT, "contact"))}
+                                            (K_CONTACT, "contact"))} if a.profile else {}
     cstats = sv.contact_stats()
     dl = sv.deleted()
     t_lo, t_hi = 1 + a.preload, a.preload + a.steps
@@ -70,6 +75,7 @@ def main():
         "pairs": pairs, "element_size": sizes, "steps": a.steps, "preload": a.preload,
         "value_M_element_updates_per_s": round(n_active * a.steps / el / 1e6, 3),
         "ms_per_step": round(el / a.steps * 1e3, 4),
+        "timed_steps_from_graphs": int(graph_steps),
         "kernel_ms_per_step": {n: round(v[0] / max(v[1], 1), 4) for n, v in k.items() if v[1]},
         "deleted_elements": int(len(dl)),
         "timed_steps_with_deletions": sum(1 for x in del_steps if t_lo <= x <= t_hi),

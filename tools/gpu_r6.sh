@@ -19,6 +19,7 @@
 #              -> gpurun_out/r6_window/ + gpurun_out/r6_window_summary.json (tools/window_trace.py)
 #   ablib      LIBS="a b cur" alternating libraries (hakai-fem_amd/lib/variants/<a>.so) under tools/sweep.py
 #   contact    tools/bench_contact.py on C4: one context, 2/4 ranks with z- and x-slab ranges -> r6_contact_c4.jsonl
+#   cgraph     C4 one context without event timers, HAKAI_GRAPH=16 vs 0 alternating -> gpurun_out/r6_cgraph.jsonl
 #   pmcwide    FETCH_SIZE / WRITE_SIZE passes + kernel trace on C5 16 M and C4 -> gpurun_out/r6_pmc_{c5,c4}.json
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r6_tests.log
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
@@ -74,6 +75,16 @@ for st in "$@"; do
                 --serial 2 --steps 40 || exit $?
             grep '^{' gpurun_out/r6_contact_cur.log >> gpurun_out/r6_contact_c4.jsonl
         done ;;
+    cgraph) : > gpurun_out/r6_cgraph.jsonl  # C4 one context, no event timers: steps from 16-step graphs vs stream mode
+        for i in 1 2; do
+            for g in 16 0; do
+                HAKAI_GRAPH=$g run 600 gpurun_out/r6_cgraph_cur.log python tools/bench_contact.py --profile 0 \
+                    --steps 64 || exit $?
+                grep '^{' gpurun_out/r6_cgraph_cur.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); \
+d.pop('contact_stats_last_step',None); d['HAKAI_GRAPH']=$g; print(json.dumps(d))" >> gpurun_out/r6_cgraph.jsonl || exit $?
+            done
+        done
+        cat gpurun_out/r6_cgraph.jsonl ;;
     rehearse4) HAKAI_RCCL_SHARED_GPU=1 run 900 gpurun_out/r6_rehearse4.json python bench.py --gpus 4 \
                    --steps 20 --warmup 5 --c5-steps 10 || exit $? ;;
     rehearse8) t0=$(date +%s.%N)
