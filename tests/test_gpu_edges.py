@@ -133,3 +133,72 @@ def test_reupload_larger_model_without_bc():
         sv.step(1, 50)
         r = sv.download(disp=True)
     assert np.array_equal(g.disp, r.disp)
+
+
+def _exact_state_equal(g, s):
+    from util import STATE, bitwise_equal
+    for k in STATE:
+        assert bitwise_equal(getattr(g, k), s[k]), k
+
+
+@pytest.mark.parametrize("exact", [1, 0])
+def test_single_element_bar(exact):
+    """The smallest mesh: one hex (8 nodes, one batch slot of 64 lanes mostly empty), plastic flow
+    under the stretch field. Reference order: bit-identical to the oracle; fused: within 1e-9."""
+    m = small_bar(1, 1, 1, v_end=2e5, n_steps=300)
+    assert m.nElement == 1 and m.nNode == 8
+    o = O.Oracle(m)
+    o.run(1, 300)
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", exact)
+        sv.step(1, 300)
+        g = sv.download()
+    assert np.any(o.s["integ_eq_plastic_strain"] > 0) and np.all(np.isfinite(o.s["disp"]))
+    if exact:
+        _exact_state_equal(g, o.s)
+    else:
+        assert rel_err(g.disp, o.s["disp"]) < 1e-9
+        assert rel_err(g.integ_stress, o.s["integ_stress"]) < 1e-9
+
+
+def test_zero_steps_is_a_no_op():
+    """hakai_step with n_steps = 0 returns success and leaves every state array as it was; the
+    run then continues bit-identically to one that never made the empty call."""
+    m = small_bar(3, 2, 6, v_end=2e5, n_steps=200)
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", 1)
+        sv.step(1, 100)
+        a = sv.download()
+        sv.step(101, 0)
+        b = sv.download()
+        for k in ("disp", "disp_pre", "velo", "integ_stress", "integ_strain", "integ_eq_plastic_strain",
+                  "integ_yield_stress", "element_flag"):
+            assert np.array_equal(getattr(a, k), getattr(b, k)), k
+        sv.step(101, 100)
+        c = sv.download()
+    o = O.Oracle(m)
+    o.run(1, 200)
+    _exact_state_equal(c, o.s)
+
+
+def test_every_element_deleted():
+    """A state whose elements are all deleted (element_flag 0 everywhere, uploaded mid-run): no
+    element contributes force or changes its state, no deletion is logged again, and the nodes
+    run on under their own momentum and the BCs -- bit-identical to the oracle."""
+    m = small_bar(3, 2, 6, v_end=2e5, n_steps=200)
+    o = O.Oracle(m)
+    o.run(1, 100)
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", 1)
+        sv.step(1, 100)
+        g = sv.download()
+        g.element_flag[:] = 0
+        sv.upload(g)
+        sv.step(101, 100)
+        r = sv.download()
+        dels = sv.deleted()
+    o.s["element_flag"][:] = 0
+    o.run(101, 100)
+    assert all(int(d[0]) <= 100 for d in dels) and all(d[0] <= 100 for d in o.deletions)
+    _exact_state_equal(r, o.s)
+    assert not np.array_equal(r.disp, g.disp)
