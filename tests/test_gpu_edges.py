@@ -202,3 +202,52 @@ def test_every_element_deleted():
     assert all(int(d[0]) <= 100 for d in dels) and all(d[0] <= 100 for d in o.deletions)
     _exact_state_equal(r, o.s)
     assert not np.array_equal(r.disp, g.disp)
+
+
+def _many_materials_deck():
+    """fast_deletion_bar with 11 materials cycled over the elements: ten scaled steel_Ductile
+    variants and one with the largest tables the ABI takes (64 plastic rows, 32 ductile rows).
+    11 > kMaxLdsMats (8), so the element kernel reads the material tables from global memory."""
+    from hakai import mesh
+    from hakai.model import Material
+    from util import fast_deletion_bar
+    base = fast_deletion_bar(3, 3, 10)
+    mats = []
+    for i in range(10):
+        pl = mesh.STEEL_PLASTIC.copy()
+        pl[:, 0] *= 1 + 0.03 * i
+        du = mesh.STEEL_DUCTILE.copy()
+        du[:, 0] *= 1 + 0.05 * i
+        mats.append(Material(f"m{i}", 7.8e-9, 210000 * (1 + 0.05 * i), 0.3 - 0.01 * i, pl, du))
+    eps = np.linspace(0, 4, 64)
+    tri = np.linspace(-0.3, 2.0, 32)
+    mats.append(Material("largest_tables", 7.8e-9, 200000., 0.29,
+                         np.stack([700 + 400 * (1 - np.exp(-5 * eps)), eps], 1),
+                         np.stack([1.0 - 0.35 * (tri + 0.3) / 2.3, tri, np.full(32, 30.)], 1)))
+    em = (np.arange(base.nElement) % len(mats) + 1).astype(np.int64)
+    m = Model(base.coordmat.copy(), base.elementmat.copy(), em, mats, bc=base.bc, ic_dofs=base.ic_dofs,
+              ic_values=base.ic_values, d_time=base.d_time, end_time=base.end_time, name="many_materials")
+    return m
+
+
+@pytest.mark.parametrize("exact", [1, 0])
+def test_many_materials_largest_tables(exact):
+    """More materials than the LDS stages and the largest plastic / ductile tables, with
+    deletions in several materials (the largest-table one included): reference order bit-identical
+    to the oracle, fused within 1e-6 with the same deletions."""
+    m = _many_materials_deck()
+    o = O.Oracle(m)
+    o.run(1, m.n_steps)
+    deleted_mats = {int(m.element_material[int(e) - 1]) for _, e in o.deletions}
+    assert len(deleted_mats) >= 3 and len(m.materials) in deleted_mats
+    with Solver(m) as sv:
+        sv.set_tuning("elem_exact", exact)
+        sv.step(1, m.n_steps)
+        g = sv.download()
+        dels = [tuple(int(v) for v in x) for x in sv.deleted()]
+    assert dels == sorted(tuple(int(v) for v in d) for d in o.deletions)
+    if exact:
+        _exact_state_equal(g, o.s)
+    else:
+        assert rel_err(g.disp, o.s["disp"]) < 1e-6
+        assert rel_err(g.integ_stress, o.s["integ_stress"]) < 1e-6
