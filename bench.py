@@ -744,7 +744,11 @@ def main():
     win, win_s0, win_end = None, None, None
     if (a.deletion_window and nparts == 1 and not a.strong and not multi and cfg["workload"].startswith("C3")
             and built[0][0].nElement == 2_000_000):
-        win, win_s0, win_end = deletion_window(g, t, exact, DEL_WINDOW_STEPS)
+        try:  # after the headline's timed region: a failure here is reported, never fatal for its line
+            win, win_s0, win_end = deletion_window(g, t, exact, DEL_WINDOW_STEPS)
+        except Exception as e:
+            win, win_s0, win_end = None, None, None
+            extra["deletion_window"] = {"error": str(e)}
         if win is not None:
             extra["deletion_window"] = win
     if nparts > 1:
