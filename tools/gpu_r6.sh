@@ -68,6 +68,17 @@ for st in "$@"; do
             done
         done
         grep -E "^==|element" gpurun_out/r6_ablib.log ;;
+    envab) : > gpurun_out/r6_envab.log  # ENVV=NAME VALS="a b": the product library under alternating env values
+        for i in 1 2 3; do
+            for v in ${VALS:-0 1}; do
+                echo "== ${ENVV}=$v $i" >> gpurun_out/r6_envab.log
+                env ${ENVV}=$v timeout -k 10 300 python tools/sweep.py --config ${CONFIG:-c3} --rounds 2 \
+                    --variants "${SWEEP:-exact:elem_exact=1;fused:elem_exact=0}" > gpurun_out/r6_envab_cur.log 2>&1 || \
+                    { tail -n 20 gpurun_out/r6_envab_cur.log; exit 1; }
+                cat gpurun_out/r6_envab_cur.log >> gpurun_out/r6_envab.log
+            done
+        done
+        grep -E "^==|element" gpurun_out/r6_envab.log ;;
     contact) : > gpurun_out/r6_contact_c4.jsonl  # C4 contact per rank: one context, 2 and 4 ranks (z- and x-slabs)
         for spec in "1 0" "2 0" "4 0" "2 1" "4 1"; do
             set -- $spec
