@@ -19,6 +19,7 @@
 #              -> gpurun_out/r6_window/ + gpurun_out/r6_window_summary.json (tools/window_trace.py)
 #   ablib      LIBS="a b cur" alternating libraries (hakai-fem_amd/lib/variants/<a>.so) under tools/sweep.py
 #   contact    tools/bench_contact.py on C4: one context, 2/4 ranks with z- and x-slab ranges -> r6_contact_c4.jsonl
+#   envab      ENVV=NAME VALS="0 1": the product library under alternating env values (tools/sweep.py) -> r6_envab.log
 #   cgraph     C4 one context without event timers, HAKAI_GRAPH=16 vs 0 alternating -> gpurun_out/r6_cgraph.jsonl
 #   pmcwide    FETCH_SIZE / WRITE_SIZE passes + kernel trace on C5 16 M and C4 -> gpurun_out/r6_pmc_{c5,c4}.json
 #   tests:<pytest -k expr>  a subset of the GPU suite      -> gpurun_out/r6_tests.log
