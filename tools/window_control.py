@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Control for bench.py's deletion window: the same hand-off sequence far from any deletion.
 
-bench.deletion_window runs C3 to step 7940, downloads the state, and per element mode uploads it,
-runs one untimed step, uploads it again and times 20 steps. Under rocprofv3 --kernel-trace
-(tools/gpu_r6.sh wcontrol) this script repeats exactly that sequence at step --first (default 441,
-the idle regime where no Gauss point is near the ductile table), so the per-step element times of the
-two windows can be compared: a hump that shows up here too comes from the hand-off itself (the GPU
-idle while the state crosses PCIe), not from the deletion regime."""
+The first version of bench.deletion_window (round 6) ran C3 to step 7940, downloaded the state, and
+per element mode uploaded it, ran one untimed step, uploaded it again and timed 20 steps. Under
+rocprofv3 --kernel-trace (tools/gpu_r6.sh wcontrol) this script repeats exactly that sequence at step
+--first (default 441, the idle regime where no Gauss point is near the ductile table), so the per-step
+element times of the two windows can be compared: the hump that showed up here too came from the
+hand-off itself (the GPU idle while the state crosses PCIe), not from the deletion regime
+(profiles/r06_window_control_trace.json). bench.py now runs 100 untimed steps per mode after the
+hand-off instead."""
 import argparse
 import os
 import sys
